@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by IMPORTING THE REFERENCE (never copied) — runs only in the build
+container, where /root/reference exists.  Writes small .npz fixtures into tests/golden/.
+
+The reference is imported from /root/reference/adaptive_nerf (PYTHONPATH style of
+mediator.py:112-113).  Three modules it imports at top level but never calls on the
+stratified/vanilla path are absent from the image and are stubbed in
+sys.modules for the import only: ``nerfacc`` (ray_rendering.py:9, used only by the occupancy
+renderer), ``jaxtyping`` (scene_box.py:3, a type annotation), ``viser.transforms``
+(scene_box.py:7, used only by OrientedBox).  No reference code runs through a stub.
+
+MetaNeRF's (x,d,params)->dict forward is wrapped in a 6-line adapter to the container
+contract expert(x_d (M,6), params) -> (M,4) (SURVEY.md §0 defect 2).
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py
+"""
+import os
+import sys
+import types
+from collections import OrderedDict
+from types import SimpleNamespace
+
+import numpy as np
+import torch
+
+REF = "/root/reference/adaptive_nerf"
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden")
+
+
+def _install_stubs():
+    nerfacc = types.ModuleType("nerfacc")
+    nerfacc.OccGridEstimator = object
+    jax = types.ModuleType("jaxtyping")
+
+    class _Sub:
+        def __class_getitem__(cls, item):
+            return torch.Tensor
+
+    jax.Float = _Sub
+    viser = types.ModuleType("viser")
+    vtf = types.ModuleType("viser.transforms")
+    viser.transforms = vtf
+    for name, mod in (("nerfacc", nerfacc), ("jaxtyping", jax), ("viser", viser), ("viser.transforms", vtf)):
+        sys.modules.setdefault(name, mod)
+
+
+def main():
+    if not os.path.isdir(REF):
+        print("reference absent; nothing to do")
+        return
+    sys.dont_write_bytecode = True
+    _install_stubs()
+    sys.path.insert(0, REF)
+    torch.set_num_threads(8)
+    from nerfs import ray_rendering as rr          # noqa: E402
+    from nerfs import ray_sampling as rs           # noqa: E402
+    from nerfs.scene_box import SceneBox           # noqa: E402
+    from nerfs.losses import compute_mse_loss     # noqa: E402
+    from models.encodings import FrequencyEncoder  # noqa: E402
+    from models.inr.meta_vanilla import MetaNeRF   # noqa: E402
+    from models.trunc_exp import trunc_exp         # noqa: E402
+
+    os.makedirs(OUT, exist_ok=True)
+    g = torch.Generator().manual_seed(1234)
+
+    # ---------------------------------------------------------------- frequency encoder
+    x = (torch.rand(512, 3, generator=g) * 12 - 6)
+    d = torch.nn.functional.normalize(torch.randn(512, 3, generator=g), dim=-1)
+    fx = FrequencyEncoder(3, 10, include_input=True, use_pi=False)
+    fd = FrequencyEncoder(3, 4, include_input=True, use_pi=False)
+    f2 = FrequencyEncoder(3, 2, include_input=True, use_pi=False)
+    np.savez_compressed(os.path.join(OUT, "freq.npz"), x=x.numpy(), enc_x=fx(x).numpy(), d=d.numpy(),
+                        enc_d=fd(d).numpy(), small_in=np.array([[0.1, 0.2, 0.3]], np.float32),
+                        small_out=f2(torch.tensor([[0.1, 0.2, 0.3]])).numpy())
+
+    # ---------------------------------------------------------------- rays
+    H = W = 800
+    focal = 0.5 * W / np.tan(0.5 * 0.6911112)
+    dirs = rs.get_ray_directions(H, W, focal, focal, W / 2, H / 2, center_pixels=True, device="cpu")
+    c2w = torch.tensor([[-0.9999, 0.0042, -0.0134, -0.0538],
+                        [-0.0140, -0.2997, 0.9539, 3.8455],
+                        [0.0000, 0.9540, 0.2997, 1.2081]], dtype=torch.float32)
+    crop = dirs[350:450, 350:450]                      # C1: centre 100x100 crop
+    rays_const = rs.get_rays(crop, c2w, near=2.0, far=6.0).reshape(-1, 8)
+    box = SceneBox(aabb=torch.tensor([[-1.5, -1.5, -1.5], [1.5, 1.5, 1.5]]))
+    dirs_small = rs.get_ray_directions(24, 40, 30.0, 28.0, 19.3, 12.1, center_pixels=True, device="cpu")
+    c2w_b = torch.tensor([[0.8, 0.0, 0.6, 3.0], [0.0, 1.0, 0.0, 0.4], [-0.6, 0.0, 0.8, 3.5]])
+    rays_aabb = rs.get_rays(dirs_small, c2w_b, scene_box=box).reshape(-1, 8)
+    clamped, valid = rs.clamp_rays_near_far(rays_aabb, near_far_override=(0.5, 4.0))
+    dirs_nc = rs.get_ray_directions(7, 9, 5.0, 6.0, 4.0, 3.5, center_pixels=False, device="cpu")
+    np.savez_compressed(os.path.join(OUT, "rays.npz"), focal=np.float32(focal), c2w=c2w.numpy(),
+                        dirs_crop=crop.numpy(), rays_const=rays_const.numpy(),
+                        dirs_small=dirs_small.numpy(), c2w_b=c2w_b.numpy(), rays_aabb=rays_aabb.numpy(),
+                        clamped=clamped.numpy(), valid=valid.numpy(), dirs_nc=dirs_nc.numpy())
+
+    # ---------------------------------------------------------------- MLP (MetaNeRF, frequency dirs)
+    torch.manual_seed(0)
+    net = MetaNeRF(encoding_dir="frequency")
+
+    class Adapter(torch.nn.Module):  # expert(x_d (M,6), params) -> (M,4)
+        def __init__(self, n):
+            super().__init__(); self.net = n; self.use_occ = False; self.submodules = [n]
+
+        def forward(self, x_d, params=None):
+            o = self.net(x_d[:, :3], x_d[:, 3:6], params=params)
+            return torch.cat([o["rgb"], o["sigma"]], -1)
+
+        def get_param_groups(self):  # meta_ngp.py:446-469 grouping
+            sig = [p for n, p in self.net.named_parameters() if not n.startswith("color_mlp")]
+            col = [p for n, p in self.net.named_parameters() if n.startswith("color_mlp")]
+            return {"sigma": {"params": sig}, "color": {"params": col}}
+
+    model = Adapter(net)
+    state = OrderedDict((n, p.detach().clone()) for n, p in net.meta_named_parameters())
+    M = 1024
+    pts = torch.rand(M, 3, generator=g) * 3 - 1.5
+    dd = torch.nn.functional.normalize(torch.randn(M, 3, generator=g), dim=-1)
+    x_d = torch.cat([pts, dd], -1)
+    out = model(x_d)
+    gup = torch.randn(M, 4, generator=g)
+    grads = torch.autograd.grad((out * gup).sum(), list(net.parameters()))
+    names = [n for n, _ in net.named_parameters()]
+    # a fast-weights forward through params= (MetaLinear path) must equal the module forward
+    fast = OrderedDict((n, p * 1.0) for n, p in net.meta_named_parameters())
+    out_fast = model(x_d, params=fast)
+    assert torch.equal(out_fast, out)
+    # trunc_exp backward outside the clamp
+    te_x = torch.tensor([-100.0, -5.0, 0.0, 3.0, 100.0], requires_grad=True)
+    te_y = trunc_exp(te_x)
+    te_g, = torch.autograd.grad(te_y.sum(), te_x)
+    arr = {f"w/{n}": v.numpy() for n, v in state.items()}
+    arr.update({f"g/{n}": gr.numpy() for n, gr in zip(names, grads)})
+    np.savez_compressed(os.path.join(OUT, "mlp.npz"), x_d=x_d.numpy(), out=out.detach().numpy(),
+                        gup=gup.numpy(), te_x=te_x.detach().numpy(), te_y=te_y.detach().numpy(),
+                        te_g=te_g.numpy(), **arr)
+
+    # ---------------------------------------------------------------- volume_render
+    vr = {}
+    for tag, (N, S) in (("s64", (128, 64)), ("s192", (64, 192))):
+        t = torch.sort(torch.rand(N, S, generator=g) * 4 + 2, -1)[0]
+        t[0, 5] = t[0, 4]  # a zero-length interval (clamp_min(1e-4) branch)
+        rgbs = torch.rand(N, S, 4, generator=g)
+        rgbs[..., :3] = rgbs[..., :3] * 1.2 - 0.1  # exercise rgb clamp(0,1)
+        rgbs[..., 3] = torch.exp(torch.randn(N, S, generator=g) * 2.0)
+        rgbs[:8, :, 3] *= -1.0  # negative sigma rows (clamp_min(0))
+        rgbs[8:16, :, 3] = 1e4  # fully opaque rays (alpha clamp at 1-1e-7)
+        rgbs.requires_grad_(True)
+        bg = torch.ones(N, 3)
+        rgb, depth, w, acc = rr.volume_render(rgbs, t, bg_rgb=bg)
+        g_rgb, g_d, g_a, g_w = (torch.randn(N, 3, generator=g), torch.randn(N, generator=g),
+                                torch.randn(N, generator=g), torch.randn(N, S, generator=g))
+        grad_all, = torch.autograd.grad((rgb * g_rgb).sum() + (depth * g_d).sum() + (acc * g_a).sum()
+                                        + (w * g_w).sum(), rgbs)
+        grad_rgb, = torch.autograd.grad((rr.volume_render(rgbs, t, bg_rgb=bg)[0] * g_rgb).sum(), rgbs)
+        vr.update({f"{tag}/t": t, f"{tag}/rgbs": rgbs.detach(), f"{tag}/rgb": rgb.detach(),
+                   f"{tag}/depth": depth.detach(), f"{tag}/w": w.detach(), f"{tag}/acc": acc.detach(),
+                   f"{tag}/g_rgb": g_rgb, f"{tag}/g_d": g_d, f"{tag}/g_a": g_a, f"{tag}/g_w": g_w,
+                   f"{tag}/grad_all": grad_all, f"{tag}/grad_rgb": grad_rgb})
+    np.savez_compressed(os.path.join(OUT, "volume_render.npz"), **{k: v.numpy() for k, v in vr.items()})
+
+    # ---------------------------------------------------------------- render_rays end to end
+    idx = torch.randperm(rays_const.shape[0], generator=g)[:128]
+    rays = rays_const[idx].contiguous()
+    model.eval()
+    with torch.no_grad():
+        e_rgb, e_depth, e_w, e_acc = rr.render_rays(model, rays, ray_samples=64, chunk=4096)
+    model.train()
+    torch.manual_seed(77)
+    u = torch.rand(128, 64)
+    torch.manual_seed(77)
+    with torch.no_grad():
+        t_rgb, t_depth, t_w, t_acc = rr.render_rays(model, rays, ray_samples=64, chunk=4096)
+    # reproduce the reference's jitter draw exactly: stratified_t_vals draws rand_like((N,S))
+    torch.manual_seed(77)
+    tv = rr.stratified_t_vals(rays[:, 6], rays[:, 7], 64, randomized=True)
+    np.savez_compressed(os.path.join(OUT, "render.npz"), rays=rays.numpy(), e_rgb=e_rgb.numpy(),
+                        e_depth=e_depth.numpy(), e_w=e_w.numpy(), e_acc=e_acc.numpy(), u=u.numpy(),
+                        t_train=tv.numpy(), t_rgb=t_rgb.numpy(), t_depth=t_depth.numpy(),
+                        t_w=t_w.numpy(), t_acc=t_acc.numpy())
+
+    # ---------------------------------------------------------------- one train step (runtime_adapt.py:286-310)
+    gt = torch.rand(128, 3, generator=g)
+    P = SimpleNamespace(optimizer="adam", sigma_lr=2e-3, color_lr=2e-3, lr=1e-4, weight_decay=0.0,
+                        ray_samples=64, chunk_points=4096, color_space="linear")
+    # common/utils.py:16-76 get_optimizer(P) with P.optimizer="adam" (not importable here: its module
+    # imports torchvision, absent from the image) — same groups/lrs built directly:
+    grp = model.get_param_groups()
+    optimizer = torch.optim.Adam([{"params": grp["sigma"]["params"], "lr": P.sigma_lr, "name": "sigma"},
+                                  {"params": grp["color"]["params"], "lr": P.color_lr, "name": "color"}],
+                                 lr=P.lr, weight_decay=P.weight_decay)
+    model.train()
+    optimizer.zero_grad()
+    torch.manual_seed(77)  # same jitter u as above
+    loss = compute_mse_loss(P, model, {"rays": rays, "rgbs": gt})
+    loss.backward()
+    gnorm = torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+    optimizer.step()
+    keep = ["trunk.0.linear.weight", "trunk.4.linear.weight", "trunk.7.linear.bias", "sigma_head.weight",
+            "sigma_head.bias", "geo_head.weight", "color_mlp.layer0.linear.weight",
+            "color_mlp.color_out.weight", "color_mlp.color_out.bias"]
+    after = {f"p/{n}": p.detach().numpy() for n, p in net.named_parameters() if n in keep}
+    np.savez_compressed(os.path.join(OUT, "train_step.npz"), gt=gt.numpy(), loss=np.float32(loss.item()),
+                        gnorm=np.float32(gnorm.item()), lr=np.float32(2e-3), **after)
+    for f in sorted(os.listdir(OUT)):
+        print(f, os.path.getsize(os.path.join(OUT, f)))
+
+
+if __name__ == "__main__":
+    main()
