@@ -1,0 +1,154 @@
+/*
+ * nerf_amd.h — C-ABI of the MI355X (gfx950) NeRF hot-path library  libnerf_amd.so
+ *
+ * Every entry point is `extern "C"`, takes plain device pointers + sizes + a hipStream_t,
+ * never allocates device memory, never synchronises the device, and returns an int status:
+ *     0  ok
+ *    <0  invalid argument (shape / alignment / enum)  — see NERF_E_* below
+ *    >0  hipError_t of the failed launch (passthrough)
+ * All buffers are caller-owned (PyTorch allocates them).  All floating point is fp32.
+ * Thread-safe and re-entrant: no mutable global state.
+ *
+ * Each function names the reference interface it replaces (paths relative to
+ * psklavos1/NeRF-Sys adaptive_nerf/).  INTEGRATION.md shows the ctypes binding.
+ */
+#ifndef NERF_AMD_H
+#define NERF_AMD_H
+
+#include <stdint.h>
+#include <stddef.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NERF_OK 0
+#define NERF_E_ARG (-1)      /* bad size / pointer */
+#define NERF_E_ALIGN (-2)    /* pointer not 16-byte aligned */
+#define NERF_E_ENUM (-3)     /* unknown enum value */
+#define NERF_E_WORKSPACE (-4)/* workspace too small */
+
+/* ------------------------------------------------------------------ rays */
+
+/* get_ray_directions (nerfs/ray_sampling.py:111-136) + get_rays (:50-108, _rays_cam_to_world :10-24)
+ * + SceneBox.ray_aabb_intersect (nerfs/scene_box.py:45-107).
+ * Pixel p of the batch is (img, row, col) = pix[3p..3p+2] (pix may be NULL: dense H*W image of
+ * pose 0, row-major).  c2w: n_poses x 3 x 4 row-major.  aabb (6 floats min,max) or NULL for the
+ * constant [near,far].  Writes rays (n,8) = [o, d, near, far].  If images_u8 != NULL (n_poses x H x
+ * W x 3 bytes) the gathered pixel colour /255 is written to rgb_out (n,3). */
+int nerf_rays_gen(const float* c2w, int n_poses, const int32_t* pix, int64_t n, int H, int W,
+                  float fx, float fy, float cx, float cy, int center_pixels, float near_v, float far_v,
+                  const float* aabb, float aabb_max_bound, float aabb_invalid,
+                  const uint8_t* images_u8, float* rays_out, float* rgb_out, hipStream_t stream);
+
+/* Random training batch: draws n (img,row,col) triplets with a counter-based RNG (seed) into
+ * pix_out (n,3) — the data path of RamRaysDataset/DataLoader (pipelines/online_stage/runtime_adapt.py:76-86). */
+int nerf_pick_pixels(int64_t n, int n_images, int H, int W, uint64_t seed, int32_t* pix_out,
+                     hipStream_t stream);
+
+/* clamp_rays_near_far (nerfs/ray_sampling.py:139-176), in place; valid_out (n) bytes or NULL.
+ * has_near/has_far select the overrides. */
+int nerf_clamp_near_far(float* rays, int64_t n, int has_near, float near_v, int has_far, float far_v,
+                        float eps, float invalid_value, uint8_t* valid_out, hipStream_t stream);
+
+/* Forward-facing NDC rays (canonical NeRF; absent in the reference).  rays_in/out (n,8); output
+ * near=0, far=1. */
+int nerf_rays_ndc(const float* rays_in, int64_t n, int H, int W, float focal, float near_plane,
+                  float* rays_out, hipStream_t stream);
+
+/* ------------------------------------------------------------------ sampling */
+
+/* stratified_t_vals (nerfs/ray_rendering.py:262-287).  randomized!=0 jitters each interval with u
+ * (n,S) if given, else with the counter RNG (seed).  t_out (n,S). */
+int nerf_sample_stratified(const float* rays, int64_t n, int S, int randomized, const float* u,
+                           uint64_t seed, float* t_out, hipStream_t stream);
+
+/* Point construction of render_rays_stratified (nerfs/ray_rendering.py:317-319):
+ * x_d[r*S+s] = [o + d t, d]  (n*S, 6). */
+int nerf_build_xd(const float* rays, const float* t, int64_t n, int S, float* xd_out, hipStream_t stream);
+
+/* Hierarchical inverse-CDF resampling (canonical NeRF sample_pdf; ABSENT in the reference).
+ * t (n,S) sorted coarse depths, w (n,S) coarse weights.  Draws n_imp samples from the pdf of the
+ * interior weights over the S-1 t-midpoints (u (n,n_imp) in [0,1) if given, else linspace when
+ * det!=0, else counter RNG(seed)), and writes the sorted union t_out (n, S+n_imp).
+ * Requires S+n_imp <= 512 and S >= 3. */
+int nerf_sample_pdf(const float* t, const float* w, int64_t n, int S, int n_imp, const float* u, int det,
+                    uint64_t seed, float* t_out, hipStream_t stream);
+
+/* ------------------------------------------------------------------ encoding */
+
+/* FrequencyEncoder.torch_forward (models/encodings.py:437-444): out (n, D*(2L+inc)) with row
+ * stride ld_out floats; per dim [cos 2^0..2^{L-1}, sin ...] after the optional raw input. */
+int nerf_freq_encode(const float* x, int64_t n, int D, int L, int include_input, float* out, int ld_out,
+                     hipStream_t stream);
+
+/* ------------------------------------------------------------------ MLP (vanilla expert) */
+
+/* Packed weight layout of the 8x256 NeRF MLP (models/inr/meta_vanilla.py:13-154, frequency dirs):
+ * tensors (PyTorch (out,in) row-major, zero-padded):  trunk.i W (256 x Kpad_i) b(256), i=0..7 with
+ * Kpad = 64 / 256 / 320 (skip, [h|enc] hidden first) ; head W (32 x 256) rows [sigma, geo0..14, 0..]
+ * b(32) ; color0 W (128 x 64) cols [geo 15 | dir-enc 27 | 0] b(128) ; color1 W (32 x 128) b(32).
+ * nerf_mlp_layout fills table[t*4 + {offset, rows, cols_padded, cols_real}] for t < 22 tensors
+ * (order: W0,b0,...,W7,b7, Wh,bh, Wc0,bc0, Wc1,bc1) and returns the total packed floats. */
+int64_t nerf_mlp_layout(int64_t* table);
+
+/* Workspace (bytes) needed by nerf_mlp_fwd/bwd for M samples.  training!=0 keeps every
+ * activation for nerf_mlp_bwd. */
+int64_t nerf_mlp_workspace_bytes(int64_t M, int training);
+
+/* expert(x_d (M,6), params) -> (M,4) [sigmoid rgb, trunc_exp sigma]  (meta_vanilla.py:123-154,
+ * metamodule.py:140-156, trunc_exp.py:43-61).  w: packed weights.  ws: workspace (16B aligned). */
+int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws, int64_t ws_bytes,
+                 int training, hipEvent_t* events, hipStream_t stream);
+
+/* events: NULL, or 16 caller-created hipEvent_t recorded on `stream` around each trunk layer's GEMM
+ * (events[2i], events[2i+1] bracket trunk.i) — for live per-kernel timing (bench.py roofline). */
+
+/* Backward of nerf_mlp_fwd (autograd of the same modules).  Needs the workspace of a training
+ * forward on the same x_d/w.  d_w (packed layout) is overwritten, or accumulated into if
+ * accumulate!=0. */
+int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
+                 int64_t ws_bytes, hipEvent_t* events, hipStream_t stream);
+/* events: NULL, or 32 hipEvent_t: events[4i+0/1] bracket the weight-gradient GEMM of trunk.i,
+ * events[4i+2/3] its input-gradient GEMM (i >= 1). */
+
+/* ------------------------------------------------------------------ compositing + loss */
+
+/* volume_render (nerfs/ray_rendering.py:114-165, raw_rgb=raw_sigma=False).  rgb_sigma (n,S,4),
+ * t (n,S), bg (n,3) or NULL.  Outputs rgb (n,3), depth (n), weights (n,S), acc (n).
+ * Optional fused loss head (nerfs/losses.py:10-32 + color_space.py:22-66): if gt != NULL,
+ * loss_sum[0] += inv_count * sum((cs(pred)-cs(gt))^2) and d_rgb (n,3) = dloss/drgb.
+ * color_space: 0 linear, 1 srgb, 2 identity.  S <= 1024. */
+int nerf_composite_fwd(const float* rgb_sigma, const float* t, const float* bg, int64_t n, int S,
+                       float sigma_scale, float* rgb, float* depth, float* weights, float* acc,
+                       const float* gt, int color_space, float inv_count, float* loss_sum, float* d_rgb,
+                       hipStream_t stream);
+
+/* Backward of volume_render: upstream grads g_rgb (n,3) [required], g_depth (n), g_acc (n),
+ * g_weights (n,S) [each nullable] -> d_rgb_sigma (n,S,4). */
+int nerf_composite_bwd(const float* rgb_sigma, const float* t, const float* bg, int64_t n, int S,
+                       float sigma_scale, const float* g_rgb, const float* g_depth, const float* g_acc,
+                       const float* g_weights, float* d_rgb_sigma, hipStream_t stream);
+
+/* ------------------------------------------------------------------ optimiser */
+
+/* Per-block partial sums of squares of g (n) into partials[256] (first pass of
+ * clip_grad_norm_, pipelines/online_stage/runtime_adapt.py:305-307). */
+int nerf_grad_sqnorm(const float* g, int64_t n, float* partials, hipStream_t stream);
+
+/* torch.optim.Adam step (common/utils.py:16-76 param groups) over a flat buffer split into
+ * n_seg segments [seg_off[i], seg_off[i+1]) with learning rate seg_lr[i] (n_seg <= 8).
+ * If partials != NULL and max_norm > 0 the gradient is first scaled by
+ * min(1, max_norm / (sqrt(sum(partials)) + 1e-6))  (clip_grad_norm_). step is 1-based. */
+int nerf_adam(float* p, const float* g, float* m, float* v, int64_t n, const int64_t* seg_off_host,
+              const double* seg_lr_host, int n_seg, double beta1, double beta2, float eps, float weight_decay,
+              int step, const float* partials, float max_norm, hipStream_t stream);
+
+/* Library build identification (string, static). */
+const char* nerf_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NERF_AMD_H */

@@ -1,0 +1,288 @@
+// fp32-input MFMA GEMMs for the NeRF MLP (gfx950 `v_mfma_f32_32x32x2_f32`, exact fp32 fmaf chains).
+//
+// Three shapes cover the whole MLP forward/backward (weights PyTorch (out,in) row-major):
+//   gemm_nt     C[m][n] = epi( sum_k A[m][k] * B[n][k] )      forward  (B = W)      and
+//                                                             dgrad    (B = W^T, copied once per step)
+//   gemm_wgrad  P[s][n][k] = sum_{m in split s} G[m][n] * X[m][k]   (+ column sums of G -> bias grad)
+//   reduce      dW = sum_s P[s]                                deterministic split-M reduction
+//
+// Tiling (one 256-thread workgroup = 4 waves, fp32 MFMA runs at the fp32 vector rate, 64 FLOP/clk/SIMD):
+//   * BK = 16 k-slab, double-buffered in LDS, register-staged float4 global loads issued before the
+//     MFMA block of the current slab and written to the other LDS buffer after it (one barrier / slab).
+//   * lane l of a 32x32x2 MFMA supplies A[i=l&31][k-slot h=l>>5]; the slab's 16 k are split as
+//     k = 8h + s for MFMA s = 0..7, so each lane reads its 8 k-values as two ds_read_b128 from a row of
+//     the [rows][20]-float LDS tile (80-B row pitch: 16 consecutive rows hit 16 distinct 16-B bank slots).
+//   * XCD-aware bijective blockIdx remap so that the column tiles of one row panel share an XCD L2.
+#pragma once
+#include "common.hpp"
+
+typedef float nerf_f32x16 __attribute__((ext_vector_type(16)));
+
+enum NerfEpi { EPI_BIAS = 0, EPI_BIAS_RELU = 1, EPI_MASK = 2, EPI_NONE = 3 };
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+// ------------------------------------------------------------------------------------------ gemm_nt
+// Requirements (checked by the host wrapper): M % BM == 0, N % BN == 0, K % 16 == 0, lda/ldb/ldc/ldm % 4
+// == 0, 16-byte aligned A/B.
+template <int BM, int BN, int WAVES_M, int EPI>
+__global__ __launch_bounds__(256) void gemm_nt_kernel(const float* __restrict__ A, int lda,
+                                                      const float* __restrict__ B, int ldb,
+                                                      const float* __restrict__ bias, float* __restrict__ C, int ldc,
+                                                      const float* __restrict__ mask, int ldm, int K, int n_ntiles) {
+  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0, "wave tile");
+  constexpr int BK = 16, LS = 20;  // LDS row pitch in floats
+  constexpr int A_F4 = BM * BK / 4, B_F4 = BN * BK / 4;
+  constexpr int A_PER = (A_F4 + 255) / 256, B_PER = (B_F4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LS];
+
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
+  const int64_t m0 = (int64_t)mt * BM;
+  const int n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int li = lane & 31, lh = lane >> 5;
+
+  const float* Ab = A + m0 * lda;
+  const float* Bb = B + (int64_t)n0 * ldb;
+
+  float4 ra[A_PER], rb[B_PER];
+#define NT_GLOAD(k0_)                                                                          \
+  _Pragma("unroll") for (int i = 0; i < A_PER; ++i) {                                         \
+    const int f = tid + 256 * i;                                                               \
+    if (A_F4 % 256 == 0 || f < A_F4)                                                           \
+      ra[i] = *reinterpret_cast<const float4*>(Ab + (int64_t)(f >> 2) * lda + (k0_) + ((f & 3) << 2)); \
+  }                                                                                            \
+  _Pragma("unroll") for (int i = 0; i < B_PER; ++i) {                                         \
+    const int f = tid + 256 * i;                                                               \
+    if (B_F4 % 256 == 0 || f < B_F4)                                                           \
+      rb[i] = *reinterpret_cast<const float4*>(Bb + (int64_t)(f >> 2) * ldb + (k0_) + ((f & 3) << 2)); \
+  }
+#define NT_SSTORE(buf_)                                                                        \
+  {                                                                                            \
+    float* As_ = smem + (buf_) * (BM + BN) * LS;                                               \
+    float* Bs_ = As_ + BM * LS;                                                                \
+    _Pragma("unroll") for (int i = 0; i < A_PER; ++i) {                                       \
+      const int f = tid + 256 * i;                                                             \
+      if (A_F4 % 256 == 0 || f < A_F4)                                                         \
+        *reinterpret_cast<float4*>(As_ + (f >> 2) * LS + ((f & 3) << 2)) = ra[i];              \
+    }                                                                                          \
+    _Pragma("unroll") for (int i = 0; i < B_PER; ++i) {                                       \
+      const int f = tid + 256 * i;                                                             \
+      if (B_F4 % 256 == 0 || f < B_F4)                                                         \
+        *reinterpret_cast<float4*>(Bs_ + (f >> 2) * LS + ((f & 3) << 2)) = rb[i];              \
+    }                                                                                          \
+  }
+
+  nerf_f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int nk = K / BK;
+  NT_GLOAD(0);
+  NT_SSTORE(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    NT_GLOAD((kt + 1 < nk ? kt + 1 : kt) * BK);
+    const float* As = smem + cur * (BM + BN) * LS;
+    const float* Bs = As + BM * LS;
+    float af[TM][8], bf[TN][8];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const float* p = As + (wm * WTM + a * 32 + li) * LS + 8 * lh;
+      const float4 x0 = *reinterpret_cast<const float4*>(p);
+      const float4 x1 = *reinterpret_cast<const float4*>(p + 4);
+      af[a][0] = x0.x; af[a][1] = x0.y; af[a][2] = x0.z; af[a][3] = x0.w;
+      af[a][4] = x1.x; af[a][5] = x1.y; af[a][6] = x1.z; af[a][7] = x1.w;
+    }
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const float* p = Bs + (wn * WTN + b * 32 + li) * LS + 8 * lh;
+      const float4 x0 = *reinterpret_cast<const float4*>(p);
+      const float4 x1 = *reinterpret_cast<const float4*>(p + 4);
+      bf[b][0] = x0.x; bf[b][1] = x0.y; bf[b][2] = x0.z; bf[b][3] = x0.w;
+      bf[b][4] = x1.x; bf[b][5] = x1.y; bf[b][6] = x1.z; bf[b][7] = x1.w;
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
+    NT_SSTORE(cur ^ 1);
+    __syncthreads();
+  }
+#undef NT_GLOAD
+#undef NT_SSTORE
+
+  // epilogue: lane holds column li, rows (r&3) + 8(r>>2) + 4 lh of each 32x32 tile
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int n = n0 + wn * WTN + b * 32 + li;
+    float bv = 0.f;
+    if (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) bv = bias[n];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm * WTM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        float v = acc[a][b][r];
+        if (EPI == EPI_BIAS) v += bv;
+        if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
+        if (EPI == EPI_MASK) v = mask[m * ldm + n] > 0.f ? v : 0.f;
+        C[m * ldc + n] = v;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ gemm_wgrad
+// P[s][n][k] (row pitch ldp) = sum over rows m of split s of G[m][n] * X[m][k]; the tile of column
+// block 0 also writes Pb[s][n] = sum_m G[m][n] (bias gradient).  MFMA A = G^T (i = n, k-slot = m),
+// B = X (k-slot = m, j = k).  LDS tiles [16 rows][cols] read with ds_read_b32 (32 consecutive floats per
+// half-wave: conflict-free).
+template <int BN, int BK, int WAVES_N>
+__global__ __launch_bounds__(256) void gemm_wgrad_kernel(const float* __restrict__ G, int ldg,
+                                                         const float* __restrict__ X, int ldx,
+                                                         float* __restrict__ P, int ldp, float* __restrict__ Pb,
+                                                         int64_t slab, int64_t rows_per_split, int64_t M,
+                                                         int n_ktiles) {
+  constexpr int WAVES_K = 4 / WAVES_N;
+  constexpr int WTN = BN / WAVES_N, WTK = BK / WAVES_K;
+  constexpr int TM = WTN / 32, TN = WTK / 32;
+  static_assert(TM >= 1 && TN >= 1, "wave tile");
+  constexpr int MR = 16;
+  constexpr int G_F4 = MR * BN / 4, X_F4 = MR * BK / 4;
+  constexpr int G_PER = (G_F4 + 255) / 256, X_PER = (X_F4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float smem[2 * MR * (BN + BK)];
+
+  const int nt = blockIdx.x / n_ktiles, kt = blockIdx.x - nt * n_ktiles;
+  const int s = blockIdx.y;
+  const int n0 = nt * BN, k0 = kt * BK;
+  const int64_t r0 = (int64_t)s * rows_per_split;
+  int64_t r1 = r0 + rows_per_split;
+  if (r1 > M) r1 = M;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave / WAVES_K, wk = wave % WAVES_K;
+  const int li = lane & 31, lh = lane >> 5;
+  const bool do_bias = (Pb != nullptr) && kt == 0 && wk == 0;
+
+  float4 rg[G_PER], rx[X_PER];
+#define WG_GLOAD(m_)                                                                           \
+  _Pragma("unroll") for (int i = 0; i < G_PER; ++i) {                                         \
+    const int f = tid + 256 * i;                                                               \
+    if (G_F4 % 256 == 0 || f < G_F4)                                                           \
+      rg[i] = *reinterpret_cast<const float4*>(G + ((m_) + f / (BN / 4)) * ldg + n0 + (f % (BN / 4)) * 4); \
+  }                                                                                            \
+  _Pragma("unroll") for (int i = 0; i < X_PER; ++i) {                                         \
+    const int f = tid + 256 * i;                                                               \
+    if (X_F4 % 256 == 0 || f < X_F4)                                                           \
+      rx[i] = *reinterpret_cast<const float4*>(X + ((m_) + f / (BK / 4)) * ldx + k0 + (f % (BK / 4)) * 4); \
+  }
+#define WG_SSTORE(buf_)                                                                        \
+  {                                                                                            \
+    float* Gs_ = smem + (buf_) * MR * (BN + BK);                                               \
+    float* Xs_ = Gs_ + MR * BN;                                                                \
+    _Pragma("unroll") for (int i = 0; i < G_PER; ++i) {                                       \
+      const int f = tid + 256 * i;                                                             \
+      if (G_F4 % 256 == 0 || f < G_F4) *reinterpret_cast<float4*>(Gs_ + f * 4) = rg[i];        \
+    }                                                                                          \
+    _Pragma("unroll") for (int i = 0; i < X_PER; ++i) {                                       \
+      const int f = tid + 256 * i;                                                             \
+      if (X_F4 % 256 == 0 || f < X_F4) *reinterpret_cast<float4*>(Xs_ + f * 4) = rx[i];        \
+    }                                                                                          \
+  }
+
+  nerf_f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  float bsum[TM];
+#pragma unroll
+  for (int a = 0; a < TM; ++a) bsum[a] = 0.f;
+
+  const int64_t nit = (r1 - r0) / MR;
+  if (nit > 0) {
+    WG_GLOAD(r0);
+    WG_SSTORE(0);
+  }
+  __syncthreads();
+  for (int64_t it = 0; it < nit; ++it) {
+    const int cur = (int)(it & 1);
+    WG_GLOAD(r0 + (it + 1 < nit ? it + 1 : it) * MR);
+    const float* Gs = smem + cur * MR * (BN + BK);
+    const float* Xs = Gs + MR * BN;
+#pragma unroll
+    for (int ss = 0; ss < 8; ++ss) {
+      const int row = 8 * lh + ss;
+      float af[TM], bf[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) af[a] = Gs[row * BN + wn * WTN + a * 32 + li];
+#pragma unroll
+      for (int b = 0; b < TN; ++b) bf[b] = Xs[row * BK + wk * WTK + b * 32 + li];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        if (do_bias) bsum[a] += af[a];
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a], bf[b], acc[a][b], 0, 0, 0);
+      }
+    }
+    WG_SSTORE(cur ^ 1);
+    __syncthreads();
+  }
+#undef WG_GLOAD
+#undef WG_SSTORE
+
+  float* Ps = P + (int64_t)s * slab;
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int k = k0 + wk * WTK + b * 32 + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + wn * WTN + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        Ps[(int64_t)n * ldp + k] = acc[a][b][r];
+      }
+    }
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const float v = bsum[a] + __shfl_xor(bsum[a], 32, 64);
+      if (lh == 0) Pb[(int64_t)s * slab + n0 + wn * WTN + a * 32 + li] = v;
+    }
+  }
+}
+
+// dst[i] = (acc ? dst[i] : 0) + sum_{s<S} src[s*slab + i]   (float4 lanes, deterministic order)
+__global__ void reduce_splits_kernel(const float* __restrict__ src, int64_t slab, int S, float* __restrict__ dst,
+                                     int64_t n4, int accumulate) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4* p = reinterpret_cast<const float4*>(src) + i;
+  const int64_t st = slab / 4;
+  for (int s = 0; s < S; ++s) {
+    const float4 v = p[s * st];
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  reinterpret_cast<float4*>(dst)[i] = a;
+}

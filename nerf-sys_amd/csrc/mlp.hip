@@ -1,0 +1,421 @@
+// The vanilla NeRF expert — 8x256 ReLU trunk with the [h|enc] skip at layer 4, sigma/geo heads,
+// 2-layer colour MLP — forward and backward on fp32 MFMA (gfx950).
+//
+// Restates (psklavos1/NeRF-Sys adaptive_nerf/):
+//   MetaNeRF.density / color / forward   models/inr/meta_vanilla.py:109-154 (ctor :36-97)
+//   MetaLinear.forward (x W^T + b)       models/metamodule/metamodule.py:140-156
+//   FrequencyEncoder (xyz L=10, dir L=4) models/encodings.py:437-444
+//   trunc_exp fwd/bwd                    models/trunc_exp.py:30-61
+// as the expert contract x_d (M,6) -> (M,4) of models/inr/meta_ngp.py:226-241.
+//
+// Activation layout in the caller's workspace (Mp = M rounded up to 256, row-major, fp32):
+//   X3E [Mp][320] : cols 0..255 = trunk.3 output, cols 256..318 = xyz encoding, col 319 = 0
+//                   (so trunk.4 reads cat([h, enc]) with K = 320 and no copy; trunk.0 reads cols 256..319)
+//   Y0..Y2, Y4..Y7 [Mp][256], O16 [Mp][32] (sigma_raw, geo0..14, 0...), CIN [Mp][64] (geo | dir-enc | 0),
+//   C0 [Mp][128], O3 [Mp][32].  Backward adds dA/dB [Mp][256], dO16, dO3, dCIN [Mp][32], dC0 [Mp][128],
+//   transposed weights, and S split-M partial slabs of the packed gradient.
+#include "gemm.hpp"
+
+namespace {
+
+constexpr int NT = 22;  // tensors in the packed layout
+constexpr int KPAD[8] = {64, 256, 256, 256, 320, 256, 256, 256};
+constexpr int KREAL[8] = {63, 256, 256, 256, 319, 256, 256, 256};
+
+struct Layout {
+  int64_t off[NT];
+  int rows[NT], cols[NT], creal[NT];
+  int64_t total;
+};
+
+Layout make_layout() {
+  Layout L{};
+  int64_t o = 0;
+  int t = 0;
+  auto add = [&](int r, int c, int cr) {
+    L.off[t] = o; L.rows[t] = r; L.cols[t] = c; L.creal[t] = cr;
+    o += (int64_t)r * c;
+    o = (o + 31) & ~int64_t(31);  // keep every tensor 128-B aligned
+    ++t;
+  };
+  for (int i = 0; i < 8; ++i) {
+    add(256, KPAD[i], KREAL[i]);
+    add(256, 1, 1);
+  }
+  add(32, 256, 256);  // head W: row 0 sigma_head, rows 1..15 geo_head
+  add(32, 1, 1);
+  add(128, 64, 42);   // color_mlp.layer0
+  add(128, 1, 1);
+  add(32, 128, 128);  // color_mlp.color_out (rows 0..2)
+  add(32, 1, 1);
+  L.total = o;
+  return L;
+}
+
+const Layout& layout() {
+  static const Layout L = make_layout();
+  return L;
+}
+
+inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+
+int n_splits(int64_t Mp) {
+  int64_t s = Mp / 2048;
+  if (s < 1) s = 1;
+  if (s > 256) s = 256;
+  return (int)s;
+}
+
+struct WS {
+  int64_t Mp;
+  float *X3E, *Y[8], *O16, *CIN, *C0, *O3;
+  // backward
+  float *dA, *dB, *dO16, *dO3, *dCIN, *dC0, *WT, *partial;
+  int S;
+  int64_t rps;
+  int64_t bytes;
+};
+
+constexpr int64_t WT_FLOATS = 7 * 65536 + 256 * 32 + 128 * 32 + 32 * 128;
+
+WS carve(void* base, int64_t M, int training) {
+  WS w{};
+  w.Mp = round_up(M < 1 ? 1 : M, 256);
+  const int64_t Mp = w.Mp;
+  float* p = reinterpret_cast<float*>(base);
+  auto take = [&](int64_t n) {
+    float* q = p;
+    p += round_up(n, 64);
+    return q;
+  };
+  w.X3E = take(Mp * 320);
+  if (training) {
+    for (int i = 0; i < 8; ++i) w.Y[i] = (i == 3) ? w.X3E : take(Mp * 256);
+  } else {
+    float* q = take(Mp * 256);
+    for (int i = 0; i < 8; ++i) w.Y[i] = (i % 2 == 0) ? q : w.X3E;  // ping-pong
+  }
+  w.O16 = take(Mp * 32);
+  w.CIN = take(Mp * 64);
+  w.C0 = take(Mp * 128);
+  w.O3 = take(Mp * 32);
+  if (training) {
+    w.dA = take(Mp * 256);
+    w.dB = take(Mp * 256);
+    w.dO16 = take(Mp * 32);
+    w.dO3 = take(Mp * 32);
+    w.dCIN = take(Mp * 32);
+    w.dC0 = take(Mp * 128);
+    w.WT = take(WT_FLOATS);
+    w.S = n_splits(Mp);
+    w.rps = round_up(nerf_cdiv(Mp, w.S), 16);
+    w.partial = take((int64_t)w.S * layout().total);
+  }
+  w.bytes = (int64_t)((char*)p - (char*)base);
+  return w;
+}
+
+inline int ld_of(const WS& w, int i) { return (i == 3) ? 320 : 256; }
+
+// ------------------------------------------------------------------ elementwise kernels
+
+// xyz positional encoding of x_d[:, :3] into X3E cols 256..319 (pad col 319 = 0; rows >= M zero).
+__global__ void pe_xyz_kernel(const float* __restrict__ xd, int64_t M, int64_t Mp, float* __restrict__ X3E) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (row, dim)
+  if (idx >= Mp * 3) return;
+  const int64_t m = idx / 3;
+  const int k = (int)(idx - m * 3);
+  float* q = X3E + m * 320 + 256;
+  if (m >= M) {
+    for (int c = k; c < 64; c += 3) q[c] = 0.f;
+    if (k == 0) q[63] = 0.f;
+    return;
+  }
+  const float v = xd[m * 6 + k];
+  q[k] = v;
+  float* pe = q + 3 + k * 20;
+  float band = 1.0f;
+#pragma unroll
+  for (int l = 0; l < 10; ++l) {
+    float s, c;
+    sincosf(v * band, &s, &c);
+    pe[l] = c;
+    pe[10 + l] = s;
+    band *= 2.0f;
+  }
+  if (k == 0) q[63] = 0.f;
+}
+
+// CIN[m] = [O16[m][1..15], direction encoding (27), zeros]
+__global__ void build_cin_kernel(const float* __restrict__ xd, const float* __restrict__ O16, int64_t M, int64_t Mp,
+                                 float* __restrict__ CIN) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= Mp) return;
+  float4* q4 = reinterpret_cast<float4*>(CIN + m * 64);
+  if (m >= M) {
+    for (int c = 0; c < 16; ++c) q4[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  float v[64];
+  const float* o = O16 + m * 32;
+#pragma unroll
+  for (int c = 0; c < 15; ++c) v[c] = o[1 + c];
+  const float d[3] = {xd[m * 6 + 3], xd[m * 6 + 4], xd[m * 6 + 5]};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    v[15 + k] = d[k];
+    float band = 1.0f;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      float s, c;
+      sincosf(d[k] * band, &s, &c);
+      v[18 + k * 8 + l] = c;
+      v[18 + k * 8 + 4 + l] = s;
+      band *= 2.0f;
+    }
+  }
+#pragma unroll
+  for (int c = 42; c < 64; ++c) v[c] = 0.f;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) q4[c] = make_float4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+constexpr float EXP_MAX = 88.722839111f;
+
+__global__ void head_out_kernel(const float* __restrict__ O3, const float* __restrict__ O16, int64_t M,
+                                float* __restrict__ out) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  const float* c = O3 + m * 32;
+  const float sr = O16[m * 32];
+  const float sg = expf(fminf(fmaxf(sr, -EXP_MAX), EXP_MAX));
+  reinterpret_cast<float4*>(out)[m] = make_float4(sigmoidf_(c[0]), sigmoidf_(c[1]), sigmoidf_(c[2]), sg);
+}
+
+// d_rgb_sigma -> dO3 (cols 0..2, rest 0) and dO16 col 0 (sigma), cols 16..31 = 0.
+__global__ void head_out_bwd_kernel(const float* __restrict__ g, const float* __restrict__ O3,
+                                    const float* __restrict__ O16, int64_t M, int64_t Mp, float* __restrict__ dO3,
+                                    float* __restrict__ dO16) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= Mp) return;
+  float4* q3 = reinterpret_cast<float4*>(dO3 + m * 32);
+  float4* q16 = reinterpret_cast<float4*>(dO16 + m * 32);
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  float a = 0.f, b = 0.f, c = 0.f, ds = 0.f;
+  if (m < M) {
+    const float4 gg = reinterpret_cast<const float4*>(g)[m];
+    const float* o = O3 + m * 32;
+    const float s0 = sigmoidf_(o[0]), s1 = sigmoidf_(o[1]), s2 = sigmoidf_(o[2]);
+    a = gg.x * (s0 * (1.0f - s0));
+    b = gg.y * (s1 * (1.0f - s1));
+    c = gg.z * (s2 * (1.0f - s2));
+    const float sr = O16[m * 32];
+    ds = gg.w * expf(fminf(fmaxf(sr, -EXP_MAX), EXP_MAX));
+  }
+  q3[0] = make_float4(a, b, c, 0.f);
+#pragma unroll
+  for (int i = 1; i < 8; ++i) q3[i] = z;
+  q16[0].x = ds;
+#pragma unroll
+  for (int i = 4; i < 8; ++i) q16[i] = z;
+}
+
+// dO16[m][1..15] = dCIN[m][0..14]
+__global__ void geo_bwd_kernel(const float* __restrict__ dCIN, int64_t Mp, float* __restrict__ dO16) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= Mp * 15) return;
+  const int64_t m = idx / 15;
+  const int c = (int)(idx - m * 15);
+  dO16[m * 32 + 1 + c] = dCIN[m * 32 + c];
+}
+
+// batched transpose: dst_i[c][r] = src_i[r][c] for r < rows_i, c < cols_i  (src pitch lds_i)
+struct TJob {
+  const float* src;
+  float* dst;
+  int rows, cols, lds;
+};
+struct TJobs {
+  TJob j[10];
+};
+__global__ void transpose_kernel(TJobs jobs) {
+  const TJob J = jobs.j[blockIdx.z];
+  __shared__ float tile[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  if (r0 >= J.rows || c0 >= J.cols) return;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int y = ty; y < 32; y += 8) {
+    const int r = r0 + y, c = c0 + tx;
+    tile[y][tx] = (r < J.rows && c < J.cols) ? J.src[(int64_t)r * J.lds + c] : 0.f;
+  }
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) {
+    const int c = c0 + y, r = r0 + tx;
+    if (c < J.cols && r < J.rows) J.dst[(int64_t)c * J.rows + r] = tile[tx][y];
+  }
+}
+
+// ------------------------------------------------------------------ launch helpers
+
+template <int BM, int BN, int WAVES_M, int EPI>
+int launch_nt(const float* A, int lda, const float* B, int ldb, const float* bias, float* C, int ldc,
+              const float* mask, int ldm, int64_t M, int N, int K, hipStream_t st) {
+  if (M % BM || N % BN || K % 16) return NERF_E_ARG;
+  const int ntn = N / BN;
+  const int64_t nblk = (M / BM) * ntn;
+  gemm_nt_kernel<BM, BN, WAVES_M, EPI><<<(unsigned)nblk, 256, 0, st>>>(A, lda, B, ldb, bias, C, ldc, mask, ldm, K, ntn);
+  return NERF_OK;
+}
+
+// dispatch on N for the trunk-like GEMMs
+template <int EPI>
+int nt(const float* A, int lda, const float* B, int ldb, const float* bias, float* C, int ldc, const float* mask,
+       int ldm, int64_t M, int N, int K, hipStream_t st) {
+  if (N == 256 || N == 128) return launch_nt<128, 128, 2, EPI>(A, lda, B, ldb, bias, C, ldc, mask, ldm, M, N, K, st);
+  if (N == 32) return launch_nt<256, 32, 4, EPI>(A, lda, B, ldb, bias, C, ldc, mask, ldm, M, N, K, st);
+  return NERF_E_ARG;
+}
+
+int wgrad(const float* G, int ldg, const float* X, int ldx, int tensor_w, const WS& w, int N, int K, hipStream_t st) {
+  const Layout& L = layout();
+  float* P = w.partial + L.off[tensor_w];
+  float* Pb = w.partial + L.off[tensor_w + 1];
+  const int ldp = L.cols[tensor_w];
+  const int64_t slab = L.total;
+  if (N % 32 || K % 32) return NERF_E_ARG;
+  if (N >= 128 && K % 128 == 0) {
+    dim3 grid((N / 128) * (K / 128), w.S);
+    gemm_wgrad_kernel<128, 128, 2><<<grid, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, K / 128);
+  } else if (N >= 128 && K % 64 == 0) {
+    dim3 grid((N / 128) * (K / 64), w.S);
+    gemm_wgrad_kernel<128, 64, 2><<<grid, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, K / 64);
+  } else if (N == 32 && K % 128 == 0) {
+    dim3 grid(K / 128, w.S);
+    gemm_wgrad_kernel<32, 128, 1><<<grid, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, K / 128);
+  } else {
+    return NERF_E_ARG;
+  }
+  return NERF_OK;
+}
+
+#define TRY(x)                     \
+  do {                             \
+    int _e = (x);                  \
+    if (_e != NERF_OK) return _e;  \
+  } while (0)
+
+}  // namespace
+
+extern "C" int64_t nerf_mlp_layout(int64_t* table) {
+  const Layout& L = layout();
+  if (table) {
+    for (int t = 0; t < NT; ++t) {
+      table[4 * t + 0] = L.off[t];
+      table[4 * t + 1] = L.rows[t];
+      table[4 * t + 2] = L.cols[t];
+      table[4 * t + 3] = L.creal[t];
+    }
+  }
+  return L.total;
+}
+
+extern "C" int64_t nerf_mlp_workspace_bytes(int64_t M, int training) {
+  if (M < 0) return -1;
+  return carve(nullptr, M, training).bytes + 256;
+}
+
+extern "C" int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws, int64_t ws_bytes,
+                            int training, hipEvent_t* ev, hipStream_t st) {
+  NERF_CHECK_ARG(w && x_d && rgb_sigma && ws && M >= 0);
+  if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(rgb_sigma)) return NERF_E_ALIGN;
+  const WS W = carve(ws, M, training);
+  if (ws_bytes < W.bytes) return NERF_E_WORKSPACE;
+  if (M == 0) return NERF_OK;
+  const Layout& L = layout();
+  const int64_t Mp = W.Mp;
+  auto Wt = [&](int t) { return w + L.off[t]; };
+
+  pe_xyz_kernel<<<(unsigned)nerf_cdiv(Mp * 3, 256), 256, 0, st>>>(x_d, M, Mp, W.X3E);
+  // trunk
+  const float* in = W.X3E + 256;
+  int ld_in = 320;
+  for (int i = 0; i < 8; ++i) {
+    float* out = W.Y[i];
+    const int ld_out = training ? ld_of(W, i) : ((i % 2 == 0) ? 256 : 320);
+    if (i == 4) { in = W.X3E; ld_in = 320; }  // cat([h3, enc]) lives in X3E
+    if (ev) (void)hipEventRecord(ev[2 * i], st);
+    TRY(nt<EPI_BIAS_RELU>(in, ld_in, Wt(2 * i), KPAD[i], Wt(2 * i + 1), out, ld_out, nullptr, 0, Mp, 256, KPAD[i], st));
+    if (ev) (void)hipEventRecord(ev[2 * i + 1], st);
+    in = out;
+    ld_in = ld_out;
+  }
+  // heads
+  TRY(nt<EPI_BIAS>(in, ld_in, Wt(16), 256, Wt(17), W.O16, 32, nullptr, 0, Mp, 32, 256, st));
+  build_cin_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(x_d, W.O16, M, Mp, W.CIN);
+  TRY(nt<EPI_BIAS_RELU>(W.CIN, 64, Wt(18), 64, Wt(19), W.C0, 128, nullptr, 0, Mp, 128, 64, st));
+  TRY(nt<EPI_BIAS>(W.C0, 128, Wt(20), 128, Wt(21), W.O3, 32, nullptr, 0, Mp, 32, 128, st));
+  head_out_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(W.O3, W.O16, M, rgb_sigma);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
+                            int64_t ws_bytes, hipEvent_t* ev, hipStream_t st) {
+  NERF_CHECK_ARG(w && d_rgb_sigma && d_w && ws && M >= 0);
+  if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(d_w) || !nerf_aligned16(d_rgb_sigma))
+    return NERF_E_ALIGN;
+  const WS W = carve(ws, M, 1);
+  if (ws_bytes < W.bytes) return NERF_E_WORKSPACE;
+  const Layout& L = layout();
+  if (M == 0) {
+    if (!accumulate) (void)hipMemsetAsync(d_w, 0, L.total * sizeof(float), st);
+    return nerf_launch_status();
+  }
+  const int64_t Mp = W.Mp;
+  auto Wt = [&](int t) { return w + L.off[t]; };
+
+  // transposed weights for the dgrad GEMMs
+  float* T = W.WT;
+  float* WTi[8] = {nullptr};
+  TJobs jobs{};
+  int nj = 0;
+  for (int i = 1; i < 8; ++i) {
+    WTi[i] = T;
+    jobs.j[nj++] = TJob{Wt(2 * i), T, 256, 256, KPAD[i]};  // first 256 input cols (h part for trunk.4)
+    T += 65536;
+  }
+  float* Wht = T;  jobs.j[nj++] = TJob{Wt(16), Wht, 32, 256, 256};  T += 256 * 32;   // [256][32]
+  float* Wc1t = T; jobs.j[nj++] = TJob{Wt(20), Wc1t, 32, 128, 128}; T += 128 * 32;  // [128][32]
+  float* Wc0t = T; jobs.j[nj++] = TJob{Wt(18), Wc0t, 128, 32, 64};                  // [32][128]
+  transpose_kernel<<<dim3(8, 8, nj), 256, 0, st>>>(jobs);
+
+  head_out_bwd_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(d_rgb_sigma, W.O3, W.O16, M, Mp, W.dO3, W.dO16);
+  // colour MLP
+  TRY(nt<EPI_MASK>(W.dO3, 32, Wc1t, 32, nullptr, W.dC0, 128, W.C0, 128, Mp, 128, 32, st));
+  TRY(wgrad(W.dO3, 32, W.C0, 128, 20, W, 32, 128, st));
+  TRY(nt<EPI_NONE>(W.dC0, 128, Wc0t, 128, nullptr, W.dCIN, 32, nullptr, 0, Mp, 32, 128, st));
+  TRY(wgrad(W.dC0, 128, W.CIN, 64, 18, W, 128, 64, st));
+  geo_bwd_kernel<<<(unsigned)nerf_cdiv(Mp * 15, 256), 256, 0, st>>>(W.dCIN, Mp, W.dO16);
+  // heads -> dZ7
+  float* dcur = W.dA;
+  float* dnext = W.dB;
+  TRY(nt<EPI_MASK>(W.dO16, 32, Wht, 32, nullptr, dcur, 256, W.Y[7], 256, Mp, 256, 32, st));
+  TRY(wgrad(W.dO16, 32, W.Y[7], 256, 16, W, 32, 256, st));
+  // trunk
+  for (int i = 7; i >= 0; --i) {
+    const float* X = (i == 0) ? W.X3E + 256 : (i == 4 ? W.X3E : W.Y[i - 1]);
+    const int ldx = (i == 0 || i == 4) ? 320 : ld_of(W, i - 1);
+    if (ev) (void)hipEventRecord(ev[4 * i], st);
+    TRY(wgrad(dcur, 256, X, ldx, 2 * i, W, 256, KPAD[i], st));
+    if (ev) (void)hipEventRecord(ev[4 * i + 1], st);
+    if (i > 0) {
+      if (ev) (void)hipEventRecord(ev[4 * i + 2], st);
+      TRY(nt<EPI_MASK>(dcur, 256, WTi[i], 256, nullptr, dnext, 256, W.Y[i - 1], ld_of(W, i - 1), Mp, 256, 256, st));
+      if (ev) (void)hipEventRecord(ev[4 * i + 3], st);
+      float* t = dcur; dcur = dnext; dnext = t;
+    }
+  }
+  const int64_t n4 = L.total / 4;
+  reduce_splits_kernel<<<(unsigned)nerf_cdiv(n4, 256), 256, 0, st>>>(W.partial, L.total, W.S, d_w, n4, accumulate);
+  return nerf_launch_status();
+}

@@ -1,0 +1,95 @@
+"""ctypes binding of libnerf_amd.so (include/nerf_amd.h).
+
+This is the only place the product path touches native code.  There is NO CPU fallback: if the
+library is missing the import of any op raises, and every op requires CUDA(=HIP) tensors.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_double, c_float, c_int, c_int64, c_uint64, c_void_p
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NERF_AMD_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libnerf_amd.so"))
+
+_ERR = {-1: "invalid argument", -2: "pointer not 16-byte aligned", -3: "unknown enum value",
+        -4: "workspace too small"}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libnerf_amd.so not built ({LIB_PATH}); run `python __graft_entry__.py build`"
+                               " or `make -C nerf-sys_amd` — there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        P, I, I64, F, D, U64 = c_void_p, c_int, c_int64, c_float, c_double, c_uint64
+        sig = {
+            "nerf_rays_gen": [P, I, P, I64, I, I, F, F, F, F, I, F, F, P, F, F, P, P, P, P],
+            "nerf_pick_pixels": [I64, I, I, I, U64, P, P],
+            "nerf_clamp_near_far": [P, I64, I, F, I, F, F, F, P, P],
+            "nerf_rays_ndc": [P, I64, I, I, F, F, P, P],
+            "nerf_sample_stratified": [P, I64, I, I, P, U64, P, P],
+            "nerf_build_xd": [P, P, I64, I, P, P],
+            "nerf_sample_pdf": [P, P, I64, I, I, P, I, U64, P, P],
+            "nerf_freq_encode": [P, I64, I, I, I, P, I, P],
+            "nerf_mlp_layout": [P],
+            "nerf_mlp_workspace_bytes": [I64, I],
+            "nerf_mlp_fwd": [P, P, I64, P, P, I64, I, P, P],
+            "nerf_mlp_bwd": [P, I64, P, P, I, P, I64, P, P],
+            "nerf_composite_fwd": [P, P, P, I64, I, F, P, P, P, P, P, I, F, P, P, P],
+            "nerf_composite_bwd": [P, P, P, I64, I, F, P, P, P, P, P, P],
+            "nerf_grad_sqnorm": [P, I64, P, P],
+            "nerf_adam": [P, P, P, P, I64, P, P, I, D, D, F, F, I, P, F, P],
+            "nerf_version": [],
+        }
+        for name, args in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = c_int
+        L.nerf_mlp_layout.restype = c_int64
+        L.nerf_mlp_workspace_bytes.restype = c_int64
+        L.nerf_version.restype = ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+EXPORTS = ("nerf_rays_gen", "nerf_pick_pixels", "nerf_clamp_near_far", "nerf_rays_ndc",
+           "nerf_sample_stratified", "nerf_build_xd", "nerf_sample_pdf", "nerf_freq_encode",
+           "nerf_mlp_layout", "nerf_mlp_workspace_bytes", "nerf_mlp_fwd", "nerf_mlp_bwd",
+           "nerf_composite_fwd", "nerf_composite_bwd", "nerf_grad_sqnorm", "nerf_adam", "nerf_version")
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        msg = _ERR.get(status, f"hipError {status}")
+        if status in (-1, -3):
+            raise ValueError(f"{what}: {msg}")
+        raise RuntimeError(f"{what}: {msg}")
+
+
+def ptr(t):
+    """Device pointer of a CUDA tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("nerf_amd ops take HIP device tensors only (no CPU fallback)")
+    return c_void_p(t.data_ptr())
+
+
+def stream():
+    return c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def need(t, name, dtype=torch.float32):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ValueError(f"{name} must be a HIP device tensor (no CPU fallback)")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return t

@@ -1,0 +1,204 @@
+"""Typed wrappers over the C-ABI: allocate outputs with torch (caller-owned buffers), launch on the
+current stream, raise on a non-zero status.  No autograd here (see ray_rendering / vanilla)."""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import torch
+
+from ._lib import check, lib, need, ptr, stream
+
+F32 = torch.float32
+_CS = {"linear": 0, "srgb": 1, "identity": 2}
+
+
+def _empty(shape, like):
+    return torch.empty(shape, dtype=F32, device=like.device)
+
+
+def rays_gen(c2w, H, W, fx, fy, cx, cy, *, pix=None, near=None, far=None, aabb=None, center_pixels=True,
+             images_u8=None, aabb_max_bound=1e10, aabb_invalid=1e10):
+    """get_rays(get_ray_directions(...)) for a dense image (pix=None) or a batch of (img,row,col)."""
+    need(c2w, "c2w")
+    if c2w.dim() == 2:
+        c2w = c2w[:3, :4].reshape(1, 3, 4).contiguous()
+    c2w = c2w[..., :3, :4].contiguous()
+    n_poses = c2w.shape[0]
+    if pix is not None:
+        need(pix, "pix", torch.int32)
+        n = pix.shape[0]
+    else:
+        n = H * W
+    if aabb is None and (near is None or far is None):
+        raise ValueError("Provide near/far when scene_box is None")
+    if aabb is not None:
+        aabb = need(aabb.reshape(6).contiguous(), "aabb")
+    rays = torch.empty((n, 8), dtype=F32, device=c2w.device)
+    rgb = torch.empty((n, 3), dtype=F32, device=c2w.device) if images_u8 is not None else None
+    if images_u8 is not None:
+        need(images_u8, "images_u8", torch.uint8)
+    st = lib().nerf_rays_gen(ptr(c2w), n_poses, ptr(pix), n, H, W, fx, fy, cx, cy, int(center_pixels),
+                             float(near or 0.0), float(far or 0.0), ptr(aabb), aabb_max_bound, aabb_invalid,
+                             ptr(images_u8), ptr(rays), ptr(rgb), stream())
+    check(st, "nerf_rays_gen")
+    return (rays, rgb) if images_u8 is not None else rays
+
+
+def pick_pixels(n, n_images, H, W, seed, device):
+    pix = torch.empty((n, 3), dtype=torch.int32, device=device)
+    check(lib().nerf_pick_pixels(n, n_images, H, W, ctypes.c_uint64(seed & (2**64 - 1)), ptr(pix), stream()),
+          "nerf_pick_pixels")
+    return pix
+
+
+def clamp_near_far(rays, near=None, far=None, eps=1e-6, invalid_value=float("inf")):
+    need(rays, "rays")
+    rays = rays.clone()
+    valid = torch.empty(rays.shape[0], dtype=torch.uint8, device=rays.device)
+    check(lib().nerf_clamp_near_far(ptr(rays), rays.shape[0], int(near is not None), float(near or 0.0),
+                                    int(far is not None), float(far or 0.0), eps, invalid_value, ptr(valid),
+                                    stream()), "nerf_clamp_near_far")
+    return rays, valid.bool()
+
+
+def rays_ndc(rays, H, W, focal, near_plane=1.0):
+    need(rays, "rays")
+    out = torch.empty_like(rays)
+    check(lib().nerf_rays_ndc(ptr(rays), rays.shape[0], H, W, focal, near_plane, ptr(out), stream()), "nerf_rays_ndc")
+    return out
+
+
+def sample_stratified(rays, S, randomized, u=None, seed=0):
+    need(rays, "rays")
+    if u is not None:
+        need(u, "u")
+    t = _empty((rays.shape[0], S), rays)
+    check(lib().nerf_sample_stratified(ptr(rays), rays.shape[0], S, int(bool(randomized)), ptr(u),
+                                       ctypes.c_uint64(seed & (2**64 - 1)), ptr(t), stream()),
+          "nerf_sample_stratified")
+    return t
+
+
+def build_xd(rays, t):
+    need(rays, "rays"), need(t, "t")
+    n, S = t.shape
+    xd = _empty((n * S, 6), rays)
+    check(lib().nerf_build_xd(ptr(rays), ptr(t), n, S, ptr(xd), stream()), "nerf_build_xd")
+    return xd
+
+
+def sample_pdf(t, w, n_imp, u=None, det=False, seed=0):
+    need(t, "t"), need(w, "weights")
+    if u is not None:
+        need(u, "u")
+    n, S = t.shape
+    out = _empty((n, S + n_imp), t)
+    check(lib().nerf_sample_pdf(ptr(t), ptr(w), n, S, n_imp, ptr(u), int(bool(det)),
+                                ctypes.c_uint64(seed & (2**64 - 1)), ptr(out), stream()), "nerf_sample_pdf")
+    return out
+
+
+def freq_encode(x, L, include_input=True):
+    need(x, "x")
+    D = x.shape[-1]
+    flat = x.reshape(-1, D)
+    od = D * (2 * L + (1 if include_input else 0))
+    out = _empty((flat.shape[0], od), x)
+    check(lib().nerf_freq_encode(ptr(flat), flat.shape[0], D, L, int(include_input), ptr(out), od, stream()),
+          "nerf_freq_encode")
+    return out.view(*x.shape[:-1], od)
+
+
+# ------------------------------------------------------------------ MLP
+
+
+def mlp_workspace(M, training, device):
+    nb = lib().nerf_mlp_workspace_bytes(M, int(training))
+    return torch.empty(nb, dtype=torch.uint8, device=device)
+
+
+def _events_arg(events):
+    if events is None:
+        return None
+    arr = (ctypes.c_void_p * len(events))(*[ctypes.c_void_p(e.cuda_event) for e in events])
+    return arr
+
+
+def mlp_fwd(w_packed, x_d, ws, training, out=None, events=None):
+    need(w_packed, "packed weights"), need(x_d, "x_d")
+    M = x_d.shape[0]
+    if out is None:
+        out = _empty((M, 4), x_d)
+    check(lib().nerf_mlp_fwd(ptr(w_packed), ptr(x_d), M, ptr(out), ptr(ws), ws.numel(), int(training),
+                             _events_arg(events), stream()), "nerf_mlp_fwd")
+    return out
+
+
+def mlp_bwd(w_packed, M, d_rgb_sigma, ws, d_w=None, accumulate=False, events=None):
+    need(w_packed, "packed weights"), need(d_rgb_sigma, "d_rgb_sigma")
+    if d_w is None:
+        d_w = torch.empty_like(w_packed)
+        accumulate = False
+    check(lib().nerf_mlp_bwd(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws), ws.numel(),
+                             _events_arg(events), stream()), "nerf_mlp_bwd")
+    return d_w
+
+
+# ------------------------------------------------------------------ compositing
+
+
+def composite_fwd(rgb_sigma, t, bg=None, sigma_scale=1.0, gt=None, color_space="linear", inv_count=None,
+                  loss_sum=None, outs=None):
+    need(rgb_sigma, "rgb_sigma"), need(t, "t")
+    n, S = t.shape
+    if bg is not None:
+        need(bg, "bg")
+    if outs is None:
+        rgb, depth, w, acc = _empty((n, 3), t), _empty((n,), t), _empty((n, S), t), _empty((n,), t)
+    else:
+        rgb, depth, w, acc = outs
+    d_rgb = None
+    if gt is not None:
+        need(gt, "gt")
+        d_rgb = _empty((n, 3), t)
+        if loss_sum is None:
+            loss_sum = torch.zeros(1, dtype=F32, device=t.device)
+        if inv_count is None:
+            inv_count = 1.0 / (3 * n)
+    cs = _CS.get(color_space)
+    if cs is None:
+        raise ValueError(f"Invalid color_space={color_space!r}; use 'linear'|'srgb'|'identity'")
+    check(lib().nerf_composite_fwd(ptr(rgb_sigma), ptr(t), ptr(bg), n, S, float(sigma_scale), ptr(rgb), ptr(depth),
+                                   ptr(w), ptr(acc), ptr(gt), cs, float(inv_count or 0.0), ptr(loss_sum),
+                                   ptr(d_rgb), stream()), "nerf_composite_fwd")
+    if gt is not None:
+        return rgb, depth, w, acc, loss_sum, d_rgb
+    return rgb, depth, w, acc
+
+
+def composite_bwd(rgb_sigma, t, bg, g_rgb, g_depth=None, g_acc=None, g_w=None, sigma_scale=1.0, out=None):
+    n, S = t.shape
+    if out is None:
+        out = torch.empty_like(rgb_sigma)
+    check(lib().nerf_composite_bwd(ptr(rgb_sigma), ptr(t), ptr(bg), n, S, float(sigma_scale), ptr(g_rgb),
+                                   ptr(g_depth), ptr(g_acc), ptr(g_w), ptr(out), stream()), "nerf_composite_bwd")
+    return out
+
+
+# ------------------------------------------------------------------ optimiser
+
+
+def grad_sqnorm(g, partials=None):
+    if partials is None:
+        partials = torch.empty(256, dtype=F32, device=g.device)
+    check(lib().nerf_grad_sqnorm(ptr(g), g.numel(), ptr(partials), stream()), "nerf_grad_sqnorm")
+    return partials
+
+
+def adam(p, g, m, v, seg_off: Sequence[int], seg_lr: Sequence[float], step, betas=(0.9, 0.999), eps=1e-8,
+         weight_decay=0.0, partials=None, max_norm=0.0):
+    off = (ctypes.c_int64 * len(seg_off))(*seg_off)
+    lr = (ctypes.c_double * len(seg_lr))(*seg_lr)
+    check(lib().nerf_adam(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), off, lr, len(seg_lr), betas[0], betas[1], eps,
+                          weight_decay, step, ptr(partials), max_norm, stream()), "nerf_adam")

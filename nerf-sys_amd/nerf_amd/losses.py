@@ -1,0 +1,58 @@
+"""Loss head — nerfs/losses.py:10-32 + nerfs/color_space.py:4-66 of the reference.
+
+``compute_mse_loss(P, model, data, ...)`` keeps the reference signature (P.ray_samples,
+P.chunk_points, P.color_space) and adds the canonical coarse+fine term when P.n_importance > 0.
+The fused training engine (trainer.py) computes the same loss inside the compositing kernel.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .ray_rendering import render_rays
+
+
+def linear_to_srgb(x):
+    x = x.clamp(0, 1)
+    return torch.where(x <= 0.0031308, 12.92 * x, 1.055 * x.pow(1 / 2.4) - 0.055)
+
+
+def srgb_to_linear(x):
+    return torch.where(x <= 0.04045, x / 12.92, ((x + 0.055) / 1.055).pow(2.4))
+
+
+def color_space_transformer(pred_linear, gt_tensor, color_space: str):
+    cs = str(color_space).lower()
+    pred32 = pred_linear.to(torch.float32)
+    gt32 = gt_tensor.to(torch.float32).clamp(0, 1)
+    if cs == "linear":
+        pred, gt = pred32.clamp(0, 1), srgb_to_linear(gt32).clamp(0, 1)
+    elif cs == "srgb":
+        pred, gt = linear_to_srgb(pred32).clamp(0, 1), gt32.clamp(0, 1)
+    elif cs == "identity":
+        if (gt32.max() > 1) or (gt32.min() < 0):
+            raise ValueError("GT out of [0,1]; identity mode assumes normalized linear GT.")
+        pred, gt = pred32, gt32
+    else:
+        raise ValueError(f"Invalid color_space={color_space!r}; use 'linear'|'srgb'|'identity'")
+    return pred.to(pred_linear.dtype), gt.to(pred_linear.dtype)
+
+
+def compute_mse_loss(P, model, data, params=None, active_module=None, reduction="mean"):
+    gt_rgb, rays = data["rgbs"], data["rays"]
+    n_imp = int(getattr(P, "n_importance", 0) or 0)
+    out = render_rays(model, rays, ray_samples=P.ray_samples, params=params, active_module=active_module,
+                      chunk=P.chunk_points, n_importance=n_imp, return_extras=True)
+    pred_rgb, extras = out[0], out[-1]
+    cs = getattr(P, "color_space", "linear")
+    a, b = color_space_transformer(pred_rgb, gt_rgb, cs)
+    loss = F.mse_loss(a, b, reduction=reduction)
+    if n_imp > 0:
+        a, b = color_space_transformer(extras["rgb_coarse"], gt_rgb, cs)
+        loss = loss + F.mse_loss(a, b, reduction=reduction)
+    return loss
+
+
+def psnr(mse: float) -> float:
+    import math
+    return -10.0 * math.log10(max(float(mse), 1e-8))

@@ -1,0 +1,198 @@
+"""render_rays / volume_render / stratified + hierarchical sampling on the HIP kernels.
+
+Drop-in for nerfs/ray_rendering.py of the reference (same names, argument meaning, return shapes
+and error behaviour):
+  get_bg_default_color (:48-79), _get_bg_rgb (:23-45), volume_render (:114-165),
+  stratified_t_vals (:262-287), render_rays_stratified (:290-345), render_rays (:564-574),
+  render_image (:577-627).
+Extensions (absent in the reference, parity pinned against the CPU oracle only): hierarchical
+sampling through ``sample_pdf`` (canonical NeRF) via the ``n_importance`` keyword, which renders the
+fine pass with ``fine_model`` (or ``model.fine``, or the same expert) and returns the coarse outputs
+in ``extras`` when ``return_extras=True``.  The occupancy / MoE renderer (render_rays_occ, :349-558)
+is out of this round's scope and raises.
+"""
+from __future__ import annotations
+
+import warnings
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+from torch.autograd.function import once_differentiable
+
+from . import kernels as K
+from .ray_sampling import clamp_rays_near_far, rays_for_camera
+
+
+def _seed() -> int:
+    # one draw of torch's CPU generator per call: respects torch.manual_seed, no device sync
+    return int(torch.randint(0, 2**62, (1,)).item())
+
+
+# ------------------------------------------------------------------ background
+
+
+def get_bg_default_color(rgb_sigma, N: int, bg_color: str = "white") -> Optional[Tensor]:
+    device = None if rgb_sigma is None else rgb_sigma.device
+    dtype = None if rgb_sigma is None else rgb_sigma.dtype
+    if bg_color == "none":
+        return None
+    if bg_color == "white":
+        return torch.ones(N, 3, device=device, dtype=dtype)
+    if bg_color == "black":
+        return torch.zeros(N, 3, device=device, dtype=dtype)
+    if bg_color == "random":
+        return torch.rand(N, 3, device=device, dtype=dtype)
+    if bg_color == "last_sample":
+        if rgb_sigma is None or rgb_sigma.dim() != 3 or rgb_sigma.size(-1) < 3:
+            raise ValueError("bg_color='last_sample' requires rgb_sigma of shape (N,S,4) or (N,S,>=3).")
+        return rgb_sigma[:, -1, :3]
+    raise ValueError(f"Unknown background policy: {bg_color}")
+
+
+def _get_bg_rgb(model, dirs, params, rgb_sigma_or_map, N, bg_color_default):
+    if getattr(model, "use_bg_nerf", False):
+        return model.background_color(dirs)
+    return get_bg_default_color(rgb_sigma_or_map, N, bg_color_default)
+
+
+# ------------------------------------------------------------------ compositing
+
+
+class VolumeRenderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, rgb_sigma, t_vals, bg, sigma_scale):
+        rs = rgb_sigma.contiguous().float()
+        t = t_vals.contiguous().float()
+        bgc = None if bg is None else bg.contiguous().float()
+        rgb, depth, w, acc = K.composite_fwd(rs, t, bgc, sigma_scale)
+        ctx.save_for_backward(rs, t, bgc if bgc is not None else torch.empty(0), acc)
+        ctx.has_bg = bgc is not None
+        ctx.sigma_scale = sigma_scale
+        return rgb, depth, w, acc
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g_rgb, g_depth, g_w, g_acc):
+        rs, t, bg, acc = ctx.saved_tensors
+        bg = bg if ctx.has_bg else None
+        n = t.shape[0]
+        if g_rgb is None:
+            g_rgb = torch.zeros(n, 3, device=t.device)
+        d = K.composite_bwd(rs, t, bg, g_rgb.contiguous().float(),
+                            None if g_depth is None else g_depth.contiguous().float(),
+                            None if g_acc is None else g_acc.contiguous().float(),
+                            None if g_w is None else g_w.contiguous().float(), ctx.sigma_scale)
+        d_bg = None
+        if ctx.has_bg and ctx.needs_input_grad[2]:
+            d_bg = (1.0 - acc).unsqueeze(-1) * g_rgb
+        return d, None, d_bg, None
+
+
+def volume_render(rgb_sigma: Tensor, t_vals: Tensor, bg_rgb: Optional[Tensor] = None, *, raw_rgb: bool = False,
+                  raw_sigma: bool = False, sigma_scale: float = 1.0, **kwargs) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """nerfs/ray_rendering.py:114-165 on the HIP compositing kernel."""
+    if raw_rgb or raw_sigma:
+        from .vanilla import trunc_exp_torch  # raw activations are applied by torch before compositing
+        rgb = torch.sigmoid(rgb_sigma[..., :3]) if raw_rgb else rgb_sigma[..., :3]
+        sig = trunc_exp_torch(rgb_sigma[..., 3:4]) if raw_sigma else rgb_sigma[..., 3:4]
+        rgb_sigma = torch.cat([rgb, sig], -1)
+    if bg_rgb is not None:
+        bg_rgb = bg_rgb.to(rgb_sigma.device, dtype=torch.float32)
+    return VolumeRenderFn.apply(rgb_sigma, t_vals.detach(), bg_rgb, float(sigma_scale))
+
+
+# ------------------------------------------------------------------ sampling
+
+
+@torch.no_grad()
+def stratified_t_vals(near: Tensor, far: Tensor, ray_samples: int, randomized: bool = True, u: Optional[Tensor] = None,
+                      seed: Optional[int] = None) -> Tensor:
+    """ray_rendering.py:262-287.  ``u`` (N,S) replaces torch.rand_like; else the kernel's counter RNG."""
+    n = near.shape[0]
+    rays = torch.zeros(n, 8, device=near.device, dtype=torch.float32)
+    rays[:, 6] = near
+    rays[:, 7] = far
+    return K.sample_stratified(rays, ray_samples, randomized, u, _seed() if seed is None else seed)
+
+
+@torch.no_grad()
+def sample_pdf_merged(t_vals: Tensor, weights: Tensor, n_importance: int, det: bool, u: Optional[Tensor] = None,
+                      seed: Optional[int] = None) -> Tensor:
+    """Hierarchical inverse-CDF samples merged (sorted) with the coarse t: (N, S + n_importance)."""
+    return K.sample_pdf(t_vals.contiguous().float(), weights.detach().contiguous().float(), n_importance, u=u, det=det,
+                        seed=_seed() if seed is None else seed)
+
+
+# ------------------------------------------------------------------ renderers
+
+
+def _eval_points(model_eff, rays, t, params, chunk):
+    xd = K.build_xd(rays, t)
+    outs = [model_eff(xd[s:s + chunk], params=params) for s in range(0, xd.shape[0], chunk)]
+    return torch.cat(outs, 0).view(t.shape[0], t.shape[1], 4)
+
+
+def render_rays_stratified(model, rays: Tensor, ray_samples: int, params=None, active_module: Optional[int] = None,
+                           bg_color_default: str = "white", chunk: int = 1_000_000, sigma_scale=1.0, *,
+                           n_importance: int = 0, fine_model=None, fine_params=None, return_extras: bool = False,
+                           u_strat: Optional[Tensor] = None, u_pdf: Optional[Tensor] = None, **kwargs):
+    """ray_rendering.py:290-345 (+ hierarchical extension).  Returns (rgb (N,3), depth (N,),
+    weights (N,S[+n_importance]), acc (N,)) [, extras]."""
+    rays = rays.contiguous().float()
+    N = rays.shape[0]
+    training = bool(getattr(model, "training", False))
+    t = stratified_t_vals(rays[:, 6], rays[:, 7], ray_samples, randomized=training, u=u_strat)
+    model_eff = model.submodules[active_module] if active_module is not None else model
+    rgb_sigma = _eval_points(model_eff, rays, t, params, chunk)
+    bg = _get_bg_rgb(model, rays[:, 3:6], params, rgb_sigma, N, bg_color_default)
+    out = volume_render(rgb_sigma, t, bg_rgb=bg, sigma_scale=sigma_scale)
+    extras = {}
+    if n_importance and n_importance > 0:
+        tm = sample_pdf_merged(t, out[2], n_importance, det=not training, u=u_pdf)
+        fine = fine_model if fine_model is not None else getattr(model, "fine", None)
+        if fine is None:
+            fine, fparams = model_eff, params
+        else:
+            fparams = fine_params
+        rs_f = _eval_points(fine, rays, tm, fparams, chunk)
+        extras = {"rgb_coarse": out[0], "depth_coarse": out[1], "weights_coarse": out[2], "acc_coarse": out[3],
+                  "t_coarse": t, "t_fine": tm}
+        bg_f = bg if bg_color_default != "last_sample" else _get_bg_rgb(model, rays[:, 3:6], params, rs_f, N,
+                                                                         bg_color_default)
+        out = volume_render(rs_f, tm, bg_rgb=bg_f, sigma_scale=sigma_scale)
+    if return_extras:
+        return (*out, extras)
+    return out
+
+
+def render_rays(model, rays, *args, **kwargs):
+    """ray_rendering.py:564-574 dispatch."""
+    if getattr(model, "use_occ", False) and getattr(model, "occ_ready", False):
+        raise NotImplementedError("occupancy / MoE renderer (render_rays_occ) is not part of this build yet")
+    return render_rays_stratified(model, rays, *args, **kwargs)
+
+
+@torch.no_grad()
+def render_image(model, *, H: int, W: int, fx: float, fy: float, cx: float, cy: float, c2w: Tensor, scene_box=None,
+                 near: Optional[float] = None, far: Optional[float] = None, params=None,
+                 active_module: Optional[int] = None, ray_samples: int = 64, n_importance: int = 0,
+                 chunk_points: int = 1 << 22, bg_color_default: str = "white", center_pixels: bool = True,
+                 ndc: Optional[Tuple[float, float]] = None, rays_per_chunk: int = 1 << 15, use_amp: bool = False):
+    """ray_rendering.py:577-627 — rays from the fused HIP kernel, rendered in ray chunks.
+    ``ndc=(focal, near_plane)`` converts rays to forward-facing NDC first (LLFF config)."""
+    device = next(model.parameters()).device
+    rays = rays_for_camera(H, W, fx, fy, cx, cy, c2w.to(device), near=near, far=far, scene_box=scene_box,
+                           center_pixels=center_pixels)
+    if ndc is not None:
+        from .ray_sampling import ndc_rays
+        rays = ndc_rays(H, W, ndc[0], ndc[1], rays)
+    rays, _ = clamp_rays_near_far(rays, near_far_override=None)
+    rgbs, depths, accs = [], [], []
+    for s in range(0, rays.shape[0], rays_per_chunk):
+        rgb, depth, _, acc = render_rays(model, rays[s:s + rays_per_chunk], ray_samples=ray_samples, params=params,
+                                         active_module=active_module, bg_color_default=bg_color_default,
+                                         chunk=chunk_points, n_importance=n_importance)
+        rgbs.append(rgb), depths.append(depth), accs.append(acc)
+    rgb = torch.cat(rgbs).view(H, W, 3).float().clamp_(0, 1)
+    return rgb, torch.cat(depths).view(-1), torch.cat(accs).view(-1)

@@ -1,0 +1,200 @@
+"""Fused NeRF training engine on flat packed buffers — the benchmarked train step.
+
+Same step as the reference's plain train loop (pipelines/online_stage/runtime_adapt.py:278-313):
+rays -> render (coarse 64 stratified + fine 64+128 hierarchical) -> MSE (linear colour space,
+coarse + fine terms) -> backward -> clip_grad_norm_(1.0) -> Adam (per-group lr, common/utils.py:16-76),
+but every stage is a HIP launch on one stream with no host synchronisation:
+
+  pick_pixels+rays_gen(+gt gather) -> sample_stratified -> build_xd -> mlp_fwd(coarse)
+  -> composite_fwd(+loss, dL/drgb) -> sample_pdf -> build_xd -> mlp_fwd(fine) -> composite_fwd(+loss)
+  -> composite_bwd -> mlp_bwd(fine) -> composite_bwd -> mlp_bwd(coarse)
+  -> [RCCL all_reduce(SUM) of the flat gradient (+ loss) buffer, data parallel]
+  -> grad_sqnorm -> adam
+
+Both networks live in ONE flat fp32 buffer [coarse | fine] (kernel packed layout), so the data-parallel
+exchange is a single all-reduce of ~4 MB per step; the loss normaliser is 1/(3 N_global), so a SUM
+all-reduce yields exactly the global-batch mean gradient.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from . import kernels as K
+from .vanilla import PackedLayout, VanillaNeRF
+
+_CS = ("linear", "srgb", "identity")
+
+
+class RayBatcher:
+    """Random pixel batches from images resident in HBM (uint8) -> rays (N,8) + gt (N,3)."""
+
+    def __init__(self, scene, device):
+        self.scene = scene
+        self.poses = scene.poses.to(device).float().contiguous()
+        self.images = scene.images.to(device).contiguous()
+        self.device = device
+
+    def batch(self, n, seed):
+        s = self.scene
+        pix = K.pick_pixels(n, self.poses.shape[0], s.H, s.W, seed, self.device)
+        fx, fy, cx, cy = s.intrinsics
+        rays, gt = K.rays_gen(self.poses, s.H, s.W, fx, fy, cx, cy, pix=pix, near=s.near if not s.ndc else 0.0,
+                              far=s.far if not s.ndc else 1.0, images_u8=self.images)
+        if s.ndc:
+            rays = K.rays_ndc(rays, s.H, s.W, s.focal, 1.0)
+        return rays, gt
+
+
+class NeRFTrainer:
+    def __init__(self, coarse: VanillaNeRF, fine: Optional[VanillaNeRF] = None, *, n_samples: int = 64,
+                 n_importance: int = 128, lr_sigma: float = 2e-3, lr_color: float = 2e-3, betas=(0.9, 0.999),
+                 eps: float = 1e-8, weight_decay: float = 0.0, grad_clip: Optional[float] = 1.0,
+                 color_space: str = "linear", bg: str = "white", sigma_scale: float = 1.0,
+                 world_size: int = 1, device="cuda"):
+        L = PackedLayout.get()
+        self.L = L
+        self.P = L.total
+        self.nets = [coarse] + ([fine] if fine is not None else [])
+        self.n_nets = len(self.nets)
+        self.device = torch.device(device)
+        P = self.P
+        with torch.no_grad():
+            self.params = torch.cat([n.packed().detach().to(self.device) for n in self.nets]).contiguous()
+        # grads + 1 trailing float for the loss, all-reduced together
+        self.gbuf = torch.zeros(self.n_nets * P + 4, dtype=torch.float32, device=self.device)
+        self.grads = self.gbuf[: self.n_nets * P]
+        self.loss_buf = self.gbuf[self.n_nets * P: self.n_nets * P + 1]
+        self.m = torch.zeros_like(self.params)
+        self.v = torch.zeros_like(self.params)
+        self.partials = torch.empty(256, dtype=torch.float32, device=self.device)
+        cs = L.color_start
+        self.seg_off, self.seg_lr = [0], []
+        for k in range(self.n_nets):
+            self.seg_off += [k * P + cs, (k + 1) * P]
+            self.seg_lr += [lr_sigma, lr_color]
+        self.S, self.n_imp = n_samples, n_importance
+        self.betas, self.eps, self.wd = betas, eps, weight_decay
+        self.grad_clip = grad_clip
+        if color_space not in _CS:
+            raise ValueError(f"Invalid color_space={color_space!r}")
+        self.color_space = color_space
+        if bg not in ("white", "black", "none"):
+            raise ValueError("trainer background must be 'white', 'black' or 'none'")
+        self.bg_policy = bg
+        self.sigma_scale = sigma_scale
+        self.world_size = world_size
+        self.step_count = 0
+        self._ws = {}
+        self._bg = {}
+        self.timing = None  # dict of event lists when timing is enabled
+
+    # ---- helpers
+    def w(self, k):
+        return self.params[k * self.P:(k + 1) * self.P]
+
+    def g(self, k):
+        return self.grads[k * self.P:(k + 1) * self.P]
+
+    def _workspace(self, key, M):
+        ws = self._ws.get(key)
+        need = K.lib().nerf_mlp_workspace_bytes(M, 1)
+        if ws is None or ws.numel() < need:
+            ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+            self._ws[key] = ws
+        return ws
+
+    def _background(self, n):
+        if self.bg_policy == "none":
+            return None
+        b = self._bg.get(n)
+        if b is None:
+            b = torch.full((n, 3), 1.0 if self.bg_policy == "white" else 0.0, device=self.device)
+            self._bg[n] = b
+        return b
+
+    def enable_timing(self, n_steps: int = 1):
+        """Pre-create one set of HIP events per upcoming step (no host sync inside the timed steps):
+        the library records them around the fine net's trunk GEMM launches."""
+        if n_steps <= 0:
+            self.timing = None
+            return
+        mk = lambda k: [torch.cuda.Event(enable_timing=True) for _ in range(k)]
+        sets = [{"fwd": mk(16), "bwd": mk(32)} for _ in range(n_steps)]
+        for st in sets:
+            for e in st["fwd"] + st["bwd"]:
+                e.record()  # materialise the event handles
+        torch.cuda.synchronize()
+        self.timing = {"pool": sets, "used": [], "M": None}
+
+    def _next_events(self):
+        if not self.timing or not self.timing["pool"]:
+            return None
+        ev = self.timing["pool"].pop(0)
+        self.timing["used"].append(ev)
+        return ev
+
+    # ---- the step
+    def step(self, rays: torch.Tensor, gt: torch.Tensor, seed: int, u_strat=None, u_pdf=None) -> torch.Tensor:
+        """One train step on this rank's rays; returns the (global) loss as a device scalar.
+        u_strat (N,S) / u_pdf (N,n_importance) replace the in-kernel RNG (parity tests)."""
+        N = rays.shape[0]
+        S, NI = self.S, self.n_imp
+        bg = self._background(N)
+        inv_count = 1.0 / (3.0 * N * self.world_size)
+        self.gbuf.zero_()
+        fine_k = 1 if self.n_nets > 1 else 0
+        # coarse forward
+        t_c = K.sample_stratified(rays, S, True, u_strat, seed)
+        xd_c = K.build_xd(rays, t_c)
+        ws_c = self._workspace("c", N * S)
+        rs_c = K.mlp_fwd(self.w(0), xd_c, ws_c, True)
+        _, _, w_c, _, _, drgb_c = K.composite_fwd(rs_c, t_c, bg, self.sigma_scale, gt=gt,
+                                                  color_space=self.color_space, inv_count=inv_count,
+                                                  loss_sum=self.loss_buf)
+        if NI > 0:
+            t_f = K.sample_pdf(t_c, w_c, NI, u=u_pdf, det=False, seed=seed ^ 0x5EED)
+            xd_f = K.build_xd(rays, t_f)
+            ws_f = self._workspace("f", N * (S + NI))
+            ev = self._next_events()
+            rs_f = K.mlp_fwd(self.w(fine_k), xd_f, ws_f, True, events=ev["fwd"] if ev else None)
+            _, _, _, _, _, drgb_f = K.composite_fwd(rs_f, t_f, bg, self.sigma_scale, gt=gt,
+                                                    color_space=self.color_space, inv_count=inv_count,
+                                                    loss_sum=self.loss_buf)
+            d_rs_f = K.composite_bwd(rs_f, t_f, bg, drgb_f, sigma_scale=self.sigma_scale)
+            K.mlp_bwd(self.w(fine_k), N * (S + NI), d_rs_f, ws_f, d_w=self.g(fine_k), accumulate=False,
+                      events=ev["bwd"] if ev else None)
+            if ev:
+                self.timing["M"] = N * (S + NI)
+        d_rs_c = K.composite_bwd(rs_c, t_c, bg, drgb_c, sigma_scale=self.sigma_scale)
+        K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=(fine_k == 0 and NI > 0))
+        if self.world_size > 1:
+            dist.all_reduce(self.gbuf, op=dist.ReduceOp.SUM)
+        self.step_count += 1
+        if self.grad_clip is not None and self.grad_clip > 0:
+            K.grad_sqnorm(self.grads, self.partials)
+            parts, mx = self.partials, float(self.grad_clip)
+        else:
+            parts, mx = None, 0.0
+        K.adam(self.params, self.grads, self.m, self.v, self.seg_off, self.seg_lr, self.step_count, self.betas,
+               self.eps, self.wd, parts, mx)
+        return self.loss_buf
+
+    def collect_timing(self):
+        """Per-launch durations (ms) of the fine net's trunk GEMMs over every timed step:
+        {"fwd": [[8 layers] per step], "wgrad": [[8]], "dgrad": [[7: layers 1..7]], "M": samples}."""
+        out = {"fwd": [], "wgrad": [], "dgrad": [], "M": self.timing["M"]}
+        for ev in self.timing["used"]:
+            out["fwd"].append([ev["fwd"][2 * i].elapsed_time(ev["fwd"][2 * i + 1]) for i in range(8)])
+            out["wgrad"].append([ev["bwd"][4 * i].elapsed_time(ev["bwd"][4 * i + 1]) for i in range(8)])
+            out["dgrad"].append([ev["bwd"][4 * i + 2].elapsed_time(ev["bwd"][4 * i + 3]) for i in range(1, 8)])
+        return out
+
+    @torch.no_grad()
+    def sync_to_modules(self):
+        for k, net in enumerate(self.nets):
+            vals = self.L.unpack(self.w(k))
+            for n, p in net.named_parameters():
+                p.copy_(vals[n])
