@@ -248,11 +248,12 @@ extern "C" int nerf_composite_fwd(const float* rgb_sigma, const float* t, const 
                                   float sigma_scale, float* rgb, float* depth, float* weights, float* acc,
                                   const float* gt, int color_space, float inv_count, float* loss_sum, float* d_rgb,
                                   hipStream_t stream) {
-  NERF_CHECK_ARG(rgb_sigma && t && rgb && weights && n >= 0 && S >= 2);
-  if (gt) NERF_CHECK_ARG(loss_sum && d_rgb);
   if (color_space < 0 || color_space > 2) return NERF_E_ENUM;
-  if (!nerf_aligned16(rgb_sigma)) return NERF_E_ALIGN;
+  NERF_CHECK_ARG(n >= 0 && S >= 2);
   if (n == 0) return NERF_OK;
+  NERF_CHECK_ARG(rgb_sigma && t && rgb && weights);
+  if (gt) NERF_CHECK_ARG(loss_sum && d_rgb);
+  if (!nerf_aligned16(rgb_sigma)) return NERF_E_ALIGN;
   switch (spl_for(S)) {
     case 1: launch_fwd<1>(rgb_sigma, t, bg, n, S, sigma_scale, rgb, depth, weights, acc, gt, color_space, inv_count, loss_sum, d_rgb, stream); break;
     case 2: launch_fwd<2>(rgb_sigma, t, bg, n, S, sigma_scale, rgb, depth, weights, acc, gt, color_space, inv_count, loss_sum, d_rgb, stream); break;
@@ -268,9 +269,10 @@ extern "C" int nerf_composite_fwd(const float* rgb_sigma, const float* t, const 
 extern "C" int nerf_composite_bwd(const float* rgb_sigma, const float* t, const float* bg, int64_t n, int S,
                                   float sigma_scale, const float* g_rgb, const float* g_depth, const float* g_acc,
                                   const float* g_weights, float* d_rgb_sigma, hipStream_t stream) {
-  NERF_CHECK_ARG(rgb_sigma && t && g_rgb && d_rgb_sigma && n >= 0 && S >= 2);
-  if (!nerf_aligned16(rgb_sigma) || !nerf_aligned16(d_rgb_sigma)) return NERF_E_ALIGN;
+  NERF_CHECK_ARG(n >= 0 && S >= 2);
   if (n == 0) return NERF_OK;
+  NERF_CHECK_ARG(rgb_sigma && t && g_rgb && d_rgb_sigma);
+  if (!nerf_aligned16(rgb_sigma) || !nerf_aligned16(d_rgb_sigma)) return NERF_E_ALIGN;
   switch (spl_for(S)) {
     case 1: launch_bwd<1>(rgb_sigma, t, bg, n, S, sigma_scale, g_rgb, g_depth, g_acc, g_weights, d_rgb_sigma, stream); break;
     case 2: launch_bwd<2>(rgb_sigma, t, bg, n, S, sigma_scale, g_rgb, g_depth, g_acc, g_weights, d_rgb_sigma, stream); break;

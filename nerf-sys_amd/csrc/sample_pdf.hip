@@ -38,21 +38,29 @@ __global__ __launch_bounds__(256) void sample_pdf_kernel(const float* __restrict
   float* edge = s_edge[wv];
   float* stage = s_stage[wv];
 
-  // ---- pdf / cdf (chunks of 64 bins; exclusive carry across chunks)
-  float tot = 0.f;
+  // ---- pdf / cdf.  torch's CPU sum/cumsum accumulate float in double (at::acc_type<float>), so the
+  // reduction and the scan run in fp64 and each cdf entry is rounded to fp32 once, like the oracle.
+  double totd = 0.0;
   for (int b0 = 0; b0 < B; b0 += 64) {
     const int b = b0 + lane;
-    tot += (b < B) ? wr[1 + b] + 1e-5f : 0.f;
+    totd += (b < B) ? (double)(wr[1 + b] + 1e-5f) : 0.0;
   }
-  tot = wave_sum(tot);
-  float carry = 0.f;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) totd += __shfl_xor(totd, d, 64);
+  const float tot = (float)totd;
+  double carry = 0.0;
   if (lane == 0) cdf[0] = 0.f;
   for (int b0 = 0; b0 < B; b0 += 64) {
     const int b = b0 + lane;
-    const float pdf = (b < B) ? (wr[1 + b] + 1e-5f) / tot : 0.f;
-    const float inc = wave_incl_sum(pdf) + carry;
-    if (b < B) cdf[b + 1] = inc;
-    carry = __shfl(inc, 63, 64);
+    double v = (b < B) ? (double)((wr[1 + b] + 1e-5f) / tot) : 0.0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const double o = __shfl_up(v, d, 64);
+      if (lane >= d) v += o;
+    }
+    v += carry;
+    if (b < B) cdf[b + 1] = (float)v;
+    carry = __shfl(v, 63, 64);
   }
   for (int j = lane; j < S - 1; j += 64) edge[j] = 0.5f * (tr[j + 1] + tr[j]);
   __builtin_amdgcn_wave_barrier();

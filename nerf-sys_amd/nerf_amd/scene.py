@@ -83,7 +83,7 @@ def _spheres(seed: int, forward: bool):
 
 
 @torch.no_grad()
-def render_analytic(poses, H, W, focal, seed=0, forward=False, device="cpu", rows_per_chunk=64):
+def render_analytic(poses, H, W, focal, seed=0, forward=False, device="cpu", rows_per_chunk=None):
     """Exact images of the sphere scene (torch device ops; data generation, not the hot path)."""
     cen, rad, col = [t.to(device) for t in _spheres(seed, forward)]
     light = torch.tensor([0.4, 0.5, 0.75], device=device)
@@ -93,6 +93,8 @@ def render_analytic(poses, H, W, focal, seed=0, forward=False, device="cpu", row
                           torch.arange(W, device=device, dtype=torch.float32), indexing="ij")
     dirs = torch.stack([(i + 0.5 - W / 2) / focal, -(j + 0.5 - H / 2) / focal, -torch.ones_like(i)], -1)
     dirs = dirs / dirs.norm(dim=-1, keepdim=True)
+    if rows_per_chunk is None:  # whole image per pass on the GPU, bounded chunks on the CPU
+        rows_per_chunk = H if str(device).startswith("cuda") else 64
     for p in range(poses.shape[0]):
         c2w = poses[p].to(device)
         for r0 in range(0, H, rows_per_chunk):

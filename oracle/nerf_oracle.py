@@ -131,7 +131,9 @@ def sample_pdf(bins, weights, n_samples, u=None, det=False):
     bins (N,B+1) interval edges, weights (N,B).  Returns (N,n_samples).  ``u`` (N,n) in [0,1)
     is consumed as given (the GPU kernel sorts it first; the merged output is identical)."""
     weights = weights + 1e-5
-    pdf = weights / weights.sum(-1, keepdim=True)
+    # normaliser accumulated in fp64 and rounded once (ISA-independent; torch's own fp32 sum order
+    # depends on the host's vector width).  cumsum already accumulates fp32 in fp64 on the CPU.
+    pdf = weights / weights.double().sum(-1, keepdim=True).to(weights.dtype)
     cdf = torch.cumsum(pdf, -1)
     cdf = torch.cat([torch.zeros_like(cdf[:, :1]), cdf], -1)  # (N,B+1)
     if u is None:

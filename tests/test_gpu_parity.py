@@ -21,7 +21,8 @@ def _close(a, b, atol=TOL, rel_scale=False, what=""):
     b = b.detach().float().cpu()
     assert a.shape == b.shape, (what, a.shape, b.shape)
     tol = atol * max(1.0, b.abs().max().item()) if rel_scale else atol
-    err = (a - b).abs().max().item() if a.numel() else 0.0
+    same = (a == b) | (torch.isnan(a) & torch.isnan(b))
+    err = torch.where(same, torch.zeros_like(a), (a - b).abs()).max().item() if a.numel() else 0.0
     assert err <= tol, f"{what}: max err {err:.3e} > {tol:.3e}"
     return err
 
@@ -276,8 +277,23 @@ def test_hierarchical_render_vs_oracle(K):
 # ------------------------------------------------------------------ train steps
 
 
+def _adam_step1_close(p, ref, g, g_ref, lr, what, eps=1e-8):
+    """Post-Adam parameters after ONE step from the same start point.  Adam's first update is
+    -lr * g/(|g|+eps) per element, so two gradients that agree to rounding level can still move an
+    element whose gradient is at the noise floor by up to 2 lr.  The allowed deviation per element is
+    exactly the update difference the two measured gradients imply, plus fp32 rounding."""
+    p, ref = p.detach().double().cpu(), ref.detach().double().cpu()
+    g, g_ref = g.detach().double().cpu(), g_ref.detach().double().cpu()
+    phi = lambda x: x / (x.abs() + eps)
+    bound = lr * (phi(g) - phi(g_ref)).abs() * 1.02 + 1e-6 * lr + 2.5e-7 * (1 + ref.abs())
+    err = (p - ref).abs()
+    bad = err > bound
+    assert not bad.any(), f"{what}: {int(bad.sum())} elements beyond the implied bound, max err {err.max():.3e}"
+
+
 def test_train_step_golden(net):
-    """Reference runtime_adapt train step: autograd through the HIP ops + torch Adam."""
+    """Reference runtime_adapt train step (runtime_adapt.py:286-310): autograd through the HIP ops,
+    MSE in linear colour space, clip_grad_norm_(1.0), torch Adam — vs the reference's golden step."""
     from nerf_amd import ray_rendering as rr
     from nerf_amd.losses import color_space_transformer
     from nerf_amd.vanilla import VanillaNeRF
@@ -291,23 +307,35 @@ def test_train_step_golden(net):
     loss = torch.nn.functional.mse_loss(a, b)
     assert abs(loss.item() - float(z["loss"])) < 1e-5
     loss.backward()
-    torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
-    opt.step()
+    gn = torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
+    assert abs(gn.item() - float(z["gnorm"])) < 1e-4 * float(z["gnorm"])
+    # the same step through the CPU oracle (itself pinned to this golden step in test_oracle_golden.py)
+    ot = O.OracleTrainer(mlp_params("w/"), lr_sigma=2e-3, lr_color=2e-3)
+    lref = ot.step(zr["rays"], z["gt"], 64, training=True, u_strat=zr["u"])
+    assert abs(lref - float(z["loss"])) < 1e-6
     named = dict(m.named_parameters())
-    for k, v in z.items():
+    for n, p in named.items():
+        _close(p.grad, ot.nets[0][n].grad, rel_scale=True, what=f"clipped grad {n}")
+    opt.step()
+    for n, p in named.items():
+        _adam_step1_close(p, ot.nets[0][n], p.grad, ot.nets[0][n].grad, 2e-3, what=f"post-Adam {n}")
+    for k, v in z.items():   # golden parameters: loose absolute bound (2 lr) + mean at rounding level
         if k.startswith("p/"):
-            _close(named[k[2:]], v, 2e-5, what=f"post-Adam {k}")
+            err = (named[k[2:]].detach().cpu() - v).abs()
+            assert err.max() <= 4e-3 and err.mean() <= 5e-6, (k, err.max().item(), err.mean().item())
 
 
 def test_engine_step_vs_oracle(K):
-    """Fused engine (two nets, 64+128, fused loss, clip, HIP Adam) vs the oracle trainer on identical u."""
-    from nerf_amd.vanilla import VanillaNeRF
+    """Fused engine (two nets, 64+128, fused loss, clip, HIP Adam) vs the oracle trainer on identical u:
+    per-step loss over 3 steps, first-step clipped gradients and post-Adam parameters of both nets."""
+    from nerf_amd.vanilla import VanillaNeRF, PackedLayout
     from nerf_amd.trainer import NeRFTrainer
     pc, pf = O.init_vanilla_params(1), O.init_vanilla_params(2)
     coarse = VanillaNeRF().load_reference_state(pc).to(DEV)
     fine = VanillaNeRF().load_reference_state(pf).to(DEV)
     tr = NeRFTrainer(coarse, fine, n_samples=64, n_importance=128, lr_sigma=2e-3, lr_color=1e-3)
     ot = O.OracleTrainer(pc, pf, lr_sigma=2e-3, lr_color=1e-3)
+    L = PackedLayout.get()
     zr = load("render")
     rays = zr["rays"]
     g = torch.Generator().manual_seed(5)
@@ -318,10 +346,16 @@ def test_engine_step_vs_oracle(K):
         loss = tr.step(rays.to(DEV), gt.to(DEV), seed=step, u_strat=us.to(DEV), u_pdf=up.to(DEV)).item()
         lref = ot.step(rays, gt, 64, n_importance=128, training=True, u_strat=us, u_pdf=up)
         assert abs(loss - lref) < 1e-5 + 1e-4 * lref, (step, loss, lref)
-    tr.sync_to_modules()
-    for k, (netm, refp) in enumerate(((coarse, ot.nets[0]), (fine, ot.nets[1]))):
-        for n, p in netm.named_parameters():
-            _close(p, refp[n], 5e-5, what=f"net{k} {n} after 3 steps")
+        if step == 0:
+            norm = tr.grads.double().norm().item()
+            coef = min(1.0, 1.0 / (norm + 1e-6))
+            for k in range(2):
+                gk = L.unpack(tr.g(k).detach().cpu() * coef)
+                pk = L.unpack(tr.w(k).detach().cpu())
+                for n, v in gk.items():
+                    _close(v, ot.nets[k][n].grad, rel_scale=True, what=f"net{k} grad {n}")
+                    lr = 1e-3 if n.startswith("color_mlp") else 2e-3
+                    _adam_step1_close(pk[n], ot.nets[k][n], v, ot.nets[k][n].grad, lr, what=f"net{k} {n} step 1")
 
 
 def test_adam_kernel_matches_torch(K):
