@@ -91,9 +91,12 @@ def main():
     tr = NeRFTrainer(coarse, fine, n_samples=a.samples, n_importance=a.importance, world_size=world, device=dev)
     rb = RayBatcher(scene, dev)
 
+    from nerf_amd.dp import shard_seed
+
     def one(step):
-        rays, gt = rb.batch(a.batch, seed=step * world + rank)  # disjoint per-rank batches
-        return tr.step(rays, gt, seed=step * world + rank)
+        sd = shard_seed(step, rank, world)  # disjoint per-rank ray batches
+        rays, gt = rb.batch(a.batch, seed=sd)
+        return tr.step(rays, gt, seed=sd)
 
     for s in range(a.warmup):
         loss = one(s)
@@ -159,7 +162,8 @@ def main():
         coarse.eval()
         fx, fy, cx, cy = scene.intrinsics
         img, _, _ = render_image(coarse, H=800, W=800, fx=fx, fy=fy, cx=cx, cy=cy, c2w=scene.test_poses[0],
-                                 near=2.0, far=6.0, ray_samples=a.samples, n_importance=a.importance)
+                                 near=2.0, far=6.0, ray_samples=a.samples, n_importance=a.importance,
+                                 fine_model=fine.eval())
         mse = ((img - scene.test_images[0].float() / 255.0) ** 2).mean().item()
         out["psnr_after_steps"] = round(-10 * math.log10(max(mse, 1e-8)), 3)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

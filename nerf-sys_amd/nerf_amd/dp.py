@@ -1,0 +1,26 @@
+"""Data-parallel scheme of the train step: rays shard across ranks, weights replicate,
+and the only exchange is one SUM all-reduce of the flat [grads | loss] buffer per step.
+
+The reference's own sharding idiom is rank-strided (`an/scripts/create_clusters.py:799`,
+`np.arange(rank, len, world)`); for random training batches the equivalent is a disjoint counter-RNG
+stream per (step, rank)."""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_seed(step: int, rank: int, world: int) -> int:
+    """Disjoint per-rank RNG stream for the ray draw of a step (rank-strided like create_clusters.py:799)."""
+    return step * world + rank
+
+
+def inv_count(n_local: int, world: int) -> float:
+    """MSE normaliser 1/(3 N_global): the SUM all-reduce of per-rank gradients is the global mean."""
+    return 1.0 / (3.0 * n_local * world)
+
+
+def allreduce_flat(buf: torch.Tensor, world: int) -> torch.Tensor:
+    if world > 1:
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+    return buf

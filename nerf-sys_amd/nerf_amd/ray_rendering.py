@@ -178,7 +178,8 @@ def render_image(model, *, H: int, W: int, fx: float, fy: float, cx: float, cy: 
                  near: Optional[float] = None, far: Optional[float] = None, params=None,
                  active_module: Optional[int] = None, ray_samples: int = 64, n_importance: int = 0,
                  chunk_points: int = 1 << 22, bg_color_default: str = "white", center_pixels: bool = True,
-                 ndc: Optional[Tuple[float, float]] = None, rays_per_chunk: int = 1 << 15, use_amp: bool = False):
+                 ndc: Optional[Tuple[float, float]] = None, rays_per_chunk: int = 1 << 15, use_amp: bool = False,
+                 fine_model=None):
     """ray_rendering.py:577-627 — rays from the fused HIP kernel, rendered in ray chunks.
     ``ndc=(focal, near_plane)`` converts rays to forward-facing NDC first (LLFF config)."""
     device = next(model.parameters()).device
@@ -192,7 +193,7 @@ def render_image(model, *, H: int, W: int, fx: float, fy: float, cx: float, cy: 
     for s in range(0, rays.shape[0], rays_per_chunk):
         rgb, depth, _, acc = render_rays(model, rays[s:s + rays_per_chunk], ray_samples=ray_samples, params=params,
                                          active_module=active_module, bg_color_default=bg_color_default,
-                                         chunk=chunk_points, n_importance=n_importance)
+                                         chunk=chunk_points, n_importance=n_importance, fine_model=fine_model)
         rgbs.append(rgb), depths.append(depth), accs.append(acc)
     rgb = torch.cat(rgbs).view(H, W, 3).float().clamp_(0, 1)
     return rgb, torch.cat(depths).view(-1), torch.cat(accs).view(-1)

@@ -20,9 +20,9 @@ from __future__ import annotations
 from typing import Optional
 
 import torch
-import torch.distributed as dist
 
 from . import kernels as K
+from .dp import allreduce_flat, inv_count as _inv_count
 from .vanilla import PackedLayout, VanillaNeRF
 
 _CS = ("linear", "srgb", "identity")
@@ -143,7 +143,7 @@ class NeRFTrainer:
         N = rays.shape[0]
         S, NI = self.S, self.n_imp
         bg = self._background(N)
-        inv_count = 1.0 / (3.0 * N * self.world_size)
+        inv_count = _inv_count(N, self.world_size)
         self.gbuf.zero_()
         fine_k = 1 if self.n_nets > 1 else 0
         # coarse forward
@@ -170,8 +170,7 @@ class NeRFTrainer:
                 self.timing["M"] = N * (S + NI)
         d_rs_c = K.composite_bwd(rs_c, t_c, bg, drgb_c, sigma_scale=self.sigma_scale)
         K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=(fine_k == 0 and NI > 0))
-        if self.world_size > 1:
-            dist.all_reduce(self.gbuf, op=dist.ReduceOp.SUM)
+        allreduce_flat(self.gbuf, self.world_size)
         self.step_count += 1
         if self.grad_clip is not None and self.grad_clip > 0:
             K.grad_sqnorm(self.grads, self.partials)

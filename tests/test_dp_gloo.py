@@ -1,0 +1,86 @@
+"""World-size-2 data-parallel check on the CPU (gloo): the trainer's exchange scheme — per-rank MSE
+normalised by 1/(3 N_global) and ONE SUM all-reduce of the flat packed [grads | loss] buffer — equals
+the single-process full-batch gradient and loss.  The per-rank gradient comes from the CPU oracle (the
+HIP kernels need a GPU); the packing, normaliser and all-reduce are the product's own code."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import nerf_oracle as O
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batch(n=32):
+    g = torch.Generator().manual_seed(7)
+    o = torch.tensor([0.0, -4.0, 0.5]).expand(n, 3)
+    d = torch.nn.functional.normalize(torch.randn(n, 3, generator=g) * 0.15 + torch.tensor([0.0, 1.0, -0.12]), dim=-1)
+    rays = torch.cat([o, d, torch.full((n, 1), 2.0), torch.full((n, 1), 6.0)], -1)
+    gt = torch.rand(n, 3, generator=g)
+    us = torch.rand(n, 16, generator=g)
+    return rays, gt, us
+
+
+def _flat_grad(p, rays, gt, us, inv_count):
+    from nerf_amd.vanilla import PackedLayout
+    L = PackedLayout.get()
+    pg = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    rgb = O.render_rays(pg, rays, 16, training=True, u_strat=us)[0]
+    a, b = O.color_space_transformer(rgb, gt, "linear")
+    loss = ((a - b) ** 2).sum() * inv_count
+    grads = torch.autograd.grad(loss, list(pg.values()))
+    flat = L.pack([g.detach() for g in grads]).detach()
+    return torch.cat([flat, loss.detach().view(1)])
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "nerf-sys_amd"), os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from nerf_amd.dp import allreduce_flat, inv_count, shard_seed
+    torch.set_num_threads(2)
+    rays, gt, us = _batch()
+    n_local = rays.shape[0] // world
+    sl = slice(rank * n_local, (rank + 1) * n_local)
+    buf = _flat_grad(O.init_vanilla_params(3), rays[sl], gt[sl], us[sl], inv_count(n_local, world))
+    allreduce_flat(buf, world)
+    seeds = [shard_seed(s, rank, world) for s in range(5)]
+    if rank == 0:
+        q.put((buf, seeds))
+    else:
+        q.put((None, seeds))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_allreduce_equals_full_batch():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    dp = next(b for b, _ in res if b is not None)
+    seeds = [s for _, s in res]
+    assert not set(seeds[0]) & set(seeds[1])  # disjoint per-rank ray streams
+    from nerf_amd.dp import inv_count
+    rays, gt, us = _batch()
+    full = _flat_grad(O.init_vanilla_params(3), rays, gt, us, inv_count(rays.shape[0], 1))
+    torch.testing.assert_close(dp, full, rtol=1e-4, atol=1e-7)
