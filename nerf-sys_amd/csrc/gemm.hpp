@@ -28,19 +28,23 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // ------------------------------------------------------------------------------------------ gemm_nt
 // Requirements (checked by the host wrapper): M % BM == 0, N % BN == 0, K % 16 == 0, lda/ldb/ldc/ldm % 4
 // == 0, 16-byte aligned A/B.
-template <int BM, int BN, int WAVES_M, int EPI>
-__global__ __launch_bounds__(256) void gemm_nt_kernel(const float* __restrict__ A, int lda,
+template <int BM, int BN, int WAVES_M, int EPI, int MINW = 1, int BK = 16, int NBUF = 2>
+__global__ __launch_bounds__(256, MINW) void gemm_nt_kernel(const float* __restrict__ A, int lda,
                                                       const float* __restrict__ B, int ldb,
                                                       const float* __restrict__ bias, float* __restrict__ C, int ldc,
-                                                      const float* __restrict__ mask, int ldm, int K, int n_ntiles) {
+                                                      const uint32_t* __restrict__ mbits, int ldmb,
+                                                      uint32_t* __restrict__ mbits_out, int K, int n_ntiles) {
   constexpr int WAVES_N = 4 / WAVES_M;
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int TM = WTM / 32, TN = WTN / 32;
   static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0, "wave tile");
-  constexpr int BK = 16, LS = 20;  // LDS row pitch in floats
-  constexpr int A_F4 = BM * BK / 4, B_F4 = BN * BK / 4;
+  static_assert(BK == 16 || BK == 32, "k-slab");
+  constexpr int LS = BK + 4;         // LDS row pitch (floats): 80 / 144 B, 16 rows -> 16 distinct bank slots
+  constexpr int C4 = BK / 4;         // float4 per row per slab
+  constexpr int HK = BK / 2;         // k per lane half per slab
+  constexpr int A_F4 = BM * C4, B_F4 = BN * C4;
   constexpr int A_PER = (A_F4 + 255) / 256, B_PER = (B_F4 + 255) / 256;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LS];
+  __shared__ __attribute__((aligned(16))) float smem[NBUF * (BM + BN) * LS];
 
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
@@ -58,12 +62,12 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const float* __restrict__ 
   _Pragma("unroll") for (int i = 0; i < A_PER; ++i) {                                         \
     const int f = tid + 256 * i;                                                               \
     if (A_F4 % 256 == 0 || f < A_F4)                                                           \
-      ra[i] = *reinterpret_cast<const float4*>(Ab + (int64_t)(f >> 2) * lda + (k0_) + ((f & 3) << 2)); \
+      ra[i] = *reinterpret_cast<const float4*>(Ab + (int64_t)(f / C4) * lda + (k0_) + (f % C4) * 4); \
   }                                                                                            \
   _Pragma("unroll") for (int i = 0; i < B_PER; ++i) {                                         \
     const int f = tid + 256 * i;                                                               \
     if (B_F4 % 256 == 0 || f < B_F4)                                                           \
-      rb[i] = *reinterpret_cast<const float4*>(Bb + (int64_t)(f >> 2) * ldb + (k0_) + ((f & 3) << 2)); \
+      rb[i] = *reinterpret_cast<const float4*>(Bb + (int64_t)(f / C4) * ldb + (k0_) + (f % C4) * 4); \
   }
 #define NT_SSTORE(buf_)                                                                        \
   {                                                                                            \
@@ -72,12 +76,12 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const float* __restrict__ 
     _Pragma("unroll") for (int i = 0; i < A_PER; ++i) {                                       \
       const int f = tid + 256 * i;                                                             \
       if (A_F4 % 256 == 0 || f < A_F4)                                                         \
-        *reinterpret_cast<float4*>(As_ + (f >> 2) * LS + ((f & 3) << 2)) = ra[i];              \
+        *reinterpret_cast<float4*>(As_ + (f / C4) * LS + (f % C4) * 4) = ra[i];                \
     }                                                                                          \
     _Pragma("unroll") for (int i = 0; i < B_PER; ++i) {                                       \
       const int f = tid + 256 * i;                                                             \
       if (B_F4 % 256 == 0 || f < B_F4)                                                         \
-        *reinterpret_cast<float4*>(Bs_ + (f >> 2) * LS + ((f & 3) << 2)) = rb[i];              \
+        *reinterpret_cast<float4*>(Bs_ + (f / C4) * LS + (f % C4) * 4) = rb[i];                \
     }                                                                                          \
   }
 
@@ -94,56 +98,74 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const float* __restrict__ 
   NT_SSTORE(0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
+    const int cur = NBUF == 2 ? (kt & 1) : 0;
     NT_GLOAD((kt + 1 < nk ? kt + 1 : kt) * BK);
     const float* As = smem + cur * (BM + BN) * LS;
     const float* Bs = As + BM * LS;
-    float af[TM][8], bf[TN][8];
+    // lane half h owns k = h*HK + s of the slab; its k-values of a row are read 4 at a time
 #pragma unroll
-    for (int a = 0; a < TM; ++a) {
-      const float* p = As + (wm * WTM + a * 32 + li) * LS + 8 * lh;
-      const float4 x0 = *reinterpret_cast<const float4*>(p);
-      const float4 x1 = *reinterpret_cast<const float4*>(p + 4);
-      af[a][0] = x0.x; af[a][1] = x0.y; af[a][2] = x0.z; af[a][3] = x0.w;
-      af[a][4] = x1.x; af[a][5] = x1.y; af[a][6] = x1.z; af[a][7] = x1.w;
-    }
-#pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const float* p = Bs + (wn * WTN + b * 32 + li) * LS + 8 * lh;
-      const float4 x0 = *reinterpret_cast<const float4*>(p);
-      const float4 x1 = *reinterpret_cast<const float4*>(p + 4);
-      bf[b][0] = x0.x; bf[b][1] = x0.y; bf[b][2] = x0.z; bf[b][3] = x0.w;
-      bf[b][4] = x1.x; bf[b][5] = x1.y; bf[b][6] = x1.z; bf[b][7] = x1.w;
-    }
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
+    for (int hh = 0; hh < HK / 4; ++hh) {
+      float4 af[TM], bf[TN];
 #pragma unroll
       for (int a = 0; a < TM; ++a)
+        af[a] = *reinterpret_cast<const float4*>(As + (wm * WTM + a * 32 + li) * LS + HK * lh + 4 * hh);
 #pragma unroll
-        for (int b = 0; b < TN; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
-    NT_SSTORE(cur ^ 1);
+      for (int b = 0; b < TN; ++b)
+        bf[b] = *reinterpret_cast<const float4*>(Bs + (wn * WTN + b * 32 + li) * LS + HK * lh + 4 * hh);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)  // swapped operands: the tile is C^T (i = n, j = m)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(bf[b][s], af[a][s], acc[a][b], 0, 0, 0);
+    }
+    if (NBUF == 1) __syncthreads();  // single buffer: every wave done reading before the overwrite
+    NT_SSTORE(NBUF == 2 ? (cur ^ 1) : 0);
     __syncthreads();
   }
 #undef NT_GLOAD
 #undef NT_SSTORE
 
-  // epilogue: lane holds column li, rows (r&3) + 8(r>>2) + 4 lh of each 32x32 tile
+  // epilogue.  The MFMA computed C^T, so lane li holds ONE output row m = ... + li and register
+  // r = 4q + e holds column 8q + 4 lh + e of the 32-column tile: four float4 runs per row -> 16-B stores.
+  // ReLU masks travel as bits: the forward writes word g = column/32 of row m (the lane's 16 bits OR'd
+  // with its partner lane's li+32), the input-gradient GEMM reads one word per row instead of 32 floats.
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
-    const int n = n0 + wn * WTN + b * 32 + li;
-    float bv = 0.f;
-    if (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) bv = bias[n];
+    const int nb = n0 + wn * WTN + b * 32;
+    const int g = nb >> 5;
+    float4 bv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) bv[q] = *reinterpret_cast<const float4*>(bias + nb + 8 * q + 4 * lh);
+    }
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
+      const int64_t m = m0 + wm * WTM + a * 32 + li;
+      uint32_t word = 0;
+      if (EPI == EPI_MASK) word = mbits[m * ldmb + g];
+      float* crow = C + m * ldc + nb + 4 * lh;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t m = m0 + wm * WTM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        float v = acc[a][b][r];
-        if (EPI == EPI_BIAS) v += bv;
-        if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
-        if (EPI == EPI_MASK) v = mask[m * ldm + n] > 0.f ? v : 0.f;
-        C[m * ldc + n] = v;
+      for (int q = 0; q < 4; ++q) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[a][b][4 * q + e];
+          const float bb = e == 0 ? bv[q].x : (e == 1 ? bv[q].y : (e == 2 ? bv[q].z : bv[q].w));
+          if (EPI == EPI_BIAS) v[e] += bb;
+          if (EPI == EPI_BIAS_RELU) {
+            v[e] = fmaxf(v[e] + bb, 0.f);
+            word |= (v[e] > 0.f ? 1u : 0u) << (8 * q + 4 * lh + e);
+          }
+          if (EPI == EPI_MASK) v[e] = ((word >> (8 * q + 4 * lh + e)) & 1u) ? v[e] : 0.f;
+        }
+        *reinterpret_cast<float4*>(crow + 8 * q) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+      if (EPI == EPI_BIAS_RELU && mbits_out) {
+        word |= __shfl_xor(word, 32, 64);
+        if (lh == 0) mbits_out[m * ldmb + g] = word;
       }
     }
   }
@@ -159,7 +181,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const float* __restrict
                                                          const float* __restrict__ X, int ldx,
                                                          float* __restrict__ P, int ldp, float* __restrict__ Pb,
                                                          int64_t slab, int64_t rows_per_split, int64_t M,
-                                                         int n_ktiles) {
+                                                         int n_ktiles, int n_tiles) {
   constexpr int WAVES_K = 4 / WAVES_N;
   constexpr int WTN = BN / WAVES_N, WTK = BK / WAVES_K;
   constexpr int TM = WTN / 32, TN = WTK / 32;
@@ -169,8 +191,12 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const float* __restrict
   constexpr int G_PER = (G_F4 + 255) / 256, X_PER = (X_F4 + 255) / 256;
   __shared__ __attribute__((aligned(16))) float smem[2 * MR * (BN + BK)];
 
-  const int nt = blockIdx.x / n_ktiles, kt = blockIdx.x - nt * n_ktiles;
-  const int s = blockIdx.y;
+  // 1-D grid of (split, tile) pairs, tile fastest, remapped so that the output tiles of one split are
+  // consecutive on ONE XCD: they stream the same G / X rows, which then come from that XCD's L2 once.
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int s = lin / n_tiles;
+  const int tile = lin - s * n_tiles;
+  const int nt = tile / n_ktiles, kt = tile - nt * n_ktiles;
   const int n0 = nt * BN, k0 = kt * BK;
   const int64_t r0 = (int64_t)s * rows_per_split;
   int64_t r1 = r0 + rows_per_split;

@@ -69,6 +69,7 @@ int n_splits(int64_t Mp) {
 struct WS {
   int64_t Mp;
   float *X3E, *Y[8], *O16, *CIN, *C0, *O3;
+  uint32_t *MB[8], *MC0;  // ReLU bitmasks of the trunk outputs [Mp][8] and colour layer 0 [Mp][4]
   // backward
   float *dA, *dB, *dO16, *dO3, *dCIN, *dC0, *WT, *partial;
   int S;
@@ -100,6 +101,8 @@ WS carve(void* base, int64_t M, int training) {
   w.C0 = take(Mp * 128);
   w.O3 = take(Mp * 32);
   if (training) {
+    for (int i = 0; i < 8; ++i) w.MB[i] = reinterpret_cast<uint32_t*>(take(Mp * 8));
+    w.MC0 = reinterpret_cast<uint32_t*>(take(Mp * 4));
     w.dA = take(Mp * 256);
     w.dB = take(Mp * 256);
     w.dO16 = take(Mp * 32);
@@ -258,22 +261,27 @@ __global__ void transpose_kernel(TJobs jobs) {
 
 // ------------------------------------------------------------------ launch helpers
 
+// MINW = 4 waves per SIMD: the register budget (128 unified VGPR+AGPR per lane) that lets four 256-thread
+// workgroups share a CU; measured +9..12 % over the unconstrained allocation (tools/gemm_bench.hip).
 template <int BM, int BN, int WAVES_M, int EPI>
 int launch_nt(const float* A, int lda, const float* B, int ldb, const float* bias, float* C, int ldc,
-              const float* mask, int ldm, int64_t M, int N, int K, hipStream_t st) {
+              const uint32_t* mbits, uint32_t* mbits_out, int64_t M, int N, int K, hipStream_t st) {
   if (M % BM || N % BN || K % 16) return NERF_E_ARG;
   const int ntn = N / BN;
   const int64_t nblk = (M / BM) * ntn;
-  gemm_nt_kernel<BM, BN, WAVES_M, EPI><<<(unsigned)nblk, 256, 0, st>>>(A, lda, B, ldb, bias, C, ldc, mask, ldm, K, ntn);
+  gemm_nt_kernel<BM, BN, WAVES_M, EPI, (BN >= 128 ? 4 : 1)><<<(unsigned)nblk, 256, 0, st>>>(A, lda, B, ldb, bias, C, ldc, mbits,
+                                                                           N / 32, mbits_out, K, ntn);
   return NERF_OK;
 }
 
-// dispatch on N for the trunk-like GEMMs
+// dispatch on N for the trunk-like GEMMs.  mbits: ReLU bitmask [M][N/32] read by EPI_MASK; mbits_out:
+// bitmask written by EPI_BIAS_RELU (nullable).
 template <int EPI>
-int nt(const float* A, int lda, const float* B, int ldb, const float* bias, float* C, int ldc, const float* mask,
-       int ldm, int64_t M, int N, int K, hipStream_t st) {
-  if (N == 256 || N == 128) return launch_nt<128, 128, 2, EPI>(A, lda, B, ldb, bias, C, ldc, mask, ldm, M, N, K, st);
-  if (N == 32) return launch_nt<256, 32, 4, EPI>(A, lda, B, ldb, bias, C, ldc, mask, ldm, M, N, K, st);
+int nt(const float* A, int lda, const float* B, int ldb, const float* bias, float* C, int ldc, const uint32_t* mbits,
+       uint32_t* mbits_out, int64_t M, int N, int K, hipStream_t st) {
+  if (N == 256 || N == 128)
+    return launch_nt<128, 128, 2, EPI>(A, lda, B, ldb, bias, C, ldc, mbits, mbits_out, M, N, K, st);
+  if (N == 32) return launch_nt<256, 32, 4, EPI>(A, lda, B, ldb, bias, C, ldc, mbits, mbits_out, M, N, K, st);
   return NERF_E_ARG;
 }
 
@@ -285,14 +293,14 @@ int wgrad(const float* G, int ldg, const float* X, int ldx, int tensor_w, const 
   const int64_t slab = L.total;
   if (N % 32 || K % 32) return NERF_E_ARG;
   if (N >= 128 && K % 128 == 0) {
-    dim3 grid((N / 128) * (K / 128), w.S);
-    gemm_wgrad_kernel<128, 128, 2><<<grid, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, K / 128);
+    const int nt = (N / 128) * (K / 128);
+    gemm_wgrad_kernel<128, 128, 2><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, K / 128, nt);
   } else if (N >= 128 && K % 64 == 0) {
-    dim3 grid((N / 128) * (K / 64), w.S);
-    gemm_wgrad_kernel<128, 64, 2><<<grid, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, K / 64);
+    const int nt = (N / 128) * (K / 64);
+    gemm_wgrad_kernel<128, 64, 2><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, K / 64, nt);
   } else if (N == 32 && K % 128 == 0) {
-    dim3 grid(K / 128, w.S);
-    gemm_wgrad_kernel<32, 128, 1><<<grid, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, K / 128);
+    const int nt = K / 128;
+    gemm_wgrad_kernel<32, 128, 1><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, K / 128, nt);
   } else {
     return NERF_E_ARG;
   }
@@ -345,16 +353,18 @@ extern "C" int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* 
     const int ld_out = training ? ld_of(W, i) : ((i % 2 == 0) ? 256 : 320);
     if (i == 4) { in = W.X3E; ld_in = 320; }  // cat([h3, enc]) lives in X3E
     if (ev) (void)hipEventRecord(ev[2 * i], st);
-    TRY(nt<EPI_BIAS_RELU>(in, ld_in, Wt(2 * i), KPAD[i], Wt(2 * i + 1), out, ld_out, nullptr, 0, Mp, 256, KPAD[i], st));
+    TRY(nt<EPI_BIAS_RELU>(in, ld_in, Wt(2 * i), KPAD[i], Wt(2 * i + 1), out, ld_out, nullptr,
+                          training ? W.MB[i] : nullptr, Mp, 256, KPAD[i], st));
     if (ev) (void)hipEventRecord(ev[2 * i + 1], st);
     in = out;
     ld_in = ld_out;
   }
   // heads
-  TRY(nt<EPI_BIAS>(in, ld_in, Wt(16), 256, Wt(17), W.O16, 32, nullptr, 0, Mp, 32, 256, st));
+  TRY(nt<EPI_BIAS>(in, ld_in, Wt(16), 256, Wt(17), W.O16, 32, nullptr, nullptr, Mp, 32, 256, st));
   build_cin_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(x_d, W.O16, M, Mp, W.CIN);
-  TRY(nt<EPI_BIAS_RELU>(W.CIN, 64, Wt(18), 64, Wt(19), W.C0, 128, nullptr, 0, Mp, 128, 64, st));
-  TRY(nt<EPI_BIAS>(W.C0, 128, Wt(20), 128, Wt(21), W.O3, 32, nullptr, 0, Mp, 32, 128, st));
+  TRY(nt<EPI_BIAS_RELU>(W.CIN, 64, Wt(18), 64, Wt(19), W.C0, 128, nullptr, training ? W.MC0 : nullptr, Mp, 128, 64,
+                        st));
+  TRY(nt<EPI_BIAS>(W.C0, 128, Wt(20), 128, Wt(21), W.O3, 32, nullptr, nullptr, Mp, 32, 128, st));
   head_out_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(W.O3, W.O16, M, rgb_sigma);
   return nerf_launch_status();
 }
@@ -391,15 +401,15 @@ extern "C" int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma,
 
   head_out_bwd_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(d_rgb_sigma, W.O3, W.O16, M, Mp, W.dO3, W.dO16);
   // colour MLP
-  TRY(nt<EPI_MASK>(W.dO3, 32, Wc1t, 32, nullptr, W.dC0, 128, W.C0, 128, Mp, 128, 32, st));
+  TRY(nt<EPI_MASK>(W.dO3, 32, Wc1t, 32, nullptr, W.dC0, 128, W.MC0, nullptr, Mp, 128, 32, st));
   TRY(wgrad(W.dO3, 32, W.C0, 128, 20, W, 32, 128, st));
-  TRY(nt<EPI_NONE>(W.dC0, 128, Wc0t, 128, nullptr, W.dCIN, 32, nullptr, 0, Mp, 32, 128, st));
+  TRY(nt<EPI_NONE>(W.dC0, 128, Wc0t, 128, nullptr, W.dCIN, 32, nullptr, nullptr, Mp, 32, 128, st));
   TRY(wgrad(W.dC0, 128, W.CIN, 64, 18, W, 128, 64, st));
   geo_bwd_kernel<<<(unsigned)nerf_cdiv(Mp * 15, 256), 256, 0, st>>>(W.dCIN, Mp, W.dO16);
   // heads -> dZ7
   float* dcur = W.dA;
   float* dnext = W.dB;
-  TRY(nt<EPI_MASK>(W.dO16, 32, Wht, 32, nullptr, dcur, 256, W.Y[7], 256, Mp, 256, 32, st));
+  TRY(nt<EPI_MASK>(W.dO16, 32, Wht, 32, nullptr, dcur, 256, W.MB[7], nullptr, Mp, 256, 32, st));
   TRY(wgrad(W.dO16, 32, W.Y[7], 256, 16, W, 32, 256, st));
   // trunk
   for (int i = 7; i >= 0; --i) {
@@ -410,7 +420,7 @@ extern "C" int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma,
     if (ev) (void)hipEventRecord(ev[4 * i + 1], st);
     if (i > 0) {
       if (ev) (void)hipEventRecord(ev[4 * i + 2], st);
-      TRY(nt<EPI_MASK>(dcur, 256, WTi[i], 256, nullptr, dnext, 256, W.Y[i - 1], ld_of(W, i - 1), Mp, 256, 256, st));
+      TRY(nt<EPI_MASK>(dcur, 256, WTi[i], 256, nullptr, dnext, 256, W.MB[i - 1], nullptr, Mp, 256, 256, st));
       if (ev) (void)hipEventRecord(ev[4 * i + 3], st);
       float* t = dcur; dcur = dnext; dnext = t;
     }

@@ -1,0 +1,65 @@
+"""Per-launch HBM bytes of the bench's dominant kernel classes from the two rocprofv3 PMC passes.
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KB) counts exactly half of the bytes of a
+16-B/lane coalesced streaming read -> x2 (our GEMM operands are float4 loads); WRITE_SIZE (KB) is exact
+for 16-B/lane stores; our GEMM epilogue stores 4 B/lane in 128-B row segments, so it is calibrated
+against the known output volume M*256*4 of the same launch (printed as write_calib).
+Writes profiles/traffic.json {class: bytes per launch} for the fine-net trunk launches (M = 786,432)."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+root = sys.argv[1]
+M_FINE = 4096 * 192
+CLASSES = {
+    "gemm_nt fwd (trunk 256x256, bias+ReLU)": ("gemm_nt_kernel<128, 128, 2, 1>", 320 * 0),
+    "gemm_nt dgrad (trunk 256x256, ReLU mask)": ("gemm_nt_kernel<128, 128, 2, 2>", 0),
+    "gemm_wgrad (trunk 256x256, split-M)": ("gemm_wgrad_kernel<128, 128, 2>", 0),
+}
+
+
+def load(counter):
+    files = glob.glob(os.path.join(root, counter, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {root}/{counter}")
+    rows = list(csv.DictReader(open(files[0])))
+    return rows
+
+
+def per_kernel(rows):
+    out = defaultdict(list)
+    for r in rows:
+        name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
+        grid = int(float(r.get("Grid_Size") or r.get("Grid_Size_X") or 0))
+        val = float(r.get("Counter_Value") or 0)
+        out[(name, grid)].append(val)
+    return out
+
+
+fetch = per_kernel(load("FETCH_SIZE"))
+write = per_kernel(load("WRITE_SIZE"))
+res, detail = {}, {}
+for cls, (pat, _) in CLASSES.items():
+    # the fine-net trunk launches are the ones with the largest grid of that kernel
+    keys = [k for k in fetch if pat in k[0]]
+    if not keys:
+        continue
+    gmax = max(k[1] for k in keys)
+    kf = [k for k in keys if k[1] == gmax]
+    fvals = [v for k in kf for v in fetch[k]]
+    wvals = [v for k in kf for v in write.get(k, [])]
+    fb = 2.0 * 1024 * sum(fvals) / len(fvals)
+    wb = 1024 * sum(wvals) / max(1, len(wvals))
+    known_w = M_FINE * 256 * 4 if "wgrad" not in cls else None
+    calib = (known_w / wb) if (known_w and wb) else 1.0
+    res[cls] = round(fb + wb * calib)
+    detail[cls] = {"fetch_bytes_x2": round(fb), "write_bytes_raw": round(wb), "write_calib": round(calib, 3),
+                   "launches": len(fvals), "grid": gmax}
+print(json.dumps(detail, indent=1))
+os.makedirs("profiles", exist_ok=True)
+json.dump(res, open("profiles/traffic.json", "w"), indent=1)
+json.dump(detail, open(os.path.join(root, "traffic_detail.json"), "w"), indent=1)
+print(json.dumps(res))

@@ -1,0 +1,12 @@
+#!/bin/bash
+# HBM traffic of the bench's kernels from rocprofv3 PMC counters: FETCH_SIZE and WRITE_SIZE in separate
+# passes (MI355X_MICROARCH.md: TCC slots — they do not fit one pass), kernel-trace only, no other tracing.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+mkdir -p gpurun_out/pmc
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d gpurun_out/pmc/$C -o run -- \
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --train-views 4 > gpurun_out/pmc/$C.log 2>&1 || { tail -20 gpurun_out/pmc/$C.log; exit 1; }
+done
+python3 tools/pmc_parse.py gpurun_out/pmc
