@@ -28,7 +28,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // ------------------------------------------------------------------------------------------ gemm_nt
 // Requirements (checked by the host wrapper): M % BM == 0, N % BN == 0, K % 16 == 0, lda/ldb/ldc/ldm % 4
 // == 0, 16-byte aligned A/B.
-template <int BM, int BN, int WAVES_M, int EPI, int MINW = 1, int BK = 16, int NBUF = 2>
+template <int BM, int BN, int WAVES_M, int EPI, int MINW = 1, int BK = 16, int NBUF = 2, int PIN = 0>
 __global__ __launch_bounds__(256, MINW) void gemm_nt_kernel(const float* __restrict__ A, int lda,
                                                       const float* __restrict__ B, int ldb,
                                                       const float* __restrict__ bias, float* __restrict__ C, int ldc,
@@ -100,11 +100,15 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_kernel(const float* __restr
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = NBUF == 2 ? (kt & 1) : 0;
     NT_GLOAD((kt + 1 < nk ? kt + 1 : kt) * BK);
+    // pin the prefetch ABOVE the MFMA block: left alone, hipcc sinks these loads below the MFMAs (to
+    // shorten register live ranges) and then waits on them at once, exposing the full HBM latency.
+    if (PIN) __builtin_amdgcn_sched_barrier(0);
     const float* As = smem + cur * (BM + BN) * LS;
     const float* Bs = As + BM * LS;
     // lane half h owns k = h*HK + s of the slab; its k-values of a row are read 4 at a time
 #pragma unroll
     for (int hh = 0; hh < HK / 4; ++hh) {
+      if (PIN >= 2 && hh > 0) __builtin_amdgcn_sched_barrier(0);
       float4 af[TM], bf[TN];
 #pragma unroll
       for (int a = 0; a < TM; ++a)

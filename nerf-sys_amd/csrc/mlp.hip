@@ -123,30 +123,34 @@ inline int ld_of(const WS& w, int i) { return (i == 3) ? 320 : 256; }
 // ------------------------------------------------------------------ elementwise kernels
 
 // xyz positional encoding of x_d[:, :3] into X3E cols 256..319 (pad col 319 = 0; rows >= M zero).
+// One thread per sample row: the 64 encoded values leave as 16 float4 stores (256 contiguous bytes).
 __global__ void pe_xyz_kernel(const float* __restrict__ xd, int64_t M, int64_t Mp, float* __restrict__ X3E) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (row, dim)
-  if (idx >= Mp * 3) return;
-  const int64_t m = idx / 3;
-  const int k = (int)(idx - m * 3);
-  float* q = X3E + m * 320 + 256;
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= Mp) return;
+  float4* q4 = reinterpret_cast<float4*>(X3E + m * 320 + 256);
   if (m >= M) {
-    for (int c = k; c < 64; c += 3) q[c] = 0.f;
-    if (k == 0) q[63] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) q4[c] = make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
-  const float v = xd[m * 6 + k];
-  q[k] = v;
-  float* pe = q + 3 + k * 20;
-  float band = 1.0f;
+  float v[64];
+  const float x[3] = {xd[m * 6], xd[m * 6 + 1], xd[m * 6 + 2]};
 #pragma unroll
-  for (int l = 0; l < 10; ++l) {
-    float s, c;
-    sincosf(v * band, &s, &c);
-    pe[l] = c;
-    pe[10 + l] = s;
-    band *= 2.0f;
+  for (int k = 0; k < 3; ++k) {
+    v[k] = x[k];
+    float band = 1.0f;
+#pragma unroll
+    for (int l = 0; l < 10; ++l) {
+      float s, c;
+      sincosf(x[k] * band, &s, &c);
+      v[3 + k * 20 + l] = c;
+      v[3 + k * 20 + 10 + l] = s;
+      band *= 2.0f;
+    }
   }
-  if (k == 0) q[63] = 0.f;
+  v[63] = 0.f;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) q4[c] = make_float4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
 }
 
 // CIN[m] = [O16[m][1..15], direction encoding (27), zeros]
@@ -292,6 +296,19 @@ int wgrad(const float* G, int ldg, const float* X, int ldx, int tensor_w, const 
   const int ldp = L.cols[tensor_w];
   const int64_t slab = L.total;
   if (N % 32 || K % 32) return NERF_E_ARG;
+  if (N == 256 && K == 64) {  // trunk.0: one 256x64 tile per split (4 waves of 64x64)
+    gemm_wgrad_kernel<256, 64, 4><<<w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, 1, 1);
+    return NERF_OK;
+  }
+  if (N >= 128 && K > 128 && K % 128 == 64) {  // trunk.4 (K = 320): 128x128 tiles + one 128x64 column
+    const int kb = K - 64;
+    const int e = wgrad(G, ldg, X, ldx, tensor_w, w, N, kb, st);
+    if (e != NERF_OK) return e;
+    const int nt = N / 128;
+    gemm_wgrad_kernel<128, 64, 2><<<nt * w.S, 256, 0, st>>>(G, ldg, X + kb, ldx, P + kb, ldp, nullptr, slab, w.rps,
+                                                           w.Mp, 1, nt);
+    return NERF_OK;
+  }
   if (N >= 128 && K % 128 == 0) {
     const int nt = (N / 128) * (K / 128);
     gemm_wgrad_kernel<128, 128, 2><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, K / 128, nt);
@@ -344,7 +361,7 @@ extern "C" int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* 
   const int64_t Mp = W.Mp;
   auto Wt = [&](int t) { return w + L.off[t]; };
 
-  pe_xyz_kernel<<<(unsigned)nerf_cdiv(Mp * 3, 256), 256, 0, st>>>(x_d, M, Mp, W.X3E);
+  pe_xyz_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(x_d, M, Mp, W.X3E);
   // trunk
   const float* in = W.X3E + 256;
   int ld_in = 320;

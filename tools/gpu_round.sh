@@ -17,7 +17,7 @@ if [[ $STEP == all || $STEP == bench ]]; then
 fi
 if [[ $STEP == all || $STEP == prof ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-    python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
+    python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --train-views 8 > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
   tail -2 gpurun_out/prof.log
   find gpurun_out/prof -name "*kernel_stats.csv" | head -3
 fi
