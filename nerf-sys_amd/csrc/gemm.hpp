@@ -25,6 +25,12 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
+template <int TM, int TN, int WTM, int WTN, int EPI>
+__device__ __forceinline__ void nt_epilogue(const nerf_f32x16 (&acc)[TM][TN], int64_t mw, int nw, int li, int lh,
+                                            const float* __restrict__ bias, float* __restrict__ C, int ldc,
+                                            const uint32_t* __restrict__ mbits, int ldmb,
+                                            uint32_t* __restrict__ mbits_out);
+
 // ------------------------------------------------------------------------------------------ gemm_nt
 // Requirements (checked by the host wrapper): M % BM == 0, N % BN == 0, K % 16 == 0, lda/ldb/ldc/ldm % 4
 // == 0, 16-byte aligned A/B.
@@ -130,14 +136,21 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_kernel(const float* __restr
   }
 #undef NT_GLOAD
 #undef NT_SSTORE
+  nt_epilogue<TM, TN, WTM, WTN, EPI>(acc, m0 + wm * WTM, n0 + wn * WTN, li, lh, bias, C, ldc, mbits, ldmb, mbits_out);
+}
 
-  // epilogue.  The MFMA computed C^T, so lane li holds ONE output row m = ... + li and register
-  // r = 4q + e holds column 8q + 4 lh + e of the 32-column tile: four float4 runs per row -> 16-B stores.
-  // ReLU masks travel as bits: the forward writes word g = column/32 of row m (the lane's 16 bits OR'd
-  // with its partner lane's li+32), the input-gradient GEMM reads one word per row instead of 32 floats.
+// epilogue.  The MFMA computed C^T, so lane li holds ONE output row m = ... + li and register
+// r = 4q + e holds column 8q + 4 lh + e of the 32-column tile: four float4 runs per row -> 16-B stores.
+// ReLU masks travel as bits: the forward writes word g = column/32 of row m (the lane's 16 bits OR'd
+// with its partner lane's li+32), the input-gradient GEMM reads one word per row instead of 32 floats.
+template <int TM, int TN, int WTM, int WTN, int EPI>
+__device__ __forceinline__ void nt_epilogue(const nerf_f32x16 (&acc)[TM][TN], int64_t mw, int nw, int li, int lh,
+                                            const float* __restrict__ bias, float* __restrict__ C, int ldc,
+                                            const uint32_t* __restrict__ mbits, int ldmb,
+                                            uint32_t* __restrict__ mbits_out) {
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
-    const int nb = n0 + wn * WTN + b * 32;
+    const int nb = nw + b * 32;
     const int g = nb >> 5;
     float4 bv[4];
 #pragma unroll
@@ -147,7 +160,7 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_kernel(const float* __restr
     }
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
-      const int64_t m = m0 + wm * WTM + a * 32 + li;
+      const int64_t m = mw + a * 32 + li;
       uint32_t word = 0;
       if (EPI == EPI_MASK) word = mbits[m * ldmb + g];
       float* crow = C + m * ldc + nb + 4 * lh;

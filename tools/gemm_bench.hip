@@ -178,8 +178,7 @@ int main(int argc, char** argv) {
   const double flop = 2.0 * M * N * K;
   struct V { const char* name; std::vector<float> ms; };
   std::vector<V> vs = {{"fwd relu+bits (lib)", {}}, {"dgrad bits (lib)", {}}, {"wgrad (lib)", {}},
-                       {"fwd pin1", {}}, {"fwd pin2", {}}, {"dgrad pin1", {}}, {"dgrad pin2", {}},
-                       {"fwd pin1 lb3", {}}, {"fwd pin2 lb2", {}}};
+                       };
   auto run = [&](int v) {
     const int ntn = N / 128; const unsigned nb = (unsigned)((M / 128) * ntn);
     switch (v) {
@@ -187,12 +186,6 @@ int main(int argc, char** argv) {
       case 1: gemm_nt_kernel<128, 128, 2, EPI_MASK, 4><<<nb, 256>>>(A, K, B, K, bias, C, N, mb, 8, nullptr, K, ntn); break;
       case 2: { const int nt = 4; const int64_t rps = M / S;
         gemm_wgrad_kernel<128, 128, 2><<<nt * S, 256>>>(A, K, C, N, P, 256, P + 65536, slab, rps, M, 2, nt); break; }
-      case 3: gemm_nt_kernel<128, 128, 2, EPI_BIAS_RELU, 4, 16, 2, 1><<<nb, 256>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, K, ntn); break;
-      case 4: gemm_nt_kernel<128, 128, 2, EPI_BIAS_RELU, 4, 16, 2, 2><<<nb, 256>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, K, ntn); break;
-      case 5: gemm_nt_kernel<128, 128, 2, EPI_MASK, 4, 16, 2, 1><<<nb, 256>>>(A, K, B, K, bias, C, N, mb, 8, nullptr, K, ntn); break;
-      case 6: gemm_nt_kernel<128, 128, 2, EPI_MASK, 4, 16, 2, 2><<<nb, 256>>>(A, K, B, K, bias, C, N, mb, 8, nullptr, K, ntn); break;
-      case 7: gemm_nt_kernel<128, 128, 2, EPI_BIAS_RELU, 3, 16, 2, 1><<<nb, 256>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, K, ntn); break;
-      case 8: gemm_nt_kernel<128, 128, 2, EPI_BIAS_RELU, 2, 16, 2, 2><<<nb, 256>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, K, ntn); break;
     }
   };
   for (int v = 0; v < (int)vs.size(); ++v) run(v);

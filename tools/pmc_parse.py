@@ -59,7 +59,6 @@ for cls, (pat, _) in CLASSES.items():
     detail[cls] = {"fetch_bytes_x2": round(fb), "write_bytes_raw": round(wb), "write_calib": round(calib, 3),
                    "launches": len(fvals), "grid": gmax}
 print(json.dumps(detail, indent=1))
-os.makedirs("profiles", exist_ok=True)
-json.dump(res, open("profiles/traffic.json", "w"), indent=1)
+json.dump(res, open(os.path.join(root, "traffic.json"), "w"), indent=1)  # copy to profiles/ after the run
 json.dump(detail, open(os.path.join(root, "traffic_detail.json"), "w"), indent=1)
 print(json.dumps(res))
