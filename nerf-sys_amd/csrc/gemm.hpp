@@ -34,12 +34,17 @@ __device__ __forceinline__ void nt_epilogue(const nerf_f32x16 (&acc)[TM][TN], in
 // ------------------------------------------------------------------------------------------ gemm_nt
 // Requirements (checked by the host wrapper): M % BM == 0, N % BN == 0, K % 16 == 0, lda/ldb/ldc/ldm % 4
 // == 0, 16-byte aligned A/B.
-template <int BM, int BN, int WAVES_M, int EPI, int MINW = 1, int BK = 16, int NBUF = 2, int PIN = 0>
-__global__ __launch_bounds__(256, MINW) void gemm_nt_kernel(const float* __restrict__ A, int lda,
-                                                      const float* __restrict__ B, int ldb,
-                                                      const float* __restrict__ bias, float* __restrict__ C, int ldc,
-                                                      const uint32_t* __restrict__ mbits, int ldmb,
-                                                      uint32_t* __restrict__ mbits_out, int K, int n_ntiles) {
+//
+// Measured alternatives (tools/gemm_bench2.hip, tools/gemm_variants/, MI355X, C2 trunk shape; this kernel
+// runs at 79 % of the fp32 MFMA peak at its in-kernel clock of 2.3 GHz, tools/clock_probe.hip): an
+// LDS-DMA (global_load_lds) ring with counted vmcnt, a weights-stationary persistent kernel with
+// activations streamed to registers, prefetch loads pinned above the MFMA block (inline asm), BK = 32,
+// a 128x256 tile and 2..3 waves/SIMD were all 2-13 % slower.
+template <int BM, int BN, int WAVES_M, int EPI, int BK = 16, int NBUF = 2>
+__device__ __forceinline__ void gemm_nt_body(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb,
+                                             const float* __restrict__ bias, float* __restrict__ C, int ldc,
+                                             const uint32_t* __restrict__ mbits, int ldmb,
+                                             uint32_t* __restrict__ mbits_out, int K, int n_ntiles) {
   constexpr int WAVES_N = 4 / WAVES_M;
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -106,15 +111,11 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_kernel(const float* __restr
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = NBUF == 2 ? (kt & 1) : 0;
     NT_GLOAD((kt + 1 < nk ? kt + 1 : kt) * BK);
-    // pin the prefetch ABOVE the MFMA block: left alone, hipcc sinks these loads below the MFMAs (to
-    // shorten register live ranges) and then waits on them at once, exposing the full HBM latency.
-    if (PIN) __builtin_amdgcn_sched_barrier(0);
     const float* As = smem + cur * (BM + BN) * LS;
     const float* Bs = As + BM * LS;
     // lane half h owns k = h*HK + s of the slab; its k-values of a row are read 4 at a time
 #pragma unroll
     for (int hh = 0; hh < HK / 4; ++hh) {
-      if (PIN >= 2 && hh > 0) __builtin_amdgcn_sched_barrier(0);
       float4 af[TM], bf[TN];
 #pragma unroll
       for (int a = 0; a < TM; ++a)
@@ -137,6 +138,15 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_kernel(const float* __restr
 #undef NT_GLOAD
 #undef NT_SSTORE
   nt_epilogue<TM, TN, WTM, WTN, EPI>(acc, m0 + wm * WTM, n0 + wn * WTN, li, lh, bias, C, ldc, mbits, ldmb, mbits_out);
+}
+
+template <int BM, int BN, int WAVES_M, int EPI, int MINW = 1, int BK = 16, int NBUF = 2>
+__global__ __launch_bounds__(256, MINW) void gemm_nt_kernel(const float* __restrict__ A, int lda,
+                                                      const float* __restrict__ B, int ldb,
+                                                      const float* __restrict__ bias, float* __restrict__ C, int ldc,
+                                                      const uint32_t* __restrict__ mbits, int ldmb,
+                                                      uint32_t* __restrict__ mbits_out, int K, int n_ntiles) {
+  gemm_nt_body<BM, BN, WAVES_M, EPI, BK, NBUF>(A, lda, B, ldb, bias, C, ldc, mbits, ldmb, mbits_out, K, n_ntiles);
 }
 
 // epilogue.  The MFMA computed C^T, so lane li holds ONE output row m = ... + li and register

@@ -56,3 +56,12 @@ def compute_mse_loss(P, model, data, params=None, active_module=None, reduction=
 def psnr(mse: float) -> float:
     import math
     return -10.0 * math.log10(max(float(mse), 1e-8))
+
+
+def image_psnr(pred_linear, gt_u8_or_srgb, color_space: str = "linear") -> float:
+    """Full-image PSNR as the reference evaluates it (pipelines/online_stage/runtime_adapt.py:150-157):
+    the rendered image is linear, the ground truth is 8-bit sRGB, and both are brought into
+    ``color_space`` (the training colour space, args.py:98-102) by color_space_transformer."""
+    gt = gt_u8_or_srgb.float() / 255.0 if gt_u8_or_srgb.dtype == torch.uint8 else gt_u8_or_srgb.float()
+    a, b = color_space_transformer(pred_linear.float(), gt.to(pred_linear.device), color_space)
+    return psnr(F.mse_loss(a, b).item())

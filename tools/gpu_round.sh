@@ -1,10 +1,12 @@
 #!/bin/bash
-# One GPU-box session: build check, gpu parity tests, smoke, bench, rocprof kernel stats.
+# One GPU-box session: gpu parity tests, smoke, bench, rocprof kernel stats of the same bench command,
+# PMC HBM traffic.  Usage: tools/gpu_round.sh [all|test|bench|prof|pmc]
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 STEP=${1:-all}
+BENCH_ARGS=${BENCH_ARGS:-"--steps 20 --warmup 5"}
 if [[ $STEP == all || $STEP == test ]]; then
   timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
   tail -30 gpurun_out/pytest_gpu.log; [[ $rc -ne 0 ]] && exit $rc
@@ -12,12 +14,15 @@ if [[ $STEP == all || $STEP == test ]]; then
   cat gpurun_out/smoke.log
 fi
 if [[ $STEP == all || $STEP == bench ]]; then
-  timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
-  tail -3 gpurun_out/bench.log
+  timeout -k 10 600 python bench.py $BENCH_ARGS > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
+  tail -1 gpurun_out/bench.log
 fi
 if [[ $STEP == all || $STEP == prof ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-    python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --train-views 8 > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
-  tail -2 gpurun_out/prof.log
-  find gpurun_out/prof -name "*kernel_stats.csv" | head -3
+    python3 bench.py $BENCH_ARGS --no-cpu-baseline > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
+  python3 tools/prof_summary.py gpurun_out/prof/run_kernel_stats.csv 25 > gpurun_out/prof_summary.txt 2>&1
+  tail -1 gpurun_out/prof.log | cut -c1-200
+fi
+if [[ $STEP == all || $STEP == pmc ]]; then
+  bash tools/pmc_traffic.sh || exit 1
 fi

@@ -18,3 +18,21 @@ for r in rows:
 for per, c, avg, n in sorted(out, reverse=True):
     print(f"{per:9.1f} us/step  calls/step={c:5.1f}  avg={avg:8.1f} us  {n}")
 print(f"sum of our kernels: {tot:.1f} us/step")
+
+
+# per (kernel, grid) averages from the kernel trace next to the stats file: the roofline kernel's launches
+# are told apart from other launches of the same symbol by their grid (fine net trunk: M = 786,432 rows)
+import glob
+import os
+tr = glob.glob(os.path.join(os.path.dirname(path), "*kernel_trace.csv"))
+if tr:
+    from collections import defaultdict
+    per = defaultdict(list)
+    for r in csv.DictReader(open(tr[0])):
+        if not r["Kernel_Name"].startswith("void gemm_"):
+            continue
+        blocks = int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"])
+        per[(r["Kernel_Name"].split("(")[0], blocks)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    print("\nper (GEMM kernel, grid) launch averages from the kernel trace:")
+    for (n, b), v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
+        print(f"{sum(v) / len(v):9.1f} us avg  x{len(v):4d}  blocks={b:6d}  {n[:80]}")
