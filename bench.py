@@ -29,6 +29,8 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "rays/sec (train step) + full-image PSNR, 800×800 Lego, 64+128 samples"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak
 MAC_PER_EVAL = 500864
 FLOP_PER_RAY = 769327104       # 6*MAC*(64 coarse + 192 fine evaluations), SURVEY.md §8(d)
 
@@ -42,10 +44,14 @@ def parse():
     ap.add_argument("--samples", type=int, default=64)
     ap.add_argument("--importance", type=int, default=128)
     ap.add_argument("--train-views", type=int, default=100)
+    ap.add_argument("--scene", default="blender", choices=["blender", "llff"],
+                    help="blender = Lego-style 800x800 (configs[1]/[2]); llff = Fern-style 1008x756 NDC (configs[3])")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--psnr", action="store_true", help="render one held-out 800x800 view after the timed steps")
     ap.add_argument("--no-overlap", action="store_true", help="run the coarse-net backward on the main stream")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
+                    help="MLP GEMM precision: fp32 = BASELINE configs[1] (default, the headline), bf16 = configs[2]")
     return ap.parse_args()
 
 
@@ -82,15 +88,18 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from nerf_amd.scene import make_blender_scene
+    from nerf_amd.scene import make_blender_scene, make_llff_scene
     from nerf_amd.trainer import NeRFTrainer, RayBatcher
     from nerf_amd.vanilla import VanillaNeRF
 
     torch.manual_seed(0)
-    scene = make_blender_scene(n_train=a.train_views, n_test=1, H=800, W=800, seed=0, device=dev)
+    if a.scene == "llff":
+        scene = make_llff_scene(n_train=min(a.train_views, 20), n_test=1, seed=0, device=dev)
+    else:
+        scene = make_blender_scene(n_train=a.train_views, n_test=1, H=800, W=800, seed=0, device=dev)
     coarse, fine = VanillaNeRF().to(dev), VanillaNeRF().to(dev)
     tr = NeRFTrainer(coarse, fine, n_samples=a.samples, n_importance=a.importance, world_size=world, device=dev,
-                     overlap=not a.no_overlap)
+                     overlap=not a.no_overlap, precision=a.precision)
     rb = RayBatcher(scene, dev)
 
     from nerf_amd.dp import shard_seed
@@ -142,29 +151,46 @@ def main():
     tot_flop = flop_trunk * sum(len(st) for st in tm["dgrad"]) + flop_head * len(tm["dgrad_head"])
     ach = tot_flop / (tot_ms * 1e-3) / 1e12
     flops_launch = tot_flop / n_launch
+    bf16 = a.precision == "bf16"
     traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    tpath = os.path.join(ROOT, "profiles", "traffic_bf16.json" if bf16 else "traffic.json")
     if os.path.exists(tpath):
         try:
             traffic = json.load(open(tpath)).get("gemm_nt dgrad (trunk 256x256, ReLU mask)")
         except Exception:
             traffic = None
+    if bf16:
+        # bf16 layers are HBM-bound: algorithmic bytes per launch = bf16 input-gradient rows in (K * 2 B) +
+        # bf16 rows out (256 * 2 B) + the ReLU bitmask word row (32 B) per sample row
+        by_trunk, by_head = M * (256 * 2 + 256 * 2 + 32.0), M * (32 * 2 + 256 * 2 + 32.0)
+        tot_by = by_trunk * sum(len(st) for st in tm["dgrad"]) + by_head * len(tm["dgrad_head"])
+        ach_gbs = tot_by / (tot_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": dom.replace("gemm_nt", "gemm_nt_bf16"), "achieved": round(ach_gbs, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "bytes_per_launch": tot_by / n_launch, "mfma_tflops": round(ach, 1),
+                "mfma_frac_bf16": round(ach / BF16_MFMA_PEAK_TFLOPS, 4)}
+    else:
+        roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                "flop_per_launch": flops_launch}
+    roof.update({"mean_launch_ms": round(tot_ms / n_launch, 4), "classes_ms": {k: round(v, 4) for k, v in cls.items()}})
+    peak_step = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
 
     rays_total = a.batch * world * a.steps
     value = rays_total / el
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "Lego-style 800x800 (synthetic analytic scene, 100 views), 64 coarse + 128 fine "
-                               "hierarchical, 2 x (8x256 MLP), fp32, train step incl. ray gen + Adam",
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if bf16 else "f32", "data": "synthetic",
+        "config": {"workload": ("Fern-style 1008x756 forward-facing NDC (synthetic analytic scene, 20 views)"
+                                if a.scene == "llff" else "Lego-style 800x800 (synthetic analytic scene, 100 views)") +
+                               ", 64 coarse + 128 fine hierarchical, 2 x (8x256 MLP), " +
+                               ("bf16 MLP + fp32 compositing" if bf16 else "fp32") +
+                               ", train step incl. ray gen + Adam",
                    "global_batch": a.batch * world, "rays_per_gpu": a.batch, "samples": [a.samples, a.importance],
-                   "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                     "flop_per_launch": flops_launch, "mean_launch_ms": round(tot_ms / n_launch, 4),
-                     "classes_ms": {k: round(v, 4) for k, v in cls.items()}},
-        "step_mfma_frac": round(value * FLOP_PER_RAY / world / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+                   "parallelism": f"dp{world}", "precision": a.precision},
+        "roofline": roof,
+        "step_mfma_frac": round(value * FLOP_PER_RAY / world / 1e12 / peak_step, 4),
         "final_loss": round(final_loss, 6),
     }
     if a.psnr and rank == 0:
@@ -172,9 +198,9 @@ def main():
         tr.sync_to_modules()
         coarse.eval()
         fx, fy, cx, cy = scene.intrinsics
-        img, _, _ = render_image(coarse, H=800, W=800, fx=fx, fy=fy, cx=cx, cy=cy, c2w=scene.test_poses[0],
-                                 near=2.0, far=6.0, ray_samples=a.samples, n_importance=a.importance,
-                                 fine_model=fine.eval())
+        img, _, _ = render_image(coarse, H=scene.H, W=scene.W, fx=fx, fy=fy, cx=cx, cy=cy, c2w=scene.test_poses[0],
+                                 near=scene.near, far=scene.far, ray_samples=a.samples, n_importance=a.importance,
+                                 fine_model=fine.eval(), ndc=(scene.focal, 1.0) if scene.ndc else None)
         from nerf_amd.losses import image_psnr
         out["psnr_after_steps"] = round(image_psnr(img, scene.test_images[0], "linear"), 3)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -111,7 +111,18 @@ int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* rgb_sigma, 
 int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
                  int64_t ws_bytes, hipEvent_t* events, hipStream_t stream);
 /* events: NULL, or 32 hipEvent_t: events[4i+0/1] bracket the weight-gradient GEMM of trunk.i,
- * events[4i+2/3] its input-gradient GEMM (i >= 1). */
+ * events[4i+2/3] its input-gradient GEMM (i >= 1); events[2/3] bracket the head's input-gradient GEMM. */
+
+/* bf16 variants (BASELINE configs[2]: "bf16 MLP with fp32 compositing"): the same network, packed fp32
+ * parameters, inputs and outputs as nerf_mlp_fwd/bwd; the layer GEMMs run on bf16 MFMA with fp32
+ * accumulation and the activations / activation gradients live in the workspace as bf16.  The weight
+ * gradient d_w is fp32.  Not bit-compatible with the fp32 path (tolerance: bf16 rounding). */
+int64_t nerf_mlp_workspace_bytes_bf16(int64_t M, int training);
+int nerf_mlp_fwd_bf16(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws, int64_t ws_bytes,
+                      int training, hipEvent_t* events, hipStream_t stream);
+int nerf_mlp_bwd_bf16(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
+                      int64_t ws_bytes, hipEvent_t* events, hipStream_t stream);
+/* events: as for nerf_mlp_fwd / nerf_mlp_bwd. */
 
 /* ------------------------------------------------------------------ compositing + loss */
 

@@ -326,7 +326,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const float* __restrict
 }
 
 // dst[i] = (acc ? dst[i] : 0) + sum_{s<S} src[s*slab + i]   (float4 lanes, deterministic order)
-__global__ void reduce_splits_kernel(const float* __restrict__ src, int64_t slab, int S, float* __restrict__ dst,
+static __global__ void reduce_splits_kernel(const float* __restrict__ src, int64_t slab, int S, float* __restrict__ dst,
                                      int64_t n4, int accumulate) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;

@@ -1,0 +1,337 @@
+// bf16 MFMA GEMMs for the C3 configuration ("bf16 MLP with fp32 compositing", BASELINE.json configs[2]):
+// bf16 operands in HBM and LDS, fp32 accumulation on gfx950 `v_mfma_f32_32x32x16_bf16`, fp32 master
+// weights and gradients.  Same three shapes as the fp32 path (gemm.hpp):
+//   gemm_nt_bf16     C[m][n] = epi( sum_k A[m][k] * B[n][k] )   forward (B = W) / input gradient (B = W^T)
+//   gemm_wgrad_bf16  P[s][n][k] = sum_{m in split s} G[m][n] * X[m][k]  (+ bias column sums), fp32 slabs
+//
+// At these layer shapes (M ~ 10^6 rows, N, K <= 320) the bf16 layers are HBM-bound (1 KB/row/layer of bf16
+// activations in + out against ~0.26 MFLOP/row), so the tiles are the fp32 kernel's: 128 x 128 blocks of
+// four 64 x 64 wave tiles (2 x 2 MFMA tiles), one barrier per k-slab, register-staged 16-B loads.
+//
+// Fragments.  32x32x16 bf16 MFMA: lane l (r = l & 31, h = l >> 5) supplies A[i = r][k = 8 h + j] and
+// B[k = 8 h + j][col r], j = 0..7 (8 bf16 = 4 VGPRs).
+//  * NT: operands are rows with k contiguous -> one ds_read_b128 per fragment from a [rows][BK] LDS tile
+//    with a 16-B row pad (pitch BK + 8 bf16: 16 consecutive rows hit 16 distinct 16-B bank slots).
+//    As in the fp32 kernel the MFMA computes C^T (i = n from W, j = m from the activations), so lane r
+//    owns one output row and the epilogue stores runs of 4 consecutive columns.
+//  * wgrad: both operands are indexed by the contraction index m = the ROW of G and X, so a fragment is a
+//    column of a row-major [m][cols] LDS tile: two ds_read_b64_tr_b16 (gfx950 transposing read: a
+//    16-lane group reads a 4-row x 16-column block and lane i receives column i) give the 8 rows.
+//    Row pitch 160 bf16 (320 B = 64 B mod 256 B): the four rows of a block sit in disjoint bank quarters.
+#pragma once
+#include "gemm.hpp"
+
+typedef __bf16 nerf_bf16;
+typedef __bf16 nerf_bf16x8 __attribute__((ext_vector_type(8)));
+typedef short nerf_s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t nerf_pack_bf16x2(float a, float b) {
+  const nerf_bf16 x = (nerf_bf16)a, y = (nerf_bf16)b;  // v_cvt_pk_bf16_f32, round to nearest even
+  return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+}
+__device__ __forceinline__ float nerf_bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float nerf_bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+// ------------------------------------------------------------------------------------------ gemm_nt_bf16
+// EPI as in gemm.hpp.  OUT_BF16: store C as bf16 (activations / activation gradients) or fp32 (head outputs).
+// Requirements (host wrapper): M % BM == 0, N % BN == 0, K % BK == 0, lda/ldb % 8 == 0, ldc % 4 == 0.
+template <int BM, int BN, int WAVES_M, int EPI, int OUT_BF16, int BK = 64, int MINW = 2>
+__global__ __launch_bounds__(256, MINW) void gemm_nt_bf16_kernel(const nerf_bf16* __restrict__ A, int lda,
+                                                                const nerf_bf16* __restrict__ B, int ldb,
+                                                                const float* __restrict__ bias, void* __restrict__ Cv,
+                                                                int ldc, const uint32_t* __restrict__ mbits, int ldmb,
+                                                                uint32_t* __restrict__ mbits_out, int K, int n_ntiles) {
+  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0, "wave tile");
+  static_assert(BK % 16 == 0, "k-slab");
+  constexpr int LS = BK + 8;              // LDS row pitch (bf16)
+  constexpr int C8 = BK / 8;              // 16-B chunks per row per slab
+  constexpr int A_CH = BM * C8, B_CH = BN * C8;
+  constexpr int A_PER = (A_CH + 255) / 256, B_PER = (B_CH + 255) / 256;
+  __shared__ __attribute__((aligned(16))) nerf_bf16 smem[2 * (BM + BN) * LS];
+
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
+  const int64_t m0 = (int64_t)mt * BM;
+  const int n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int li = lane & 31, lh = lane >> 5;
+  const nerf_bf16* Ab = A + m0 * lda;
+  const nerf_bf16* Bb = B + (int64_t)n0 * ldb;
+
+  uint4 ra[A_PER], rb[B_PER];
+#define NTB_GLOAD(k0_)                                                                                  \
+  _Pragma("unroll") for (int i = 0; i < A_PER; ++i) {                                                  \
+    const int f = tid + 256 * i;                                                                        \
+    if (A_CH % 256 == 0 || f < A_CH)                                                                    \
+      ra[i] = *reinterpret_cast<const uint4*>(Ab + (int64_t)(f / C8) * lda + (k0_) + (f % C8) * 8);     \
+  }                                                                                                     \
+  _Pragma("unroll") for (int i = 0; i < B_PER; ++i) {                                                  \
+    const int f = tid + 256 * i;                                                                        \
+    if (B_CH % 256 == 0 || f < B_CH)                                                                    \
+      rb[i] = *reinterpret_cast<const uint4*>(Bb + (int64_t)(f / C8) * ldb + (k0_) + (f % C8) * 8);     \
+  }
+#define NTB_SSTORE(buf_)                                                                                \
+  {                                                                                                     \
+    nerf_bf16* As_ = smem + (buf_) * (BM + BN) * LS;                                                    \
+    nerf_bf16* Bs_ = As_ + BM * LS;                                                                     \
+    _Pragma("unroll") for (int i = 0; i < A_PER; ++i) {                                                \
+      const int f = tid + 256 * i;                                                                      \
+      if (A_CH % 256 == 0 || f < A_CH) *reinterpret_cast<uint4*>(As_ + (f / C8) * LS + (f % C8) * 8) = ra[i]; \
+    }                                                                                                   \
+    _Pragma("unroll") for (int i = 0; i < B_PER; ++i) {                                                \
+      const int f = tid + 256 * i;                                                                      \
+      if (B_CH % 256 == 0 || f < B_CH) *reinterpret_cast<uint4*>(Bs_ + (f / C8) * LS + (f % C8) * 8) = rb[i]; \
+    }                                                                                                   \
+  }
+
+  nerf_f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int nk = K / BK;
+  NTB_GLOAD(0);
+  NTB_SSTORE(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    NTB_GLOAD((kt + 1 < nk ? kt + 1 : kt) * BK);
+    const nerf_bf16* As = smem + cur * (BM + BN) * LS;
+    const nerf_bf16* Bs = As + BM * LS;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      nerf_bf16x8 af[TM], bf[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+        af[a] = *reinterpret_cast<const nerf_bf16x8*>(As + (wm * WTM + a * 32 + li) * LS + 16 * ks + 8 * lh);
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        bf[b] = *reinterpret_cast<const nerf_bf16x8*>(Bs + (wn * WTN + b * 32 + li) * LS + 16 * ks + 8 * lh);
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)  // swapped operands: the tile is C^T (i = n, j = m)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[b], af[a], acc[a][b], 0, 0, 0);
+    }
+    NTB_SSTORE(cur ^ 1);
+    __syncthreads();
+  }
+#undef NTB_GLOAD
+#undef NTB_SSTORE
+
+  // epilogue (C^T: lane li owns row m; register r = 4q + e is column 8q + 4lh + e of the 32-column tile)
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int nb = n0 + wn * WTN + b * 32;
+    const int g = nb >> 5;
+    float4 bv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) bv[q] = *reinterpret_cast<const float4*>(bias + nb + 8 * q + 4 * lh);
+    }
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const int64_t m = m0 + wm * WTM + a * 32 + li;
+      uint32_t word = 0;
+      if (EPI == EPI_MASK) word = mbits[m * ldmb + g];
+      uint2 pk[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[a][b][4 * q + e];
+          const float bb = e == 0 ? bv[q].x : (e == 1 ? bv[q].y : (e == 2 ? bv[q].z : bv[q].w));
+          if (EPI == EPI_BIAS) v[e] += bb;
+          if (EPI == EPI_BIAS_RELU) {
+            v[e] = fmaxf(v[e] + bb, 0.f);
+            word |= (v[e] > 0.f ? 1u : 0u) << (8 * q + 4 * lh + e);
+          }
+          if (EPI == EPI_MASK) v[e] = ((word >> (8 * q + 4 * lh + e)) & 1u) ? v[e] : 0.f;
+        }
+        if constexpr (OUT_BF16) {
+          pk[q] = make_uint2(nerf_pack_bf16x2(v[0], v[1]), nerf_pack_bf16x2(v[2], v[3]));
+        } else {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cv) + m * ldc + nb + 8 * q + 4 * lh) =
+              make_float4(v[0], v[1], v[2], v[3]);
+        }
+      }
+      if constexpr (OUT_BF16) {
+        // T21 (cdna_hip_programming.md): lanes li / li + 32 hold columns 8q..8q+3 / 8q+4..8q+7 of the same row;
+        // one v_permlane32_swap per dword of the (q, q + 1) pair leaves 16 contiguous bytes in every lane
+        // (low half: columns 16p..16p+7, high half: 16p+8..16p+15) -> one 16-B store per pair.
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          uint2 x = pk[2 * pr], y = pk[2 * pr + 1];
+          const auto r0 = __builtin_amdgcn_permlane32_swap(x.x, y.x, false, false);
+          const auto r1 = __builtin_amdgcn_permlane32_swap(x.y, y.y, false, false);
+          x.x = r0[0]; y.x = r0[1];
+          x.y = r1[0]; y.y = r1[1];
+          *reinterpret_cast<uint4*>(reinterpret_cast<nerf_bf16*>(Cv) + m * ldc + nb + 16 * pr + 8 * lh) =
+              make_uint4(x.x, x.y, y.x, y.y);
+        }
+      }
+      if (EPI == EPI_BIAS_RELU && mbits_out) {
+        word |= __shfl_xor(word, 32, 64);
+        if (lh == 0) mbits_out[m * ldmb + g] = word;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ gemm_wgrad_bf16
+// P[s][n][k] (row pitch ldp, fp32) = sum over rows m of split s of G[m][n] * X[m][k]; the tiles of column
+// block 0 also write Pb[s][n] = sum_m G[m][n].  MFMA A = G^T (i = n, k-slot = m), B = X (k-slot = m, j = k).
+// Requirements: rows_per_split % 32 == 0, M % 32 == 0, ldg/ldx % 8 == 0.
+template <int BN, int BK, int WAVES_N>
+__global__ __launch_bounds__(256, 2) void gemm_wgrad_bf16_kernel(const nerf_bf16* __restrict__ G, int ldg,
+                                                                const nerf_bf16* __restrict__ X, int ldx,
+                                                                float* __restrict__ P, int ldp, float* __restrict__ Pb,
+                                                                int64_t slab, int64_t rows_per_split, int64_t M,
+                                                                int n_ktiles, int n_tiles) {
+  constexpr int WAVES_K = 4 / WAVES_N;
+  constexpr int WTN = BN / WAVES_N, WTK = BK / WAVES_K;
+  constexpr int TM = WTN / 32, TN = WTK / 32;
+  static_assert(TM >= 1 && TN >= 1, "wave tile");
+  constexpr int MR = 32;                         // rows (contraction) per LDS slab: two 16-row MFMA k-steps
+  constexpr int PG = ((BN + 127) / 128) * 128 + 32, PX = ((BK + 127) / 128) * 128 + 32;  // pitch = 64 B mod 256 B
+  constexpr int G_CH = MR * BN / 8, X_CH = MR * BK / 8;
+  constexpr int G_PER = (G_CH + 255) / 256, X_PER = (X_CH + 255) / 256;
+  __shared__ __attribute__((aligned(16))) nerf_bf16 smem[2 * MR * (PG + PX)];
+
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int s = lin / n_tiles;
+  const int tile = lin - s * n_tiles;
+  const int nt = tile / n_ktiles, kt = tile - nt * n_ktiles;
+  const int n0 = nt * BN, k0 = kt * BK;
+  const int64_t r0 = (int64_t)s * rows_per_split;
+  int64_t r1 = r0 + rows_per_split;
+  if (r1 > M) r1 = M;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave / WAVES_K, wk = wave % WAVES_K;
+  const int li = lane & 31, lh = lane >> 5;
+  const bool do_bias = (Pb != nullptr) && kt == 0 && wk == 0;
+
+  uint4 rg[G_PER], rx[X_PER];
+#define WGB_GLOAD(m_)                                                                                   \
+  _Pragma("unroll") for (int i = 0; i < G_PER; ++i) {                                                  \
+    const int f = tid + 256 * i;                                                                        \
+    if (G_CH % 256 == 0 || f < G_CH)                                                                    \
+      rg[i] = *reinterpret_cast<const uint4*>(G + ((m_) + f / (BN / 8)) * ldg + n0 + (f % (BN / 8)) * 8); \
+  }                                                                                                     \
+  _Pragma("unroll") for (int i = 0; i < X_PER; ++i) {                                                  \
+    const int f = tid + 256 * i;                                                                        \
+    if (X_CH % 256 == 0 || f < X_CH)                                                                    \
+      rx[i] = *reinterpret_cast<const uint4*>(X + ((m_) + f / (BK / 8)) * ldx + k0 + (f % (BK / 8)) * 8); \
+  }
+#define WGB_SSTORE(buf_)                                                                                \
+  {                                                                                                     \
+    nerf_bf16* Gs_ = smem + (buf_) * MR * (PG + PX);                                                    \
+    nerf_bf16* Xs_ = Gs_ + MR * PG;                                                                     \
+    _Pragma("unroll") for (int i = 0; i < G_PER; ++i) {                                                \
+      const int f = tid + 256 * i;                                                                      \
+      if (G_CH % 256 == 0 || f < G_CH)                                                                  \
+        *reinterpret_cast<uint4*>(Gs_ + (f / (BN / 8)) * PG + (f % (BN / 8)) * 8) = rg[i];              \
+    }                                                                                                   \
+    _Pragma("unroll") for (int i = 0; i < X_PER; ++i) {                                                \
+      const int f = tid + 256 * i;                                                                      \
+      if (X_CH % 256 == 0 || f < X_CH)                                                                  \
+        *reinterpret_cast<uint4*>(Xs_ + (f / (BK / 8)) * PX + (f % (BK / 8)) * 8) = rx[i];              \
+    }                                                                                                   \
+  }
+
+  nerf_f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  float bsum[TM];
+#pragma unroll
+  for (int a = 0; a < TM; ++a) bsum[a] = 0.f;
+
+  // transposing-read addressing: lane 4q + p of 16-lane group g reads row 8 h + 4 t + q (h = g >> 1, t = read
+  // 0/1 of the pair), columns c0 + 16 (g & 1) + 4 p .. + 3; lane i of the group receives column c0 + 16 (g & 1) + i
+  const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int trow = 8 * (grp >> 1) + q, tcol = 16 * (grp & 1) + 4 * p;
+
+  const int64_t nit = (r1 - r0) / MR;
+  if (nit > 0) {
+    WGB_GLOAD(r0);
+    WGB_SSTORE(0);
+  }
+  __syncthreads();
+  for (int64_t it = 0; it < nit; ++it) {
+    const int cur = (int)(it & 1);
+    WGB_GLOAD(r0 + (it + 1 < nit ? it + 1 : it) * MR);
+    const nerf_bf16* Gs = smem + cur * MR * (PG + PX);
+    const nerf_bf16* Xs = Gs + MR * PG;
+#pragma unroll
+    for (int ks = 0; ks < MR / 16; ++ks) {
+      nerf_bf16x8 af[TM], bf[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const nerf_bf16* base = Gs + (16 * ks + trow) * PG + wn * WTN + a * 32 + tcol;
+        const nerf_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) nerf_s16x4*)(base));
+        const nerf_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) nerf_s16x4*)(base + 4 * PG));
+        const short v8 __attribute__((ext_vector_type(8))) = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[a] = __builtin_bit_cast(nerf_bf16x8, v8);
+      }
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const nerf_bf16* base = Xs + (16 * ks + trow) * PX + wk * WTK + b * 32 + tcol;
+        const nerf_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) nerf_s16x4*)(base));
+        const nerf_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) nerf_s16x4*)(base + 4 * PX));
+        const short v8 __attribute__((ext_vector_type(8))) = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bf[b] = __builtin_bit_cast(nerf_bf16x8, v8);
+      }
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        if (do_bias) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bsum[a] += (float)af[a][j];
+        }
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bf[b], acc[a][b], 0, 0, 0);
+      }
+    }
+    WGB_SSTORE(cur ^ 1);
+    __syncthreads();
+  }
+#undef WGB_GLOAD
+#undef WGB_SSTORE
+
+  float* Ps = P + (int64_t)s * slab;
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int k = k0 + wk * WTK + b * 32 + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + wn * WTN + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        Ps[(int64_t)n * ldp + k] = acc[a][b][r];
+      }
+    }
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const float v = bsum[a] + __shfl_xor(bsum[a], 32, 64);
+      if (lh == 0) Pb[(int64_t)s * slab + n0 + wn * WTN + a * 32 + li] = v;
+    }
+  }
+}

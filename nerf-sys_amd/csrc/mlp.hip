@@ -15,56 +15,10 @@
 //   C0 [Mp][128], O3 [Mp][32].  Backward adds dA/dB [Mp][256], dO16, dO3, dCIN [Mp][32], dC0 [Mp][128],
 //   transposed weights, and S split-M partial slabs of the packed gradient.
 #include "gemm.hpp"
+#include "mlp_common.hpp"
 
 namespace {
-
-constexpr int NT = 22;  // tensors in the packed layout
-constexpr int KPAD[8] = {64, 256, 256, 256, 320, 256, 256, 256};
-constexpr int KREAL[8] = {63, 256, 256, 256, 319, 256, 256, 256};
-
-struct Layout {
-  int64_t off[NT];
-  int rows[NT], cols[NT], creal[NT];
-  int64_t total;
-};
-
-Layout make_layout() {
-  Layout L{};
-  int64_t o = 0;
-  int t = 0;
-  auto add = [&](int r, int c, int cr) {
-    L.off[t] = o; L.rows[t] = r; L.cols[t] = c; L.creal[t] = cr;
-    o += (int64_t)r * c;
-    o = (o + 31) & ~int64_t(31);  // keep every tensor 128-B aligned
-    ++t;
-  };
-  for (int i = 0; i < 8; ++i) {
-    add(256, KPAD[i], KREAL[i]);
-    add(256, 1, 1);
-  }
-  add(32, 256, 256);  // head W: row 0 sigma_head, rows 1..15 geo_head
-  add(32, 1, 1);
-  add(128, 64, 42);   // color_mlp.layer0
-  add(128, 1, 1);
-  add(32, 128, 128);  // color_mlp.color_out (rows 0..2)
-  add(32, 1, 1);
-  L.total = o;
-  return L;
-}
-
-const Layout& layout() {
-  static const Layout L = make_layout();
-  return L;
-}
-
-inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
-
-int n_splits(int64_t Mp) {
-  int64_t s = Mp / 2048;
-  if (s < 1) s = 1;
-  if (s > 256) s = 256;
-  return (int)s;
-}
+using namespace nerf_mlp;
 
 struct WS {
   int64_t Mp;
@@ -186,9 +140,6 @@ __global__ void build_cin_kernel(const float* __restrict__ xd, const float* __re
 #pragma unroll
   for (int c = 0; c < 16; ++c) q4[c] = make_float4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
 }
-
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
-constexpr float EXP_MAX = 88.722839111f;
 
 __global__ void head_out_kernel(const float* __restrict__ O3, const float* __restrict__ O16, int64_t M,
                                 float* __restrict__ out) {
@@ -323,12 +274,6 @@ int wgrad(const float* G, int ldg, const float* X, int ldx, int tensor_w, const 
   }
   return NERF_OK;
 }
-
-#define TRY(x)                     \
-  do {                             \
-    int _e = (x);                  \
-    if (_e != NERF_OK) return _e;  \
-  } while (0)
 
 }  // namespace
 

@@ -113,9 +113,23 @@ def freq_encode(x, L, include_input=True):
 # ------------------------------------------------------------------ MLP
 
 
-def mlp_workspace(M, training, device):
-    nb = lib().nerf_mlp_workspace_bytes(M, int(training))
-    return torch.empty(nb, dtype=torch.uint8, device=device)
+PRECISIONS = ("fp32", "bf16")
+
+
+def _check_precision(precision):
+    if precision not in PRECISIONS:
+        raise ValueError(f"precision must be one of {PRECISIONS}, got {precision!r}")
+
+
+def mlp_workspace_bytes(M, training, precision="fp32"):
+    _check_precision(precision)
+    if precision == "bf16":
+        return lib().nerf_mlp_workspace_bytes_bf16(M, int(training))
+    return lib().nerf_mlp_workspace_bytes(M, int(training))
+
+
+def mlp_workspace(M, training, device, precision="fp32"):
+    return torch.empty(mlp_workspace_bytes(M, training, precision), dtype=torch.uint8, device=device)
 
 
 def _events_arg(events):
@@ -125,21 +139,31 @@ def _events_arg(events):
     return arr
 
 
-def mlp_fwd(w_packed, x_d, ws, training, out=None, events=None):
+def mlp_fwd(w_packed, x_d, ws, training, out=None, events=None, precision="fp32"):
     need(w_packed, "packed weights"), need(x_d, "x_d")
+    _check_precision(precision)
     M = x_d.shape[0]
     if out is None:
         out = _empty((M, 4), x_d)
+    if precision == "bf16":
+        check(lib().nerf_mlp_fwd_bf16(ptr(w_packed), ptr(x_d), M, ptr(out), ptr(ws), ws.numel(), int(training),
+                                      _events_arg(events), stream()), "nerf_mlp_fwd_bf16")
+        return out
     check(lib().nerf_mlp_fwd(ptr(w_packed), ptr(x_d), M, ptr(out), ptr(ws), ws.numel(), int(training),
                              _events_arg(events), stream()), "nerf_mlp_fwd")
     return out
 
 
-def mlp_bwd(w_packed, M, d_rgb_sigma, ws, d_w=None, accumulate=False, events=None):
+def mlp_bwd(w_packed, M, d_rgb_sigma, ws, d_w=None, accumulate=False, events=None, precision="fp32"):
     need(w_packed, "packed weights"), need(d_rgb_sigma, "d_rgb_sigma")
+    _check_precision(precision)
     if d_w is None:
         d_w = torch.empty_like(w_packed)
         accumulate = False
+    if precision == "bf16":
+        check(lib().nerf_mlp_bwd_bf16(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws),
+                                      ws.numel(), _events_arg(events), stream()), "nerf_mlp_bwd_bf16")
+        return d_w
     check(lib().nerf_mlp_bwd(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws), ws.numel(),
                              _events_arg(events), stream()), "nerf_mlp_bwd")
     return d_w

@@ -53,7 +53,7 @@ class NeRFTrainer:
                  n_importance: int = 128, lr_sigma: float = 2e-3, lr_color: float = 2e-3, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.0, grad_clip: Optional[float] = 1.0,
                  color_space: str = "linear", bg: str = "white", sigma_scale: float = 1.0,
-                 world_size: int = 1, device="cuda", overlap: bool = True):
+                 world_size: int = 1, device="cuda", overlap: bool = True, precision: str = "fp32"):
         L = PackedLayout.get()
         self.L = L
         self.P = L.total
@@ -76,6 +76,9 @@ class NeRFTrainer:
             self.seg_off += [k * P + cs, (k + 1) * P]
             self.seg_lr += [lr_sigma, lr_color]
         self.S, self.n_imp = n_samples, n_importance
+        if precision not in K.PRECISIONS:
+            raise ValueError(f"precision must be one of {K.PRECISIONS}")
+        self.precision = precision  # MLP GEMMs: fp32 (configs[1]) or bf16 (configs[2]); compositing stays fp32
         self.betas, self.eps, self.wd = betas, eps, weight_decay
         self.grad_clip = grad_clip
         if color_space not in _CS:
@@ -107,7 +110,7 @@ class NeRFTrainer:
 
     def _workspace(self, key, M):
         ws = self._ws.get(key)
-        need = K.lib().nerf_mlp_workspace_bytes(M, 1)
+        need = K.mlp_workspace_bytes(M, 1, self.precision)
         if ws is None or ws.numel() < need:
             ws = torch.empty(need, dtype=torch.uint8, device=self.device)
             self._ws[key] = ws
@@ -157,7 +160,7 @@ class NeRFTrainer:
         t_c = K.sample_stratified(rays, S, True, u_strat, seed)
         xd_c = K.build_xd(rays, t_c)
         ws_c = self._workspace("c", N * S)
-        rs_c = K.mlp_fwd(self.w(0), xd_c, ws_c, True)
+        rs_c = K.mlp_fwd(self.w(0), xd_c, ws_c, True, precision=self.precision)
         _, _, w_c, _, _, drgb_c = K.composite_fwd(rs_c, t_c, bg, self.sigma_scale, gt=gt,
                                                   color_space=self.color_space, inv_count=inv_count,
                                                   loss_sum=self.loss_buf)
@@ -169,7 +172,7 @@ class NeRFTrainer:
             self._side.wait_event(fork)
             with torch.cuda.stream(self._side):
                 d_rs_c = K.composite_bwd(rs_c, t_c, bg, drgb_c, sigma_scale=self.sigma_scale)
-                K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=False)
+                K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=False, precision=self.precision)
                 side_done = torch.cuda.Event()
                 side_done.record(self._side)
         if NI > 0:
@@ -177,20 +180,22 @@ class NeRFTrainer:
             xd_f = K.build_xd(rays, t_f)
             ws_f = self._workspace("f", N * (S + NI))
             ev = self._next_events()
-            rs_f = K.mlp_fwd(self.w(fine_k), xd_f, ws_f, True, events=ev["fwd"] if ev else None)
+            rs_f = K.mlp_fwd(self.w(fine_k), xd_f, ws_f, True, events=ev["fwd"] if ev else None,
+                             precision=self.precision)
             _, _, _, _, _, drgb_f = K.composite_fwd(rs_f, t_f, bg, self.sigma_scale, gt=gt,
                                                     color_space=self.color_space, inv_count=inv_count,
                                                     loss_sum=self.loss_buf)
             d_rs_f = K.composite_bwd(rs_f, t_f, bg, drgb_f, sigma_scale=self.sigma_scale)
             K.mlp_bwd(self.w(fine_k), N * (S + NI), d_rs_f, ws_f, d_w=self.g(fine_k), accumulate=False,
-                      events=ev["bwd"] if ev else None)
+                      events=ev["bwd"] if ev else None, precision=self.precision)
             if ev:
                 self.timing["M"] = N * (S + NI)
         if side_done is not None:
             torch.cuda.current_stream(self.device).wait_event(side_done)
         else:
             d_rs_c = K.composite_bwd(rs_c, t_c, bg, drgb_c, sigma_scale=self.sigma_scale)
-            K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=(fine_k == 0 and NI > 0))
+            K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=(fine_k == 0 and NI > 0),
+                      precision=self.precision)
         allreduce_flat(self.gbuf, self.world_size)
         self.step_count += 1
         if self.grad_clip is not None and self.grad_clip > 0:

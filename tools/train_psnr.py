@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--train-views", type=int, default=100)
     ap.add_argument("--test-views", type=int, default=2)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
     a = ap.parse_args()
 
     from nerf_amd.scene import make_blender_scene, make_llff_scene
@@ -51,7 +52,7 @@ def main():
         ndc = (scene.focal, 1.0)
     coarse, fine = VanillaNeRF().to(dev), VanillaNeRF().to(dev)
     tr = NeRFTrainer(coarse, fine, n_samples=a.samples, n_importance=a.importance, lr_sigma=a.lr, lr_color=a.lr,
-                     device=dev)
+                     device=dev, precision=a.precision)
     rb = RayBatcher(scene, dev)
     fx, fy, cx, cy = scene.intrinsics
     outf = open(a.out, "w") if a.out else None
@@ -80,7 +81,7 @@ def main():
             step += 1
         torch.cuda.synchronize()
         train_s += time.perf_counter() - t0
-        rec = {"scene": a.scene, "step": step, "train_s": round(train_s, 2), "loss": round(float(loss.item()), 6),
+        rec = {"scene": a.scene, "precision": a.precision, "step": step, "train_s": round(train_s, 2), "loss": round(float(loss.item()), 6),
                "psnr": round(evaluate(), 3), "rays_per_s": round(step * a.batch / train_s, 1)}
         print(json.dumps(rec), flush=True)
         if outf:
