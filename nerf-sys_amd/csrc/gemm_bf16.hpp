@@ -32,6 +32,77 @@ __device__ __forceinline__ uint32_t nerf_pack_bf16x2(float a, float b) {
 __device__ __forceinline__ float nerf_bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float nerf_bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 
+// epilogue of the bf16 NT GEMMs (C^T: lane li owns row mw + a*32 + li; register r = 4q + e is column
+// 8q + 4lh + e of the 32-column tile b).  bf16 outputs leave as one 16-B store per (q, q+1) pair after a
+// v_permlane32_swap exchange between the lane halves (cdna_hip_programming.md T21).
+template <int TM, int TN, int WTM, int WTN, int EPI, int OUT_BF16>
+__device__ __forceinline__ void ntb_epilogue(nerf_f32x16 (&acc)[TM][TN], int64_t mw, int nw, int li, int lh,
+                                             const float* __restrict__ bias, void* __restrict__ Cv, int ldc,
+                                             const uint32_t* __restrict__ mbits, int ldmb,
+                                             uint32_t* __restrict__ mbits_out) {
+  const int64_t m0 = mw;
+  const int n0 = nw;
+  constexpr int wm = 0, wn = 0;
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int nb = n0 + wn * WTN + b * 32;
+    const int g = nb >> 5;
+    float4 bv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) bv[q] = *reinterpret_cast<const float4*>(bias + nb + 8 * q + 4 * lh);
+    }
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const int64_t m = m0 + wm * WTM + a * 32 + li;
+      uint32_t word = 0;
+      if (EPI == EPI_MASK) word = mbits[m * ldmb + g];
+      uint2 pk[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[a][b][4 * q + e];
+          const float bb = e == 0 ? bv[q].x : (e == 1 ? bv[q].y : (e == 2 ? bv[q].z : bv[q].w));
+          if (EPI == EPI_BIAS) v[e] += bb;
+          if (EPI == EPI_BIAS_RELU) {
+            v[e] = fmaxf(v[e] + bb, 0.f);
+            word |= (v[e] > 0.f ? 1u : 0u) << (8 * q + 4 * lh + e);
+          }
+          if (EPI == EPI_MASK) v[e] = ((word >> (8 * q + 4 * lh + e)) & 1u) ? v[e] : 0.f;
+        }
+        if constexpr (OUT_BF16) {
+          pk[q] = make_uint2(nerf_pack_bf16x2(v[0], v[1]), nerf_pack_bf16x2(v[2], v[3]));
+        } else {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cv) + m * ldc + nb + 8 * q + 4 * lh) =
+              make_float4(v[0], v[1], v[2], v[3]);
+        }
+      }
+      if constexpr (OUT_BF16) {
+        // T21 (cdna_hip_programming.md): lanes li / li + 32 hold columns 8q..8q+3 / 8q+4..8q+7 of the same row;
+        // one v_permlane32_swap per dword of the (q, q + 1) pair leaves 16 contiguous bytes in every lane
+        // (low half: columns 16p..16p+7, high half: 16p+8..16p+15) -> one 16-B store per pair.
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          uint2 x = pk[2 * pr], y = pk[2 * pr + 1];
+          const auto r0 = __builtin_amdgcn_permlane32_swap(x.x, y.x, false, false);
+          const auto r1 = __builtin_amdgcn_permlane32_swap(x.y, y.y, false, false);
+          x.x = r0[0]; y.x = r0[1];
+          x.y = r1[0]; y.y = r1[1];
+          *reinterpret_cast<uint4*>(reinterpret_cast<nerf_bf16*>(Cv) + m * ldc + nb + 16 * pr + 8 * lh) =
+              make_uint4(x.x, x.y, y.x, y.y);
+        }
+      }
+      if (EPI == EPI_BIAS_RELU && mbits_out) {
+        word |= __shfl_xor(word, 32, 64);
+        if (lh == 0) mbits_out[m * ldmb + g] = word;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------ gemm_nt_bf16
 // EPI as in gemm.hpp.  OUT_BF16: store C as bf16 (activations / activation gradients) or fp32 (head outputs).
 // Requirements (host wrapper): M % BM == 0, N % BN == 0, K % BK == 0, lda/ldb % 8 == 0, ldc % 4 == 0.
@@ -126,63 +197,347 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_bf16_kernel(const nerf_bf16
 #undef NTB_GLOAD
 #undef NTB_SSTORE
 
-  // epilogue (C^T: lane li owns row m; register r = 4q + e is column 8q + 4lh + e of the 32-column tile)
+  ntb_epilogue<TM, TN, WTM, WTN, EPI, OUT_BF16>(acc, m0 + wm * WTM, n0 + wn * WTN, li, lh, bias, Cv, ldc, mbits, ldmb,
+                                                mbits_out);
+}
+
+// ------------------------------------------------------------------------------------------ gemm_nt_bf16_ring
+// Persistent NT GEMM with an LDS-DMA ring: the bf16 layers are HBM-bound, and the register-staged kernel
+// above keeps one 32-deep k-slab per block in flight (latency-bound at ~3.4 TB/s).  Here every block walks
+// a strided list of output tiles as ONE stream of k-slabs (tile t0, slabs 0..nk-1, tile t0 + grid, ...)
+// and the DMA engine (global_load_lds_dwordx4, no VGPR staging) keeps STAGES-1 slabs in flight across
+// tile boundaries; a counted `s_waitcnt vmcnt` + raw barrier retire one slab per iteration.
+// LDS image per stage: A [BM][32] then B [BN][32] bf16, 64-B rows of four 16-B chunks; DMA writes are
+// lane-linear, so chunk c of row r is fetched into slot c ^ ((r >> 2) & 3) by permuting the SOURCE
+// address, and a fragment read of chunk c = 2 ks + h finds it there (16 lanes of a ds_read_b128 group:
+// 16 distinct bank slots).  Fragment reads are inline asm: a compiler-visible LDS read of the DMA target
+// would be preceded by `s_waitcnt vmcnt(0)`, draining the ring.
+__device__ __forceinline__ nerf_bf16x8 ntb_lds_read(uint32_t byte_addr) {
+  nerf_bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(byte_addr));
+  return v;
+}
+__device__ __forceinline__ void ntb_wait_vmcnt(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+  }
+}
+
+template <int BM, int BN, int WAVES_M, int EPI, int OUT_BF16, int STAGES, int MINW>
+__global__ __launch_bounds__(256, MINW) void gemm_nt_bf16_ring_kernel(const nerf_bf16* __restrict__ A, int lda,
+                                                                     const nerf_bf16* __restrict__ B, int ldb,
+                                                                     const float* __restrict__ bias,
+                                                                     void* __restrict__ Cv, int ldc,
+                                                                     const uint32_t* __restrict__ mbits, int ldmb,
+                                                                     uint32_t* __restrict__ mbits_out, int K,
+                                                                     int n_ntiles, int n_tiles) {
+  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0, "wave tile");
+  constexpr int BK = 32;                          // bf16 per row per slab: 64 B
+  constexpr int STAGE_E = (BM + BN) * BK;         // bf16 elements per stage
+  constexpr int NPIECE = (BM + BN) / 16;          // 1 KiB DMA pieces per stage (16 rows each)
+  constexpr int PPW = (NPIECE + 3) / 4;
+  static_assert(STAGES >= 2 && (STAGES - 2) * PPW <= 12, "ring depth");
+  __shared__ __attribute__((aligned(16))) nerf_bf16 smem[STAGES * STAGE_E];
+
+  const int grid = gridDim.x;
+  const int t0 = xcd_remap(blockIdx.x, grid);
+  if (t0 >= n_tiles) return;
+  const int my_tiles = (n_tiles - t0 + grid - 1) / grid;
+  const int nk = K / BK;
+  const int total = my_tiles * nk;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int li = lane & 31, lh = lane >> 5;
+  const int MYP = (NPIECE % 4 == 0) ? PPW : (NPIECE - wave + 3) / 4;
+
+  // this lane's piece rows (A rows first, then B rows) and swizzled source chunk
+  int prow[PPW], pch[PPW];
+  bool pa[PPW];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    const int piece = wave + 4 * j;
+    const int r = piece * 16 + (lane >> 2);
+    pa[j] = r < BM;
+    prow[j] = pa[j] ? r : r - BM;
+    pch[j] = (lane & 3) ^ ((prow[j] >> 2) & 3);
+  }
+  const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+
+  auto issue = [&](int g) {
+    const int ti = g / nk, kt = g - ti * nk;
+    const int tile = t0 + ti * grid;
+    const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
+    nerf_bf16* st = smem + (g % STAGES) * STAGE_E;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int piece = wave + 4 * j;
+      if (NPIECE % 4 == 0 || piece < NPIECE) {
+        const nerf_bf16* src = pa[j] ? A + ((int64_t)mt * BM + prow[j]) * lda + kt * BK + 8 * pch[j]
+                                     : B + ((int64_t)nt * BN + prow[j]) * ldb + kt * BK + 8 * pch[j];
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(st + piece * 512),
+                                         16, 0, 0);
+      }
+    }
+  };
+
+  uint32_t a_off[TM], b_off[TN];
+  int a_sw[TM], b_sw[TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+    const int r = wm * WTM + a * 32 + li;
+    a_off[a] = (uint32_t)(r * BK * 2);
+    a_sw[a] = (r >> 2) & 3;
+  }
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
-    const int nb = n0 + wn * WTN + b * 32;
-    const int g = nb >> 5;
-    float4 bv[4];
+    const int r = wn * WTN + b * 32 + li;
+    b_off[b] = (uint32_t)((BM + r) * BK * 2);
+    b_sw[b] = (r >> 2) & 3;
+  }
+
+  nerf_f32x16 acc[TM][TN];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      bv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) bv[q] = *reinterpret_cast<const float4*>(bias + nb + 8 * q + 4 * lh);
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+#pragma unroll
+  for (int s0 = 0; s0 < STAGES - 1; ++s0)
+    if (s0 < total) issue(s0);
+
+  for (int g = 0; g < total; ++g) {
+    // retire slab g: this wave's pieces of the younger in-flight slabs (at most STAGES-2) may stay outstanding
+    const int younger = (total - 1 - g) < (STAGES - 2) ? (total - 1 - g) : (STAGES - 2);
+    ntb_wait_vmcnt(younger * MYP);
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of slab g landed; every wave done reading slab g-1
+    if (g + STAGES - 1 < total) issue(g + STAGES - 1);
+    const uint32_t st = sbase + (uint32_t)((g % STAGES) * STAGE_E * 2);
+    nerf_bf16x8 af[2][TM], bf[2][TN];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a) af[ks][a] = ntb_lds_read(st + a_off[a] + 16 * ((2 * ks + lh) ^ a_sw[a]));
+#pragma unroll
+      for (int b = 0; b < TN; ++b) bf[ks][b] = ntb_lds_read(st + b_off[b] + 16 * ((2 * ks + lh) ^ b_sw[b]));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a) asm volatile("" : "+v"(af[ks][a]));
+#pragma unroll
+      for (int b = 0; b < TN; ++b) asm volatile("" : "+v"(bf[ks][b]));
     }
 #pragma unroll
-    for (int a = 0; a < TM; ++a) {
-      const int64_t m = m0 + wm * WTM + a * 32 + li;
-      uint32_t word = 0;
-      if (EPI == EPI_MASK) word = mbits[m * ldmb + g];
-      uint2 pk[4];
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float v[4];
+      for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = acc[a][b][4 * q + e];
-          const float bb = e == 0 ? bv[q].x : (e == 1 ? bv[q].y : (e == 2 ? bv[q].z : bv[q].w));
-          if (EPI == EPI_BIAS) v[e] += bb;
-          if (EPI == EPI_BIAS_RELU) {
-            v[e] = fmaxf(v[e] + bb, 0.f);
-            word |= (v[e] > 0.f ? 1u : 0u) << (8 * q + 4 * lh + e);
-          }
-          if (EPI == EPI_MASK) v[e] = ((word >> (8 * q + 4 * lh + e)) & 1u) ? v[e] : 0.f;
-        }
-        if constexpr (OUT_BF16) {
-          pk[q] = make_uint2(nerf_pack_bf16x2(v[0], v[1]), nerf_pack_bf16x2(v[2], v[3]));
-        } else {
-          *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cv) + m * ldc + nb + 8 * q + 4 * lh) =
-              make_float4(v[0], v[1], v[2], v[3]);
-        }
-      }
-      if constexpr (OUT_BF16) {
-        // T21 (cdna_hip_programming.md): lanes li / li + 32 hold columns 8q..8q+3 / 8q+4..8q+7 of the same row;
-        // one v_permlane32_swap per dword of the (q, q + 1) pair leaves 16 contiguous bytes in every lane
-        // (low half: columns 16p..16p+7, high half: 16p+8..16p+15) -> one 16-B store per pair.
+        for (int b = 0; b < TN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[ks][b], af[ks][a], acc[a][b], 0, 0, 0);
+    const int ti = g / nk;
+    if (g - ti * nk == nk - 1) {
+      const int tile = t0 + ti * grid;
+      const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
+      ntb_epilogue<TM, TN, WTM, WTN, EPI, OUT_BF16>(acc, (int64_t)mt * BM + wm * WTM, nt * BN + wn * WTN, li, lh, bias,
+                                                    Cv, ldc, mbits, ldmb, mbits_out);
 #pragma unroll
-        for (int pr = 0; pr < 2; ++pr) {
-          uint2 x = pk[2 * pr], y = pk[2 * pr + 1];
-          const auto r0 = __builtin_amdgcn_permlane32_swap(x.x, y.x, false, false);
-          const auto r1 = __builtin_amdgcn_permlane32_swap(x.y, y.y, false, false);
-          x.x = r0[0]; y.x = r0[1];
-          x.y = r1[0]; y.y = r1[1];
-          *reinterpret_cast<uint4*>(reinterpret_cast<nerf_bf16*>(Cv) + m * ldc + nb + 16 * pr + 8 * lh) =
-              make_uint4(x.x, x.y, y.x, y.y);
-        }
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ gemm_nt_bf16_wsr
+// Weights-stationary variant of the ring kernel: a persistent 512-thread block owns ONE BN-column slice of
+// B (the layer weights, BN x K bf16, loaded once into LDS) and streams 256-row panels of A through an
+// LDS-DMA ring.  Per output row the CUs then ingest only the 2K bytes of A (the ring kernel also re-reads
+// a 128-row B tile per 128-row A tile).  B image: row r (K/8 16-B chunks) keeps chunk c in slot
+// c ^ (r & 15) within its 256-B group (wsr_slot) -> the 16 rows of a ds_read_b128 group hit 16 distinct
+// bank slots (K = 64 and the K = 320 tail: 8-chunk groups, 2-way).
+// 8 waves = 4 (m) x 2 (n) of 64 x 64; blocks b and b + 8 (one XCD) take the two column slices of the same
+// panels.  LDS: B 2 K * BN bytes + STAGES * 16 KiB.
+// slot of 16-B chunk c of B row r: XOR-swizzled inside its aligned group of 16 chunks (8 for a row's
+// 8-chunk tail, K % 128 == 64), so the swizzle never leaves the row
+template <int KC>
+__device__ __forceinline__ int wsr_slot(int c, int r) {
+  static_assert(KC % 8 == 0, "K % 64");
+  const int base = c & ~15;
+  const int gmask = (base + 16 <= KC) ? 15 : 7;
+  return base | ((c ^ r) & gmask);
+}
+
+template <int K, int BN, int EPI, int OUT_BF16, int STAGES>
+__global__ __launch_bounds__(512, 1) void gemm_nt_bf16_wsr_kernel(const nerf_bf16* __restrict__ A, int lda,
+                                                                 const nerf_bf16* __restrict__ B, int ldb,
+                                                                 const float* __restrict__ bias,
+                                                                 void* __restrict__ Cv, int ldc,
+                                                                 const uint32_t* __restrict__ mbits, int ldmb,
+                                                                 uint32_t* __restrict__ mbits_out, int n_ntiles,
+                                                                 int n_panels) {
+  constexpr int BM = 256, WAVES_M = 4, WAVES_N = 2;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(TM >= 1 && TN >= 1, "wave tile");
+  constexpr int BK = 32;
+  constexpr int NK = K / BK;
+  static_assert(K % BK == 0, "k");
+  constexpr int STAGE_E = BM * BK;                // A only: 16 KiB
+  constexpr int B_E = BN * K;
+  constexpr int KC = K / 8;                       // 16-B chunks per B row
+  static_assert(STAGES >= 2 && (STAGES - 2) * 2 <= 12, "ring depth");
+  __shared__ __attribute__((aligned(16))) nerf_bf16 smem[B_E + STAGES * STAGE_E];
+
+  const int b = blockIdx.x;
+  const int cb = (b >> 3) % n_ntiles;
+  const int grp = (b & 7) + 8 * (b / (8 * n_ntiles));
+  const int n_groups = (gridDim.x / (8 * n_ntiles)) * 8;
+  const int n0 = cb * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int li = lane & 31, lh = lane >> 5;
+
+  // resident weight slice (plain loads + swizzled ds_write; once per block)
+  {
+    constexpr int NCH = BN * KC, PER = (NCH + 511) / 512;
+    uint4 v[PER];  // every load in flight before the first LDS write
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + 512 * j;
+      if (NCH % 512 == 0 || i < NCH) {
+        const int r = i / KC, c = i - r * KC;
+        v[j] = *reinterpret_cast<const uint4*>(B + (int64_t)(n0 + r) * ldb + 8 * c);
       }
-      if (EPI == EPI_BIAS_RELU && mbits_out) {
-        word |= __shfl_xor(word, 32, 64);
-        if (lh == 0) mbits_out[m * ldmb + g] = word;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + 512 * j;
+      if (NCH % 512 == 0 || i < NCH) {
+        const int r = i / KC, c = i - r * KC;
+        *reinterpret_cast<uint4*>(smem + r * K + 8 * wsr_slot<KC>(c, r)) = v[j];
       }
+    }
+  }
+  __syncthreads();
+  if (grp >= n_groups) return;
+  const int my_panels = grp < n_panels ? (n_panels - grp + n_groups - 1) / n_groups : 0;
+  const int total = my_panels * NK;
+
+  // A ring pieces: wave w loads rows [32 w, 32 w + 32) of each 256-row slab as two 1 KiB pieces
+  int prow[2], pch[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    prow[j] = 32 * wave + 16 * j + (lane >> 2);
+    pch[j] = (lane & 3) ^ ((prow[j] >> 2) & 3);
+  }
+  nerf_bf16* const ring = smem + B_E;
+  const uint32_t rbase = (uint32_t)(uintptr_t)ring, bbase = (uint32_t)(uintptr_t)smem;
+  auto issue = [&](int g) {
+    const int pi = g / NK, kt = g - pi * NK;
+    const int64_t m0 = (int64_t)(grp + pi * n_groups) * BM;
+    nerf_bf16* st = ring + (g % STAGES) * STAGE_E;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const nerf_bf16* src = A + (m0 + prow[j]) * lda + kt * BK + 8 * pch[j];
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(st + (2 * wave + j) * 512), 16, 0, 0);
+    }
+  };
+
+  uint32_t a_off[TM];
+  int a_sw[TM];
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+    const int r = wm * WTM + a * 32 + li;
+    a_off[a] = (uint32_t)(r * BK * 2);
+    a_sw[a] = (r >> 2) & 3;
+  }
+  uint32_t b_row[TN];
+  int b_sw[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    const int r = wn * WTN + t * 32 + li;
+    b_row[t] = bbase + (uint32_t)(r * K * 2);
+    b_sw[t] = r & 15;
+  }
+
+  nerf_f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][t][r] = 0.f;
+
+#pragma unroll
+  for (int s0 = 0; s0 < STAGES - 1; ++s0)
+    if (s0 < total) issue(s0);
+
+  for (int g = 0; g < total; ++g) {
+    const int younger = (total - 1 - g) < (STAGES - 2) ? (total - 1 - g) : (STAGES - 2);
+    ntb_wait_vmcnt(younger * 2);
+    __builtin_amdgcn_s_barrier();
+    if (g + STAGES - 1 < total) issue(g + STAGES - 1);
+    const int pi = g / NK, kt = g - pi * NK;
+    const uint32_t st = rbase + (uint32_t)((g % STAGES) * STAGE_E * 2);
+    nerf_bf16x8 af[2][TM], bf[2][TN];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a) af[ks][a] = ntb_lds_read(st + a_off[a] + 16 * ((2 * ks + lh) ^ a_sw[a]));
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        const int c = 4 * kt + 2 * ks + lh;  // chunk of the B row
+        bf[ks][t] = ntb_lds_read(b_row[t] + 16 * wsr_slot<KC>(c, b_sw[t]));
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a) asm volatile("" : "+v"(af[ks][a]));
+#pragma unroll
+      for (int t = 0; t < TN; ++t) asm volatile("" : "+v"(bf[ks][t]));
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int t = 0; t < TN; ++t)
+          acc[a][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[ks][t], af[ks][a], acc[a][t], 0, 0, 0);
+    if (kt == NK - 1) {
+      const int64_t m0 = (int64_t)(grp + pi * n_groups) * BM;
+      ntb_epilogue<TM, TN, WTM, WTN, EPI, OUT_BF16>(acc, m0 + wm * WTM, n0 + wn * WTN, li, lh, bias, Cv, ldc, mbits,
+                                                    ldmb, mbits_out);
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int t = 0; t < TN; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[a][t][r] = 0.f;
     }
   }
 }

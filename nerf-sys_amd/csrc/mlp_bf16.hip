@@ -236,9 +236,25 @@ int launch_ntb(const nerf_bf16* A, int lda, const nerf_bf16* B, int ldb, const f
   return NERF_OK;
 }
 
+// weights-stationary persistent kernel (gemm_bf16.hpp, gemm_nt_bf16_wsr): one 512-thread block per CU
+template <int K, int EPI, int OUT_BF16, int STAGES>
+int launch_wsr(const nerf_bf16* A, int lda, const nerf_bf16* B, int ldb, const float* bias, void* C, int ldc,
+               const uint32_t* mbits, uint32_t* mbits_out, int64_t M, int N, hipStream_t st) {
+  if (M % 256 || N % 128) return NERF_E_ARG;
+  const int ntn = N / 128;
+  gemm_nt_bf16_wsr_kernel<K, 128, EPI, OUT_BF16, STAGES><<<256, 512, 0, st>>>(A, lda, B, ldb, bias, C, ldc, mbits, N / 32,
+                                                                             mbits_out, ntn, (int)(M / 256));
+  return NERF_OK;
+}
+
 template <int EPI, int OUT_BF16>
 int ntb(const nerf_bf16* A, int lda, const nerf_bf16* B, int ldb, const float* bias, void* C, int ldc,
         const uint32_t* mbits, uint32_t* mbits_out, int64_t M, int N, int K, hipStream_t st) {
+  if ((N == 256 || N == 128) && OUT_BF16) {  // the trunk / colour-0 layers: HBM-bound, weights stationary
+    if (K == 256) return launch_wsr<256, EPI, OUT_BF16, 5>(A, lda, B, ldb, bias, C, ldc, mbits, mbits_out, M, N, st);
+    if (K == 320) return launch_wsr<320, EPI, OUT_BF16, 4>(A, lda, B, ldb, bias, C, ldc, mbits, mbits_out, M, N, st);
+    if (K == 64) return launch_wsr<64, EPI, OUT_BF16, 5>(A, lda, B, ldb, bias, C, ldc, mbits, mbits_out, M, N, st);
+  }
   if (N == 256 || N == 128)
     return launch_ntb<128, 128, 2, EPI, OUT_BF16>(A, lda, B, ldb, bias, C, ldc, mbits, mbits_out, M, N, K, st);
   if (N == 32) return launch_ntb<256, 32, 4, EPI, OUT_BF16>(A, lda, B, ldb, bias, C, ldc, mbits, mbits_out, M, N, K, st);

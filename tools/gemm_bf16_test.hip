@@ -136,14 +136,22 @@ int main(int argc, char** argv) {
         case 1: gemm_nt_bf16_kernel<128, 128, 2, EPI_MASK, 1><<<nb, 256>>>(A, K, B, K, nullptr, C, N, mb, 8, nullptr, K, 2); break;
         case 2: gemm_wgrad_bf16_kernel<128, 128, 2><<<4 * S, 256>>>(A, K, C, N, P, 256, P + 65536, slab, M / S, M, 2, 4); break;
         case 3: gemm_nt_bf16_kernel<128, 128, 2, EPI_BIAS_RELU, 1, 32, 3><<<nb, 256>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, K, 2); break;
-        case 4: gemm_nt_bf16_kernel<128, 128, 2, EPI_BIAS_RELU, 1, 32, 4><<<nb, 256>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, K, 2); break;
+        case 4: gemm_nt_bf16_ring_kernel<128, 128, 2, EPI_BIAS_RELU, 1, 4, 2><<<512, 256>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, K, 2, (int)nb); break;
+        case 5: gemm_nt_bf16_ring_kernel<128, 128, 2, EPI_BIAS_RELU, 1, 3, 3><<<768, 256>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, K, 2, (int)nb); break;
+        case 6: gemm_nt_bf16_ring_kernel<128, 128, 2, EPI_MASK, 1, 4, 2><<<512, 256>>>(A, K, B, K, nullptr, C, N, mb, 8, nullptr, K, 2, (int)nb); break;
+        case 7: gemm_nt_bf16_wsr_kernel<256, 128, EPI_BIAS_RELU, 1, 5><<<256, 512>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, 2, (int)(M / 256)); break;
+        case 8: gemm_nt_bf16_wsr_kernel<256, 128, EPI_MASK, 1, 5><<<256, 512>>>(A, K, B, K, nullptr, C, N, mb, 8, nullptr, 2, (int)(M / 256)); break;
+        case 9: gemm_nt_bf16_wsr_kernel<256, 128, EPI_BIAS_RELU, 1, 4><<<256, 512>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, 2, (int)(M / 256)); break;
+        case 10: gemm_nt_bf16_wsr_kernel<256, 128, EPI_BIAS_RELU, 1, 5><<<256, 512>>>(A, K, B, K, bias, C, 0, nullptr, 8, nullptr, 2, (int)(M / 256)); break;
+        case 11: gemm_nt_bf16_wsr_kernel<256, 128, EPI_BIAS_RELU, 1, 5><<<512, 512>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, 2, (int)(M / 256)); break;
       }
     };
-    const int NV = 5;
+    const int NV = 12;
     const char* names[NV] = {"nt_bf16 fwd bias+relu", "nt_bf16 dgrad mask", "wgrad_bf16 split-M", "nt_bf16 fwd BK=32 w3",
-                             "nt_bf16 fwd BK=32 w4"};
-    const double bytes[NV] = {M * 256.0 * 2 * 2 + M * 32.0, M * 256.0 * 2 * 2 + M * 32.0, M * 256.0 * 2 * 2,
-                              M * 256.0 * 2 * 2 + M * 32.0, M * 256.0 * 2 * 2 + M * 32.0};
+                             "ring fwd S=4 x2", "ring fwd S=3 x3", "ring dgrad S=4 x2", "wsr fwd S=5", "wsr dgrad S=5",
+                             "wsr fwd S=4", "wsr fwd no-store", "wsr fwd grid512"};
+    const double fb = M * 256.0 * 2 * 2 + M * 32.0;
+    const double bytes[NV] = {fb, fb, M * 256.0 * 2 * 2, fb, fb, fb, fb, fb, fb, fb, M * 256.0 * 2, fb};
     for (int v = 0; v < NV; ++v) run(v);
     CK(hipDeviceSynchronize());
     std::vector<float> ms[NV];
@@ -158,6 +166,65 @@ int main(int argc, char** argv) {
       printf("%-24s median %.4f ms  %.0f TFLOP/s (%.1f%% of 2500)  %.2f TB/s algorithmic (%.1f%% of 8)\n", names[v], t,
              2.0 * M * N * K / t * 1e-9, 2.0 * M * N * K / t * 1e-9 / 2500 * 100, bytes[v] / t * 1e-9,
              bytes[v] / t * 1e-9 / 8 * 100);
+    }
+  }
+  // ring kernel == register-staged kernel, bitwise (same k order), bf16 relu out + mask, at C3 size
+  {
+    const int64_t M = 4096LL * 48;
+    const int N = 256, K = 256;
+    std::vector<uint16_t> h((size_t)M * K);
+    for (auto& v : h) v = f2bf(U(rng));
+    nerf_bf16 *A, *B, *C1, *C2; float* bias; uint32_t *m1, *m2;
+    // B also serves the K = 320 case (ldb 320)
+    CK(hipMalloc(&A, M * K * 2)); CK(hipMalloc(&B, N * 320 * 2)); CK(hipMalloc(&C1, M * N * 2)); CK(hipMalloc(&C2, M * N * 2));
+    CK(hipMalloc(&bias, N * 4)); CK(hipMalloc(&m1, M * 32)); CK(hipMalloc(&m2, M * 32));
+    CK(hipMemcpy(A, h.data(), M * K * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(B, h.data() + 77, N * 320 * 2, hipMemcpyHostToDevice));
+    std::vector<float> bb(N); for (auto& v : bb) v = U(rng);
+    CK(hipMemcpy(bias, bb.data(), N * 4, hipMemcpyHostToDevice));
+    const int nt = (int)((M / 128) * 2);
+    gemm_nt_bf16_kernel<128, 128, 2, EPI_BIAS_RELU, 1, 32, 3><<<nt, 256>>>(A, K, B, K, bias, C1, N, nullptr, 8, m1, K, 2);
+    gemm_nt_bf16_ring_kernel<128, 128, 2, EPI_BIAS_RELU, 1, 4, 2><<<300, 256>>>(A, K, B, K, bias, C2, N, nullptr, 8, m2, K, 2, nt);
+    CK(hipDeviceSynchronize());
+    std::vector<uint16_t> c1(M * N), c2(M * N); std::vector<uint32_t> k1(M * 8), k2(M * 8);
+    CK(hipMemcpy(c1.data(), C1, M * N * 2, hipMemcpyDeviceToHost)); CK(hipMemcpy(c2.data(), C2, M * N * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(k1.data(), m1, M * 32, hipMemcpyDeviceToHost)); CK(hipMemcpy(k2.data(), m2, M * 32, hipMemcpyDeviceToHost));
+    size_t nd = 0, ndm = 0;
+    for (size_t i = 0; i < c1.size(); ++i) nd += c1[i] != c2[i];
+    for (size_t i = 0; i < k1.size(); ++i) ndm += k1[i] != k2[i];
+    // EPI_MASK ring vs register-staged
+    gemm_nt_bf16_kernel<128, 128, 2, EPI_MASK, 1, 32, 3><<<nt, 256>>>(A, K, B, K, nullptr, C1, N, m1, 8, nullptr, K, 2);
+    gemm_nt_bf16_ring_kernel<128, 128, 2, EPI_MASK, 1, 3, 3><<<257, 256>>>(A, K, B, K, nullptr, C2, N, m1, 8, nullptr, K, 2, nt);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(c1.data(), C1, M * N * 2, hipMemcpyDeviceToHost)); CK(hipMemcpy(c2.data(), C2, M * N * 2, hipMemcpyDeviceToHost));
+    size_t nd2 = 0;
+    for (size_t i = 0; i < c1.size(); ++i) nd2 += c1[i] != c2[i];
+    printf("ring vs register-staged: fwd %zu differing outputs, %zu mask words; dgrad %zu differing\n", nd, ndm, nd2);
+    bad += (nd || ndm || nd2);
+    gemm_nt_bf16_kernel<128, 128, 2, EPI_BIAS_RELU, 1, 32, 3><<<nt, 256>>>(A, K, B, K, bias, C1, N, nullptr, 8, m1, K, 2);
+    gemm_nt_bf16_wsr_kernel<256, 128, EPI_BIAS_RELU, 1, 5><<<256, 512>>>(A, K, B, K, bias, C2, N, nullptr, 8, m2, 2, (int)(M / 256));
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(c1.data(), C1, M * N * 2, hipMemcpyDeviceToHost)); CK(hipMemcpy(c2.data(), C2, M * N * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(k1.data(), m1, M * 32, hipMemcpyDeviceToHost)); CK(hipMemcpy(k2.data(), m2, M * 32, hipMemcpyDeviceToHost));
+    nd = 0; ndm = 0;
+    for (size_t i = 0; i < c1.size(); ++i) nd += c1[i] != c2[i];
+    for (size_t i = 0; i < k1.size(); ++i) ndm += k1[i] != k2[i];
+    printf("wsr vs register-staged: fwd %zu differing outputs, %zu mask words\n", nd, ndm);
+    bad += (nd || ndm);
+    // K = 320 (trunk.4, lda 320) and K = 64 (trunk.0 / colour layer 0)
+    for (int KK : {320, 64}) {
+      // only the first M/2 rows: A holds M x 256 elements, so M/2 rows of 320 (or 64) fit
+      gemm_nt_bf16_kernel<128, 128, 2, EPI_BIAS_RELU, 1, 32, 3><<<nt / 2, 256>>>(A, KK, B, KK, bias, C1, N, nullptr, 8, m1, KK, 2);
+      if (KK == 320)
+        gemm_nt_bf16_wsr_kernel<320, 128, EPI_BIAS_RELU, 1, 4><<<256, 512>>>(A, KK, B, KK, bias, C2, N, nullptr, 8, m2, 2, (int)(M / 256 / 2));
+      else
+        gemm_nt_bf16_wsr_kernel<64, 128, EPI_BIAS_RELU, 1, 5><<<256, 512>>>(A, KK, B, KK, bias, C2, N, nullptr, 8, m2, 2, (int)(M / 256 / 2));
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(c1.data(), C1, M / 2 * N * 2, hipMemcpyDeviceToHost)); CK(hipMemcpy(c2.data(), C2, M / 2 * N * 2, hipMemcpyDeviceToHost));
+      nd = 0;
+      for (size_t i = 0; i < (size_t)(M / 2 * N); ++i) nd += c1[i] != c2[i];
+      printf("wsr K=%d vs register-staged: %zu differing outputs (first M/2 rows)\n", KK, nd);
+      bad += nd != 0;
     }
   }
   printf(bad ? "FAILED\n" : "OK\n");
