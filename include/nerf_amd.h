@@ -156,6 +156,78 @@ int nerf_adam(float* p, const float* g, float* m, float* v, int64_t n, const int
               const double* seg_lr_host, int n_seg, double beta1, double beta2, float eps, float weight_decay,
               int step, const float* partials, float max_norm, hipStream_t stream);
 
+/* ------------------------------------------------------------------ Instant-NGP expert */
+
+#define NERF_HASH_MAX_LEVELS 32
+
+/* HashGridEncoder configuration (models/encodings.py:175-270).  resolutions[l] are the integers the
+ * reference computes, floor(min_res * growth**l) in fp32 (:205-209).  interpolation: 0 Nearest,
+ * 1 Linear, 2 Smoothstep (:331-361).  levels*features_per_level <= 64, features_per_level in {1,2,4,8}. */
+typedef struct {
+  int32_t levels;
+  int32_t features_per_level;
+  int32_t log2_hashmap_size;
+  int32_t interpolation;
+  int32_t resolutions[NERF_HASH_MAX_LEVELS];
+} NerfHashGrid;
+
+/* HashGridEncoder._torch_forward (models/encodings.py:313-381) with _hash/_gather (:288-311): table
+ * (levels * 2^log2 , F) fp32.  Positions x (M rows, pitch x_stride floats, first 3 used).  If aabb (HOST
+ * pointer, 6 floats: min xyz, max xyz — part of the expert's configuration) is non-NULL the positions are world coordinates mapped as
+ * MetaNGP._world_to_unit (models/inr/meta_ngp.py:166-169): clamp((x-min)/extent, eps, 1-eps); else x is
+ * used as given.  out (M rows, pitch out_stride >= levels*F): cols [0, L*F) = [level0 f0..fF-1, level1 ...],
+ * cols [L*F, out_stride) zero. */
+int nerf_hash_encode(const NerfHashGrid* grid, const float* table, const float* x, int64_t x_stride, int64_t M,
+                     const float* aabb, float enc_eps, float* out, int out_stride, hipStream_t stream);
+
+/* Backward of nerf_hash_encode w.r.t. the table (autograd of the reference's gather + trilinear blend):
+ * d_table += scatter of d_out (M rows, pitch d_stride).  Accumulates with fp32 atomics (the caller zeroes
+ * d_table first); the order of the additions is not deterministic. */
+int nerf_hash_encode_bwd(const NerfHashGrid* grid, const float* x, int64_t x_stride, int64_t M, const float* aabb,
+                         float enc_eps, const float* d_out, int d_stride, float* d_table, hipStream_t stream);
+
+/* SHEncoder.forward (models/encodings.py:133-151, components :27-81): normalise (clamp 1e-9), real SH of
+ * degree levels-1 (levels 1..5) -> out (M rows, pitch out_stride >= levels^2). */
+int nerf_sh_encode(const float* d, int64_t d_stride, int64_t M, int levels, float* out, int out_stride,
+                   hipStream_t stream);
+
+/* MetaNGP networks (models/inr/meta_ngp.py:75-105): sigma trunk of sigma_depth ReLU layers (hidden),
+ * sigma_head (1) + geo_head (geo_feat_dim), colour MLP of color_depth ReLU layers (color_hidden) on
+ * cat([geo, dir-enc]) and a 3-wide output (sigmoid if use_sigmoid_rgb).  dir_encoding: 0 spherical
+ * harmonics (sh_levels), 1 FrequencyEncoder(3, 4, include_input).  Every width <= 64, 1+geo <= 32. */
+typedef struct {
+  int32_t in_dim;
+  int32_t hidden;
+  int32_t sigma_depth;
+  int32_t geo_feat_dim;
+  int32_t color_hidden;
+  int32_t color_depth;
+  int32_t dir_encoding;
+  int32_t sh_levels;
+  int32_t use_sigmoid_rgb;
+} NerfNgpNet;
+
+/* Packed parameter layout: per layer (trunk 0..sd-1, head, colour 0..cd-1, out) W (Npad x Kpad) then
+ * b (Npad), PyTorch (out,in) row-major, zero padded to multiples of 32; the head's rows are [sigma, geo...].
+ * table (may be NULL) receives 4 int64 per tensor {offset, rows_pad, cols_pad, cols_real}; *n_tensors the
+ * tensor count.  Returns the packed float count, or <0 for an unsupported configuration. */
+int64_t nerf_ngp_layout(const NerfNgpNet* net, int64_t* table, int32_t* n_tensors);
+
+/* Workspace (bytes) of nerf_ngp_bwd for M samples (per-workgroup weight-gradient slabs). */
+int64_t nerf_ngp_workspace_bytes(const NerfNgpNet* net, int64_t M);
+
+/* MetaNGP.forward after the xyz encoding (meta_ngp.py:182-255): enc (M rows, pitch enc_stride) from
+ * nerf_hash_encode, directions x_d[:,3:6] (x_d (M,6)) -> rgb_sigma (M,4).  One fused kernel: all layers
+ * run on fp32 MFMA with the activations in LDS. */
+int nerf_ngp_fwd(const NerfNgpNet* net, const float* w, const float* enc, int enc_stride, const float* x_d,
+                 int64_t M, float* rgb_sigma, hipStream_t stream);
+
+/* Backward of nerf_ngp_fwd (recomputes the forward on chip): d_enc (M rows, pitch enc_stride; cols
+ * >= in_dim untouched) and d_w (packed layout; overwritten, or accumulated into if accumulate != 0). */
+int nerf_ngp_bwd(const NerfNgpNet* net, const float* w, const float* enc, int enc_stride, const float* x_d,
+                 int64_t M, const float* d_rgb_sigma, float* d_enc, float* d_w, int accumulate, void* ws,
+                 int64_t ws_bytes, hipStream_t stream);
+
 /* Library build identification (string, static). */
 const char* nerf_version(void);
 

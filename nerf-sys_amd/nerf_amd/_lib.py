@@ -49,6 +49,13 @@ def lib():
             "nerf_grad_sqnorm": [P, I64, P, P],
             "nerf_adam": [P, P, P, P, I64, P, P, I, D, D, F, F, I, P, F, P],
             "nerf_version": [],
+            "nerf_hash_encode": [P, P, P, I64, I64, P, F, P, I, P],
+            "nerf_hash_encode_bwd": [P, P, I64, I64, P, F, P, I, P, P],
+            "nerf_sh_encode": [P, I64, I64, I, P, I, P],
+            "nerf_ngp_layout": [P, P, P],
+            "nerf_ngp_workspace_bytes": [P, I64],
+            "nerf_ngp_fwd": [P, P, P, I, P, I64, P, P],
+            "nerf_ngp_bwd": [P, P, P, I, P, I64, P, P, P, I, P, I64, P],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -58,6 +65,8 @@ def lib():
         L.nerf_mlp_workspace_bytes.restype = c_int64
         L.nerf_mlp_workspace_bytes_bf16.restype = c_int64
         L.nerf_version.restype = ctypes.c_char_p
+        L.nerf_ngp_layout.restype = c_int64
+        L.nerf_ngp_workspace_bytes.restype = c_int64
         _lib = L
     return _lib
 
@@ -66,7 +75,9 @@ EXPORTS = ("nerf_rays_gen", "nerf_pick_pixels", "nerf_clamp_near_far", "nerf_ray
            "nerf_sample_stratified", "nerf_build_xd", "nerf_sample_pdf", "nerf_freq_encode",
            "nerf_mlp_layout", "nerf_mlp_workspace_bytes", "nerf_mlp_fwd", "nerf_mlp_bwd",
            "nerf_mlp_workspace_bytes_bf16", "nerf_mlp_fwd_bf16", "nerf_mlp_bwd_bf16",
-           "nerf_composite_fwd", "nerf_composite_bwd", "nerf_grad_sqnorm", "nerf_adam", "nerf_version")
+           "nerf_composite_fwd", "nerf_composite_bwd", "nerf_grad_sqnorm", "nerf_adam", "nerf_version",
+           "nerf_hash_encode", "nerf_hash_encode_bwd", "nerf_sh_encode", "nerf_ngp_layout",
+           "nerf_ngp_workspace_bytes", "nerf_ngp_fwd", "nerf_ngp_bwd")
 
 
 def check(status: int, what: str) -> None:

@@ -1,0 +1,394 @@
+"""The Instant-NGP expert on the HIP kernels: ``HashGridEncoder``, ``SHEncoder`` and
+``InstantNGP`` — drop-in mirrors of the reference's torch backends
+
+    HashGridEncoder   models/encodings.py:158-381   (torch fallback: int64 hash, every level hashed)
+    SHEncoder         models/encodings.py:84-151    (real SH, degree levels-1)
+    MetaNGP           models/inr/meta_ngp.py:15-255, get_param_groups :446-469
+
+with the same constructor arguments, parameter names (``xyz_encoder.hash_table``,
+``sigma_trunk.{i}.linear.*``, ``sigma_head.*``, ``geo_head.*``, ``color_mlp.{j}.linear.*``,
+``color_mlp.{D}.*``), the expert contract ``expert(x_d (M,6), params=None) -> (M,4)`` and the MetaModule
+fast-weights surface (the hash table is not a fast weight, as in the reference: HashGridEncoder is not a
+MetaModule, metamodule.py:20-30).
+
+Compute: ``nerf_hash_encode`` (gather, world->unit mapping fused) -> ``nerf_ngp_fwd`` (all MLP layers in
+one fused fp32-MFMA kernel) ; backward ``nerf_ngp_bwd`` (forward recomputed on chip, weight gradients
+reduced per workgroup) -> ``nerf_hash_encode_bwd`` (fp32 atomics into the table gradient).  No CPU
+fallback: every op requires HIP tensors.  The occupancy renderer (``use_occ``) is §8f row 2 and not built:
+requesting it raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import warnings
+from collections import OrderedDict
+from typing import Dict, Optional
+
+import torch
+import torch.nn as nn
+from torch.autograd.function import once_differentiable
+
+from ._lib import check, lib, need, ptr, stream
+from .vanilla import VanillaNeRF
+
+_INTERP = {"Nearest": 0, "Linear": 1, "Smoothstep": 2}
+
+
+class NerfHashGrid(ctypes.Structure):
+    _fields_ = [("levels", ctypes.c_int32), ("features_per_level", ctypes.c_int32),
+                ("log2_hashmap_size", ctypes.c_int32), ("interpolation", ctypes.c_int32),
+                ("resolutions", ctypes.c_int32 * 32)]
+
+
+class NerfNgpNet(ctypes.Structure):
+    _fields_ = [("in_dim", ctypes.c_int32), ("hidden", ctypes.c_int32), ("sigma_depth", ctypes.c_int32),
+                ("geo_feat_dim", ctypes.c_int32), ("color_hidden", ctypes.c_int32),
+                ("color_depth", ctypes.c_int32), ("dir_encoding", ctypes.c_int32), ("sh_levels", ctypes.c_int32),
+                ("use_sigmoid_rgb", ctypes.c_int32)]
+
+
+def _addr(s):
+    return ctypes.c_void_p(ctypes.addressof(s))
+
+
+# ------------------------------------------------------------------------------------------ kernel wrappers
+
+def hash_encode(grid: NerfHashGrid, table, x, aabb=None, enc_eps=1e-6, out_stride=None):
+    """nerf_hash_encode: x (M, >=3) rows (pitch = x.stride(0)); aabb: host sequence of 6 floats or None."""
+    need(table, "hash_table")
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    M = x.shape[0]
+    od = grid.levels * grid.features_per_level
+    os_ = out_stride or od
+    out = torch.empty((M, os_), dtype=torch.float32, device=x.device)
+    ab = (ctypes.c_float * 6)(*[float(v) for v in aabb]) if aabb is not None else None
+    check(lib().nerf_hash_encode(_addr(grid), ptr(table), ptr(x), x.stride(0), M, ab, float(enc_eps), ptr(out),
+                                 os_, stream()), "nerf_hash_encode")
+    return out
+
+
+def hash_encode_bwd(grid: NerfHashGrid, x, d_out, n_table_rows, aabb=None, enc_eps=1e-6, d_table=None):
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    need(d_out, "d_out")
+    if d_table is None:
+        d_table = torch.zeros((n_table_rows, grid.features_per_level), dtype=torch.float32, device=x.device)
+    ab = (ctypes.c_float * 6)(*[float(v) for v in aabb]) if aabb is not None else None
+    check(lib().nerf_hash_encode_bwd(_addr(grid), ptr(x), x.stride(0), x.shape[0], ab, float(enc_eps), ptr(d_out),
+                                     d_out.stride(0), ptr(d_table), stream()), "nerf_hash_encode_bwd")
+    return d_table
+
+
+def sh_encode(d, levels=4):
+    if d.stride(-1) != 1:
+        d = d.contiguous()
+    need(d if d.is_contiguous() else d.contiguous(), "d")
+    out = torch.empty((d.shape[0], levels * levels), dtype=torch.float32, device=d.device)
+    check(lib().nerf_sh_encode(ptr(d), d.stride(0), d.shape[0], int(levels), ptr(out), levels * levels, stream()),
+          "nerf_sh_encode")
+    return out
+
+
+# ------------------------------------------------------------------------------------------ encoders
+
+def level_resolutions(levels, min_res, max_res):
+    """HashGridEncoder ctor (models/encodings.py:196-210): growth factor in float64, resolutions
+    floor(min_res * growth**arange(L)) in float32 — the same torch expression, host side."""
+    g = 1.0 if levels <= 1 else float(math.exp((math.log(max_res) - math.log(min_res)) / (levels - 1)))
+    lv = torch.arange(levels, dtype=torch.float32)
+    return torch.floor(min_res * (g ** lv)).to(torch.int32), g
+
+
+class _HashEncodeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, table, grid, aabb, eps):
+        ctx.grid, ctx.aabb, ctx.eps = grid, aabb, eps
+        ctx.save_for_backward(x)
+        ctx.rows = table.shape[0]
+        return hash_encode(grid, table.detach(), x, aabb, eps)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError("HashGridEncoder (HIP): no gradient w.r.t. positions")
+        d_table = hash_encode_bwd(ctx.grid, x, g.contiguous(), ctx.rows, ctx.aabb, ctx.eps)
+        return None, d_table, None, None, None
+
+
+class HashGridEncoder(nn.Module):
+    """models/encodings.py:158-381 (torch backend semantics).  forward(x (...,3) in [0,1]) -> (..., L*F)."""
+
+    def __init__(self, levels: int = 16, min_res: int = 16, max_res: int = 4096, log2_hashmap_size: int = 19,
+                 features_per_level: int = 2, hash_init_scale: float = 1e-3, implementation: str = "tcnn",
+                 interpolation: Optional[str] = None) -> None:
+        super().__init__()
+        self.levels = int(levels)
+        self.min_res = int(min_res)
+        self.max_res = int(max_res)
+        self.features_per_level = int(features_per_level)
+        self.log2_hashmap_size = int(log2_hashmap_size)
+        self.hash_init_scale = float(hash_init_scale)
+        self.hash_table_size = 2 ** self.log2_hashmap_size
+        if interpolation is not None and interpolation not in _INTERP:
+            warnings.warn(f"[HashGridEncoder] interpolation '{interpolation}' not supported; using 'Linear'.",
+                          RuntimeWarning)
+            interpolation = "Linear"
+        self.interpolation = interpolation
+        res, self.growth_factor = level_resolutions(self.levels, self.min_res, self.max_res)
+        self.register_buffer("level_resolutions", res, persistent=False)
+        self.register_buffer("level_offsets", torch.arange(self.levels, dtype=torch.int64) * self.hash_table_size,
+                             persistent=False)
+        self._out_dim = self.levels * self.features_per_level
+        T = self.hash_table_size * self.levels
+        self.hash_table = nn.Parameter((torch.rand(T, self.features_per_level) * 2 - 1) * self.hash_init_scale)
+        g = NerfHashGrid()
+        g.levels, g.features_per_level, g.log2_hashmap_size = self.levels, self.features_per_level, self.log2_hashmap_size
+        g.interpolation = _INTERP[self.interpolation or "Linear"]
+        for i, r in enumerate(res.tolist()):
+            g.resolutions[i] = int(r)
+        self.grid = g
+
+    @property
+    def out_dim(self) -> int:
+        return self._out_dim
+
+    def get_out_dim(self) -> int:
+        return self._out_dim
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        assert x.shape[-1] == 3, f"Expected (...,3), got {tuple(x.shape)}"
+        flat = x.reshape(-1, 3).float().contiguous()
+        y = _HashEncodeFn.apply(flat, self.hash_table, self.grid, None, 0.0)
+        return y.view(*x.shape[:-1], self._out_dim)
+
+
+class SHEncoder(nn.Module):
+    """models/encodings.py:84-151: forward(d (...,3)) -> (..., levels^2) (directions normalised inside)."""
+
+    def __init__(self, levels: int = 4, implementation: str = "tcnn") -> None:
+        super().__init__()
+        if levels <= 0 or levels > 5:
+            raise ValueError(f"Supported levels ∈ [1, 5], got {levels}")
+        self.levels = int(levels)
+        self.degree = self.levels - 1
+        self._out_dim = self.levels ** 2
+
+    @property
+    def out_dim(self) -> int:
+        return self._out_dim
+
+    def forward(self, d: torch.Tensor) -> torch.Tensor:
+        assert d.shape[-1] == 3, f"Expected (...,3); got {tuple(d.shape)}"
+        y = sh_encode(d.reshape(-1, 3).float().contiguous(), self.levels)
+        return y.view(*d.shape[:-1], self._out_dim)
+
+
+# ------------------------------------------------------------------------------------------ MetaNGP
+
+
+class NgpLayout:
+    """Packed layout of one MetaNGP network (nerf_ngp_layout) + the index map of its named tensors."""
+
+    def __init__(self, net: NerfNgpNet, shapes: "OrderedDict[str, tuple]", sigma_depth: int, color_depth: int):
+        n = ctypes.c_int32(0)
+        total = int(lib().nerf_ngp_layout(_addr(net), None, ctypes.c_void_p(ctypes.addressof(n))))
+        if total < 0:
+            raise ValueError("unsupported MetaNGP configuration for the fused HIP MLP (every width <= 64, "
+                             "1+geo_feat_dim <= 32, geo+dir <= 64, <= 12 layers, LDS plan <= 160 KB)")
+        tbl = (ctypes.c_int64 * (4 * n.value))()
+        lib().nerf_ngp_layout(_addr(net), tbl, ctypes.c_void_p(ctypes.addressof(n)))
+        self.total = total
+        t = [(tbl[4 * i], tbl[4 * i + 1], tbl[4 * i + 2]) for i in range(n.value)]
+        place = {}
+        for i in range(sigma_depth):
+            place[f"sigma_trunk.{i}.linear.weight"] = (2 * i, 0)
+            place[f"sigma_trunk.{i}.linear.bias"] = (2 * i + 1, 0)
+        h = sigma_depth
+        place["sigma_head.weight"] = (2 * h, 0)
+        place["sigma_head.bias"] = (2 * h + 1, 0)
+        place["geo_head.weight"] = (2 * h, 1)
+        place["geo_head.bias"] = (2 * h + 1, 1)
+        for j in range(color_depth):
+            place[f"color_mlp.{j}.linear.weight"] = (2 * (h + 1 + j), 0)
+            place[f"color_mlp.{j}.linear.bias"] = (2 * (h + 1 + j) + 1, 0)
+        place[f"color_mlp.{color_depth}.weight"] = (2 * (h + 1 + color_depth), 0)
+        place[f"color_mlp.{color_depth}.bias"] = (2 * (h + 1 + color_depth) + 1, 0)
+        self.names = list(shapes)
+        idx = []
+        for name in self.names:
+            ti, r0 = place[name]
+            off, _, cols = t[ti]
+            shp = shapes[name]
+            r = shp[0]
+            c = shp[1] if len(shp) == 2 else 1
+            idx.append((off + torch.arange(r0, r0 + r).view(-1, 1) * cols + torch.arange(c).view(1, -1)).reshape(-1))
+        self.index = torch.cat(idx)
+        self._dev = {}
+
+    def pack(self, tensors):
+        flat = torch.cat([x.reshape(-1).to(torch.float32) for x in tensors])
+        key = str(flat.device)
+        if key not in self._dev:
+            self._dev[key] = self.index.to(flat.device)
+        return torch.zeros(self.total, dtype=torch.float32, device=flat.device).index_copy(0, self._dev[key], flat)
+
+
+class _NgpFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_d, table, w_packed, model):
+        x_d = x_d.contiguous().float()
+        M = x_d.shape[0]
+        enc = hash_encode(model.xyz_encoder.grid, table.detach(), x_d, model._aabb_host, model._eps)
+        out = torch.empty((M, 4), dtype=torch.float32, device=x_d.device)
+        net = model.net_struct
+        if M:
+            check(lib().nerf_ngp_fwd(_addr(net), ptr(w_packed), ptr(enc), enc.stride(0), ptr(x_d), M, ptr(out),
+                                     stream()), "nerf_ngp_fwd")
+        ctx.model = model
+        ctx.rows = table.shape[0]
+        ctx.save_for_backward(x_d, enc, w_packed)
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g):
+        x_d, enc, w_packed = ctx.saved_tensors
+        model = ctx.model
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError("InstantNGP (HIP): no gradient w.r.t. sample positions x_d")
+        g = g.contiguous().float()
+        M = x_d.shape[0]
+        net = model.net_struct
+        d_w = torch.empty_like(w_packed)
+        d_enc = torch.empty_like(enc)
+        wsb = int(lib().nerf_ngp_workspace_bytes(_addr(net), M))
+        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=x_d.device)
+        check(lib().nerf_ngp_bwd(_addr(net), ptr(w_packed), ptr(enc), enc.stride(0), ptr(x_d), M, ptr(g), ptr(d_enc),
+                                 ptr(d_w), 0, ptr(ws), wsb, stream()), "nerf_ngp_bwd")
+        d_table = None
+        if ctx.needs_input_grad[1]:
+            d_table = hash_encode_bwd(model.xyz_encoder.grid, x_d, d_enc, ctx.rows, model._aabb_host, model._eps)
+        return None, d_table, d_w, None
+
+
+class _Block(nn.Module):
+    def __init__(self, i, o):
+        super().__init__()
+        self.linear = nn.Linear(i, o)
+
+
+class InstantNGP(nn.Module):
+    """MetaNGP (models/inr/meta_ngp.py:15-255) on the HIP kernels; same constructor and parameter names."""
+
+    def __init__(self, *, occ_conf: Optional[Dict] = None, scene_box=None, hidden: int = 64, sigma_depth: int = 2,
+                 color_hidden: int = 64, geo_feat_dim: int = 15, color_depth: int = 3, use_sigmoid_rgb: bool = True,
+                 hash_enc_conf: Optional[Dict] = None, dir_encoding: str = "spherical", **kwargs) -> None:
+        super().__init__()
+        occ_conf = occ_conf or {}
+        if bool(occ_conf.get("use_occ", False)):
+            raise NotImplementedError("the occupancy renderer (nerfacc OccGridEstimator) is SURVEY §8f row 2 "
+                                      "and not built yet; use use_occ=False (stratified render_rays)")
+        aabb = scene_box.aabb if hasattr(scene_box, "aabb") else scene_box
+        aabb = torch.as_tensor(aabb, dtype=torch.float32).reshape(2, 3).cpu()
+        if not bool((aabb[0] < aabb[1]).all()):
+            raise ValueError(f"AABB invalid: min>=max ({aabb[0]} vs {aabb[1]})")
+        self.register_buffer("aabb_extent", aabb[1] - aabb[0])
+        self.register_buffer("enc_eps", torch.tensor(1e-6, dtype=torch.float32), persistent=False)
+        self._aabb_host = [float(v) for v in aabb.reshape(-1).tolist()]
+        self._eps = float(torch.tensor(1e-6, dtype=torch.float32))
+        self.scene_box = scene_box
+        self.use_occ = False
+        self.occ_ready = False
+        self.use_bg_nerf = False
+        self.dim_out = 4
+        self.geo_feat_dim = int(geo_feat_dim)
+        self.use_sigmoid_rgb = bool(use_sigmoid_rgb)
+        hc = hash_enc_conf or {}
+        self.xyz_encoder = HashGridEncoder(levels=hc.get("levels", 4), min_res=hc.get("min_res", 16),
+                                           max_res=hc.get("max_res", 4096),
+                                           log2_hashmap_size=hc.get("log2_hashmap_size", 19),
+                                           features_per_level=hc.get("features_per_level", 2),
+                                           interpolation=hc.get("interpolation", "Linear"))
+        in_xyz = self.xyz_encoder.out_dim
+        dir_encoding = dir_encoding.lower()
+        if dir_encoding == "spherical":
+            self.dir_encoder = SHEncoder(levels=4)
+            dir_dim, dir_mode = 16, 0
+        elif dir_encoding == "frequency":
+            from .encodings import FrequencyEncoder
+            self.dir_encoder = FrequencyEncoder(in_dim=3, pe_dim=4, include_input=True, use_pi=False)
+            dir_dim, dir_mode = 27, 1
+        else:
+            raise ValueError(f"Unsupported dir_encoding: {dir_encoding}")
+        self.sigma_depth = max(int(sigma_depth), 0)
+        self.color_depth = max(int(color_depth), 0)
+        trunk, last = [], in_xyz
+        for _ in range(self.sigma_depth):
+            trunk.append(_Block(last, hidden))
+            last = hidden
+        self.sigma_trunk = nn.ModuleList(trunk)
+        self.sigma_head = nn.Linear(last, 1)
+        with torch.no_grad():
+            self.sigma_head.bias.fill_(-1.0)
+        self.geo_head = nn.Linear(last, self.geo_feat_dim)
+        cm, last = [], self.geo_feat_dim + dir_dim
+        for _ in range(self.color_depth):
+            cm.append(_Block(last, color_hidden))
+            last = color_hidden
+        cm.append(nn.Linear(last, 3))
+        self.color_mlp = nn.ModuleList(cm)
+        net = NerfNgpNet()
+        net.in_dim, net.hidden, net.sigma_depth = in_xyz, int(hidden), self.sigma_depth
+        net.geo_feat_dim, net.color_hidden, net.color_depth = self.geo_feat_dim, int(color_hidden), self.color_depth
+        net.dir_encoding, net.sh_levels, net.use_sigmoid_rgb = dir_mode, 4, int(self.use_sigmoid_rgb)
+        self.net_struct = net
+        shapes = OrderedDict((n, tuple(p.shape)) for n, p in self.named_parameters() if not n.startswith("xyz_encoder."))
+        self.layout = NgpLayout(net, shapes, self.sigma_depth, self.color_depth)
+        self._subdict_cache = {}
+
+    # ---- MetaModule surface (models/metamodule/metamodule.py:20-69): the hash table is not a meta parameter
+    def meta_named_parameters(self, prefix: str = "", recurse: bool = True):
+        for n, p in self.named_parameters(prefix=prefix, recurse=recurse):
+            if not n[len(prefix):].lstrip(".").startswith("xyz_encoder."):
+                yield n, p
+
+    def meta_parameters(self, recurse: bool = True):
+        for _, p in self.meta_named_parameters(recurse=recurse):
+            yield p
+
+    get_subdict = VanillaNeRF.get_subdict
+
+    def get_param_groups(self):
+        """models/inr/meta_ngp.py:446-469."""
+        return {"encoding": {"params": list(self.xyz_encoder.parameters())},
+                "sigma": {"params": list(self.sigma_trunk.parameters()) + list(self.sigma_head.parameters())
+                          + list(self.geo_head.parameters())},
+                "color": {"params": list(self.color_mlp.parameters())}}
+
+    def tensors(self, params=None):
+        own = dict(self.named_parameters())
+        if params is None:
+            return [own[n] for n in self.layout.names]
+        return [params.get(n, own[n]) for n in self.layout.names]
+
+    def packed(self, params=None):
+        return self.layout.pack(self.tensors(params))
+
+    def load_reference_state(self, state: Dict[str, torch.Tensor]):
+        with torch.no_grad():
+            for n, p in self.named_parameters():
+                p.copy_(state[n].to(p.device, p.dtype))
+        return self
+
+    def forward(self, x_d: torch.Tensor, params=None) -> torch.Tensor:
+        assert x_d.shape[-1] == 6, f"Expected (...,6) [xyz,dir], got {x_d.shape}"
+        shp = x_d.shape[:-1]
+        out = _NgpFn.apply(x_d.reshape(-1, 6), self.xyz_encoder.hash_table, self.packed(params), self)
+        return out.view(*shp, 4)
+
+
+MetaNGP = InstantNGP

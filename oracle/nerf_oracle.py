@@ -298,7 +298,8 @@ def render_rays(p_coarse, rays, S, training=False, u_strat=None, bg="white",
     """nerfs/ray_rendering.py:290-345 (stratified) + canonical hierarchical extension.
 
     Returns (rgb, depth, weights, acc, extras) where extras holds the coarse outputs when
-    n_importance > 0.  Fine network = p_fine (or p_coarse when None)."""
+    n_importance > 0.  Fine network = p_fine (or p_coarse when None).  A network is a vanilla
+    parameter dict, or any callable expert x_d (M,6) -> (M,4) (e.g. the Instant-NGP oracle)."""
     o, d = rays[:, :3], rays[:, 3:6]
     N = rays.shape[0]
     t = stratified_t_vals(rays[:, 6], rays[:, 7], S, training, u_strat)
@@ -308,7 +309,7 @@ def render_rays(p_coarse, rays, S, training=False, u_strat=None, bg="white",
         pts = o.unsqueeze(1) + d.unsqueeze(1) * tv.unsqueeze(-1)
         dirs = d.unsqueeze(1).expand_as(pts)
         x_d = torch.cat([pts, dirs], -1).reshape(-1, 6)
-        rs = vanilla_forward(p, x_d).view(N, tv.shape[1], 4)
+        rs = (p(x_d) if callable(p) else vanilla_forward(p, x_d)).view(N, tv.shape[1], 4)
         return volume_render(rs, tv, bgc)
 
     out = one_pass(p_coarse, t)

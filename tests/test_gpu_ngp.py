@@ -1,0 +1,165 @@
+"""Instant-NGP expert on the HIP path vs the reference golden vectors
+(tests/golden/ngp.npz) and the CPU oracle (oracle/ngp_oracle.py).  Run on an MI355X: -m gpu.
+
+Tolerances: hash-grid encodings are bit-exact (same fp32 operations in the same order as the
+reference's torch backend); SH within 4e-6; network outputs within 1e-5 (north-star bar 1e-4);
+gradients within 1e-4 of their scale (the table gradient is accumulated with fp32 atomics, so its
+summation order differs from torch's index_put)."""
+from collections import OrderedDict
+
+import pytest
+import torch
+
+from golden_io import load
+from oracle import ngp_oracle as NO
+from oracle import nerf_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+HCFG = {"a": (4, 2, 12, 16, 4096, "Linear"), "b": (16, 2, 12, 16, 2048, "Smoothstep"),
+        "c": (8, 4, 10, 4, 300, "Nearest"), "d": (8, 1, 11, 16, 512, "Linear")}
+MCFG = {"m1": dict(hidden=64, sigma_depth=2, color_hidden=64, color_depth=2, dir_encoding="spherical",
+                   hash_enc_conf=dict(levels=8, features_per_level=2, log2_hashmap_size=12, min_res=16,
+                                      max_res=1024, interpolation="Linear")),
+        "m2": dict(hidden=32, sigma_depth=1, color_hidden=48, color_depth=3, dir_encoding="frequency",
+                   hash_enc_conf=dict(levels=16, features_per_level=2, log2_hashmap_size=11, min_res=16,
+                                      max_res=2048, interpolation="Linear"))}
+
+
+def _err(a, b):
+    return (a.detach().float().cpu() - b.detach().float().cpu()).abs().max().item() if a.numel() else 0.0
+
+
+@pytest.fixture(scope="module")
+def z():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return load("ngp")
+
+
+@pytest.fixture(scope="module")
+def N():
+    from nerf_amd import ngp
+    return ngp
+
+
+@pytest.mark.parametrize("lv", [1, 2, 3, 4, 5])
+def test_sh(z, N, lv):
+    enc = N.SHEncoder(levels=lv)
+    # torch's CPU norm and our sqrt differ by an ulp on some directions; degree-4 terms amplify it
+    assert _err(enc(z["sh_d"].to(DEV)), z[f"sh_{lv}"]) <= 4e-6
+
+
+@pytest.mark.parametrize("tag", list(HCFG))
+def test_hash_encode_golden(z, N, tag):
+    L, F, log2T, mn, mx, interp = HCFG[tag]
+    enc = N.HashGridEncoder(levels=L, features_per_level=F, log2_hashmap_size=log2T, min_res=mn, max_res=mx,
+                            interpolation=interp).to(DEV)
+    assert torch.equal(enc.level_resolutions.cpu(), z[f"hash_{tag}_res"])
+    with torch.no_grad():
+        enc.hash_table.copy_(z[f"hash_{tag}_table"].to(DEV))
+    y = enc(z["hash_x"].to(DEV))
+    assert torch.equal(y.detach().cpu(), z[f"hash_{tag}_out"]), f"max err {_err(y, z[f'hash_{tag}_out'])}"
+    (y * z[f"hash_{tag}_gup"].to(DEV)).sum().backward()
+    ref = z[f"hash_{tag}_gtable"]
+    assert _err(enc.hash_table.grad, ref) <= 1e-6 * max(1.0, ref.abs().max().item())
+
+
+def _ngp_from_golden(z, N, tag):
+    c = MCFG[tag]
+    net = N.InstantNGP(occ_conf={}, scene_box=z["ngp_aabb"], **c).to(DEV)
+    state = {k[len(tag) + 3:]: v for k, v in z.items() if k.startswith(f"{tag}_w/")}
+    assert set(state) == {n for n, _ in net.named_parameters()}
+    net.load_reference_state(state)
+    return net
+
+
+@pytest.mark.parametrize("tag", list(MCFG))
+def test_ngp_expert_golden(z, N, tag):
+    net = _ngp_from_golden(z, N, tag)
+    assert torch.equal(net.xyz_encoder.level_resolutions.cpu(), z[f"{tag}_res"])
+    x_d = z["ngp_x_d"].to(DEV)
+    out = net(x_d)
+    assert _err(out, z[f"{tag}_out"]) <= 1e-5
+    (out * z[f"{tag}_gup"].to(DEV)).sum().backward()
+    for n, p in net.named_parameters():
+        ref = z[f"{tag}_g/{n}"]
+        e = _err(p.grad, ref)
+        assert e <= 1e-4 * max(1.0, ref.abs().max().item()), f"{n}: {e}"
+
+
+def test_ngp_fast_weights(z, N):
+    net = _ngp_from_golden(z, N, "m1")
+    x_d = z["ngp_x_d"].to(DEV)
+    fast = OrderedDict((n, (p * 1.0).detach().requires_grad_(True)) for n, p in net.meta_named_parameters())
+    assert "xyz_encoder.hash_table" not in fast
+    out = net(x_d, params=fast)
+    assert torch.equal(out, net(x_d))
+    grads = torch.autograd.grad((out * z["m1_gup"].to(DEV)).sum(), list(fast.values()))
+    for (n, _), gr in zip(fast.items(), grads):
+        ref = z[f"m1_g/{n}"]
+        assert _err(gr, ref) <= 1e-4 * max(1.0, ref.abs().max().item()), n
+    groups = net.get_param_groups()
+    assert [id(p) for p in groups["encoding"]["params"]] == [id(net.xyz_encoder.hash_table)]
+
+
+@pytest.mark.parametrize("M", [0, 1, 63, 65, 1000])
+def test_ngp_ragged(z, N, M):
+    net = _ngp_from_golden(z, N, "m2")
+    g = torch.Generator().manual_seed(M)
+    x_d = torch.cat([torch.rand(M, 3, generator=g) * 3 - 1.5, torch.randn(M, 3, generator=g)], -1)
+    gup = torch.randn(M, 4, generator=g)
+    out = net(x_d.to(DEV))
+    (out * gup.to(DEV)).sum().backward()
+    w = OrderedDict((n, p.detach().cpu().clone().requires_grad_(True)) for n, p in net.named_parameters())
+    table = w.pop("xyz_encoder.hash_table")
+    res, _ = NO.hash_resolutions(16, 16, 2048)
+    ref = NO.ngp_forward(w, table, x_d, z["ngp_aabb"], res, 11, 2, sigma_depth=1, color_depth=3,
+                         dir_encoding="frequency")
+    assert _err(out, ref) <= 1e-5
+    if M == 0:
+        assert all(float(p.grad.abs().max()) == 0.0 for p in net.parameters())
+        return
+    grads = torch.autograd.grad((ref * gup).sum(), list(w.values()) + [table])
+    for (n, p), gr in zip(list(w.items()) + [("xyz_encoder.hash_table", table)], grads):
+        got = dict(net.named_parameters())[n].grad
+        assert _err(got, gr) <= 1e-4 * max(1.0, gr.abs().max().item()), n
+
+
+def test_ngp_production_config_render(N):
+    """The reference's production expert (nerf_runner.py:103-121 defaults: 16 levels, F=2, 2^20 table,
+    max_res 4096, 64-wide, sigma_depth 2, colour depth 2, SH dirs) inside render_rays: HIP vs oracle."""
+    from nerf_amd.ray_rendering import render_rays
+    torch.manual_seed(3)
+    aabb = torch.tensor([[-1.5, -1.5, -1.5], [1.5, 1.5, 1.5]])
+    c = dict(hidden=64, sigma_depth=2, color_hidden=64, color_depth=2, dir_encoding="spherical",
+             hash_enc_conf=dict(levels=16, features_per_level=2, log2_hashmap_size=20, min_res=16, max_res=4096))
+    net = N.InstantNGP(occ_conf={}, scene_box=aabb, **c)
+    with torch.no_grad():
+        net.xyz_encoder.hash_table.normal_(0.0, 0.3)
+    net = net.to(DEV)
+    net.eval()
+    n = 96
+    g = torch.Generator().manual_seed(5)
+    o = torch.tensor([0.0, -4.0, 0.5]).expand(n, 3)
+    d = torch.nn.functional.normalize(torch.randn(n, 3, generator=g) * 0.25 + torch.tensor([0.0, 1.0, -0.1]), dim=-1)
+    rays = torch.cat([o, d, torch.full((n, 1), 2.0), torch.full((n, 1), 6.0)], -1)
+    rgb, depth, w, acc = render_rays(net, rays.to(DEV), ray_samples=64)
+    w_cpu = OrderedDict((k, v.detach().cpu()) for k, v in net.named_parameters())
+    table = w_cpu.pop("xyz_encoder.hash_table")
+    res, _ = NO.hash_resolutions(16, 16, 4096)
+
+    def expert(x_d):
+        return NO.ngp_forward(w_cpu, table, x_d, aabb, res, 20, 2, sigma_depth=2, color_depth=2)
+
+    ref = O.render_rays(expert, rays, 64, training=False)
+    for a, b, what in ((rgb, ref[0], "rgb"), (depth, ref[1], "depth"), (w, ref[2], "weights"), (acc, ref[3], "acc")):
+        assert _err(a, b) <= 1e-4 * max(1.0, b.abs().max().item()), what
+
+
+def test_ngp_unsupported_config_raises(N):
+    with pytest.raises(ValueError):
+        N.InstantNGP(occ_conf={}, scene_box=torch.tensor([[0.0, 0, 0], [1, 1, 1]]), hidden=128)
+    with pytest.raises(NotImplementedError):
+        N.InstantNGP(occ_conf={"use_occ": True}, scene_box=torch.tensor([[0.0, 0, 0], [1, 1, 1]]))

@@ -12,7 +12,7 @@ renderer), ``jaxtyping`` (scene_box.py:3, a type annotation), ``viser.transforms
 MetaNeRF's (x,d,params)->dict forward is wrapped in a 6-line adapter to the container
 contract expert(x_d (M,6), params) -> (M,4) (SURVEY.md §0 defect 2).
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--only-ngp]
 """
 import os
 import sys
@@ -201,9 +201,89 @@ def main():
     after = {f"p/{n}": p.detach().numpy() for n, p in net.named_parameters() if n in keep}
     np.savez_compressed(os.path.join(OUT, "train_step.npz"), gt=gt.numpy(), loss=np.float32(loss.item()),
                         gnorm=np.float32(gnorm.item()), lr=np.float32(2e-3), **after)
+    gen_ngp()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 
 
+def gen_ngp():
+    """Instant-NGP expert fixtures: SHEncoder, HashGridEncoder (torch backend,
+    several level/feature/interpolation configs, incl. points outside [0,1]) and MetaNGP forward +
+    every parameter gradient (hash table included) for two network shapes."""
+    from models.encodings import SHEncoder, HashGridEncoder   # noqa: E402
+    from models.inr.meta_ngp import MetaNGP                    # noqa: E402
+    from nerfs.scene_box import SceneBox                       # noqa: E402
+    g = torch.Generator().manual_seed(4321)
+    arr = {}
+    d = torch.randn(256, 3, generator=g) * 2.0
+    arr["sh_d"] = d.numpy()
+    for lv in range(1, 6):
+        arr[f"sh_{lv}"] = SHEncoder(levels=lv, implementation="torch")(d).numpy()
+    hcfg = {"a": dict(levels=4, features_per_level=2, log2_hashmap_size=12, min_res=16, max_res=4096,
+                      interpolation="Linear"),
+            "b": dict(levels=16, features_per_level=2, log2_hashmap_size=12, min_res=16, max_res=2048,
+                      interpolation="Smoothstep"),
+            "c": dict(levels=8, features_per_level=4, log2_hashmap_size=10, min_res=4, max_res=300,
+                      interpolation="Nearest"),
+            "d": dict(levels=8, features_per_level=1, log2_hashmap_size=11, min_res=16, max_res=512,
+                      interpolation="Linear")}
+    x = torch.rand(256, 3, generator=g)
+    x[:8] = torch.rand(8, 3, generator=g) * 1.4 - 0.2   # a few points outside [0,1]: negative floors
+    arr["hash_x"] = x.numpy()
+    for tag, c in hcfg.items():
+        enc = HashGridEncoder(implementation="torch", **c)
+        with torch.no_grad():
+            enc.hash_table.copy_(torch.randn(enc.hash_table.shape, generator=g) * 0.5)
+        y = enc(x)
+        gup = torch.randn(y.shape, generator=g)
+        gt, = torch.autograd.grad((y * gup).sum(), [enc.hash_table])
+        arr[f"hash_{tag}_table"] = enc.hash_table.detach().numpy()
+        arr[f"hash_{tag}_res"] = enc.level_resolutions.numpy()
+        arr[f"hash_{tag}_out"] = y.detach().numpy()
+        arr[f"hash_{tag}_gup"] = gup.numpy()
+        arr[f"hash_{tag}_gtable"] = gt.numpy()
+    mcfg = {"m1": dict(hidden=64, sigma_depth=2, color_hidden=64, color_depth=2, dir_encoding="spherical",
+                       hash_enc_conf=dict(levels=8, features_per_level=2, log2_hashmap_size=12, min_res=16,
+                                          max_res=1024, interpolation="Linear")),
+            "m2": dict(hidden=32, sigma_depth=1, color_hidden=48, color_depth=3, dir_encoding="frequency",
+                       hash_enc_conf=dict(levels=16, features_per_level=2, log2_hashmap_size=11, min_res=16,
+                                          max_res=2048, interpolation="Linear"))}
+    aabb = torch.tensor([[-1.0, -2.0, -1.5], [2.0, 1.0, 1.5]])
+    M = 512
+    pts = torch.rand(M, 3, generator=g) * 3.4 + aabb[0] - 0.2      # some samples outside the box
+    dd = torch.randn(M, 3, generator=g)                              # non-unit: MetaNGP normalises
+    x_d = torch.cat([pts, dd], -1)
+    arr["ngp_aabb"] = aabb.numpy()
+    arr["ngp_x_d"] = x_d.numpy()
+    for tag, c in mcfg.items():
+        torch.manual_seed(7)
+        net = MetaNGP(occ_conf={}, scene_box=SceneBox(aabb=aabb.clone()), **c)
+        with torch.no_grad():
+            net.xyz_encoder.hash_table.copy_(torch.randn(net.xyz_encoder.hash_table.shape, generator=g) * 0.5)
+        out = net(x_d)
+        gup = torch.randn(M, 4, generator=g)
+        names = [n for n, _ in net.named_parameters()]
+        grads = torch.autograd.grad((out * gup).sum(), list(net.parameters()))
+        fast = OrderedDict((n, p * 1.0) for n, p in net.meta_named_parameters())
+        assert "xyz_encoder.hash_table" not in fast          # the hash table is not a fast weight
+        assert torch.equal(net(x_d, params=fast), out)
+        arr[f"{tag}_res"] = net.xyz_encoder.level_resolutions.numpy()
+        arr[f"{tag}_out"] = out.detach().numpy()
+        arr[f"{tag}_gup"] = gup.numpy()
+        for n, p in net.named_parameters():
+            arr[f"{tag}_w/{n}"] = p.detach().numpy()
+        for n, gr in zip(names, grads):
+            arr[f"{tag}_g/{n}"] = gr.numpy()
+    np.savez_compressed(os.path.join(OUT, "ngp.npz"), **arr)
+
+
 if __name__ == "__main__":
-    main()
+    if "--only-ngp" in sys.argv:
+        sys.dont_write_bytecode = True
+        _install_stubs()
+        sys.path.insert(0, REF)
+        torch.set_num_threads(8)
+        gen_ngp()
+    else:
+        main()
+
