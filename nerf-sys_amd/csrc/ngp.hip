@@ -287,6 +287,55 @@ __global__ void hash_bwd_kernel(HashArgs a, const float* __restrict__ x, int64_t
   }
 }
 
+// F = 2 backward, shaped for the memory-side atomic unit: float atomics execute at the memory side at one
+// rate of 64-B requests chip-wide (MI355X_MICROARCH.md § Global float atomics), so a wave-instruction whose
+// 64 lanes hit 64 scattered entries costs 16x one that hits 4 segments.  Four lanes cooperate on one
+// (sample, level): lane q adds feature f = q & 1 of the x-corner dx = q >> 1 for each of the four (y,z)
+// corners.  With the reference's x-prime of 1 the two x-corners hash to h and h ^ (ix ^ (ix+1)), the same
+// 64-B segment 7 times in 8, so each instruction carries ~16 requests instead of 64.
+__global__ void hash_bwd_f2_kernel(HashArgs a, const float* __restrict__ x, int64_t xs, int64_t M,
+                                   const float* __restrict__ g, int gs, float* __restrict__ dtab) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = (int)(gid & 3);
+  const int64_t pair = gid >> 2;
+  const int64_t m = pair / a.L;
+  const int l = (int)(pair - m * a.L);
+  if (m >= M) return;
+  float p[3];
+  load_x01(a, x, xs, m, p);
+  const float r = (float)a.res[l];
+  const uint32_t mask = (1u << a.log2T) - 1u;
+  float* tb = dtab + ((int64_t)l << a.log2T) * 2;
+  const int dx = q >> 1, f = q & 1;
+  const float gg = g[m * gs + l * 2 + f];
+  if (a.interp == 0) {
+    if (dx == 0) {
+      const int ix = (int)rintf(__fmul_rn(p[0], r)), iy = (int)rintf(__fmul_rn(p[1], r)),
+                iz = (int)rintf(__fmul_rn(p[2], r));
+      unsafeAtomicAdd(tb + (int64_t)ngp_hash(ix, iy, iz, mask) * 2 + f, gg);
+    }
+    return;
+  }
+  float w[3];
+  int i0[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float s = __fmul_rn(p[c], r);
+    const float fl = floorf(s);
+    w[c] = __fsub_rn(s, fl);
+    i0[c] = (int)fl;
+    if (a.interp == 2) w[c] = __fmul_rn(__fmul_rn(w[c], w[c]), __fsub_rn(3.0f, __fmul_rn(2.0f, w[c])));
+  }
+  const float u[3] = {__fsub_rn(1.0f, w[0]), __fsub_rn(1.0f, w[1]), __fsub_rn(1.0f, w[2])};
+  const float wx = dx ? w[0] : u[0];
+#pragma unroll
+  for (int yz = 0; yz < 4; ++yz) {
+    const int dy = yz >> 1, dz = yz & 1;
+    const float v = __fmul_rn(__fmul_rn(__fmul_rn(gg, dz ? w[2] : u[2]), dy ? w[1] : u[1]), wx);
+    unsafeAtomicAdd(tb + (int64_t)ngp_hash(i0[0] + dx, i0[1] + dy, i0[2] + dz, mask) * 2 + f, v);
+  }
+}
+
 // ---------------------------------------------------------------------------------------- direction encodings
 
 // SH components of degree `deg` of a unit direction into v[0..(deg+1)^2) (models/encodings.py:27-81; the
@@ -750,7 +799,9 @@ extern "C" int nerf_hash_encode_bwd(const NerfHashGrid* grid, const float* x, in
   const unsigned blocks = (unsigned)nerf_cdiv(n, 256);
   switch (a.F) {
     case 1: hash_bwd_kernel<1><<<blocks, 256, 0, st>>>(a, x, x_stride, M, d_out, d_stride, d_table); break;
-    case 2: hash_bwd_kernel<2><<<blocks, 256, 0, st>>>(a, x, x_stride, M, d_out, d_stride, d_table); break;
+    case 2:
+      hash_bwd_f2_kernel<<<(unsigned)nerf_cdiv(4 * n, 256), 256, 0, st>>>(a, x, x_stride, M, d_out, d_stride, d_table);
+      break;
     case 4: hash_bwd_kernel<4><<<blocks, 256, 0, st>>>(a, x, x_stride, M, d_out, d_stride, d_table); break;
     default: hash_bwd_kernel<8><<<blocks, 256, 0, st>>>(a, x, x_stride, M, d_out, d_stride, d_table); break;
   }

@@ -91,6 +91,42 @@ def sh_encode(d, levels=4):
     return out
 
 
+def ngp_fwd(net: NerfNgpNet, w_packed, enc, x_d, out=None):
+    """nerf_ngp_fwd: enc (M, >=in_dim), x_d (M,6) -> rgb_sigma (M,4)."""
+    M = x_d.shape[0]
+    if out is None:
+        out = torch.empty((M, 4), dtype=torch.float32, device=x_d.device)
+    check(lib().nerf_ngp_fwd(_addr(net), ptr(w_packed), ptr(enc), enc.stride(0), ptr(x_d), M, ptr(out), stream()),
+          "nerf_ngp_fwd")
+    return out
+
+
+_WS = {}
+
+
+def ngp_workspace(net: NerfNgpNet, M, device):
+    need_b = max(int(lib().nerf_ngp_workspace_bytes(_addr(net), M)), 16)
+    key = str(device)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < need_b:
+        ws = torch.empty(need_b, dtype=torch.uint8, device=device)
+        _WS[key] = ws
+    return ws
+
+
+def ngp_bwd(net: NerfNgpNet, w_packed, enc, x_d, d_rgb_sigma, d_enc=None, d_w=None, accumulate=False):
+    """nerf_ngp_bwd -> (d_enc (M, enc pitch), d_w (packed))."""
+    M = x_d.shape[0]
+    if d_enc is None:
+        d_enc = torch.empty_like(enc)
+    if d_w is None:
+        d_w = torch.empty_like(w_packed)
+    ws = ngp_workspace(net, M, x_d.device)
+    check(lib().nerf_ngp_bwd(_addr(net), ptr(w_packed), ptr(enc), enc.stride(0), ptr(x_d), M, ptr(d_rgb_sigma),
+                             ptr(d_enc), ptr(d_w), int(accumulate), ptr(ws), ws.numel(), stream()), "nerf_ngp_bwd")
+    return d_enc, d_w
+
+
 # ------------------------------------------------------------------------------------------ encoders
 
 def level_resolutions(levels, min_res, max_res):
@@ -228,6 +264,9 @@ class NgpLayout:
             idx.append((off + torch.arange(r0, r0 + r).view(-1, 1) * cols + torch.arange(c).view(1, -1)).reshape(-1))
         self.index = torch.cat(idx)
         self._dev = {}
+        self.tensors_table = t
+        # Adam groups inside the packed MLP: 'sigma' = trunk + heads, 'color' = colour MLP (meta_ngp.py:446-469)
+        self.color_start = t[2 * (sigma_depth + 1)][0]
 
     def pack(self, tensors):
         flat = torch.cat([x.reshape(-1).to(torch.float32) for x in tensors])
@@ -243,11 +282,7 @@ class _NgpFn(torch.autograd.Function):
         x_d = x_d.contiguous().float()
         M = x_d.shape[0]
         enc = hash_encode(model.xyz_encoder.grid, table.detach(), x_d, model._aabb_host, model._eps)
-        out = torch.empty((M, 4), dtype=torch.float32, device=x_d.device)
-        net = model.net_struct
-        if M:
-            check(lib().nerf_ngp_fwd(_addr(net), ptr(w_packed), ptr(enc), enc.stride(0), ptr(x_d), M, ptr(out),
-                                     stream()), "nerf_ngp_fwd")
+        out = ngp_fwd(model.net_struct, w_packed, enc, x_d) if M else x_d.new_empty((0, 4))
         ctx.model = model
         ctx.rows = table.shape[0]
         ctx.save_for_backward(x_d, enc, w_packed)
@@ -261,14 +296,9 @@ class _NgpFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             raise NotImplementedError("InstantNGP (HIP): no gradient w.r.t. sample positions x_d")
         g = g.contiguous().float()
-        M = x_d.shape[0]
-        net = model.net_struct
-        d_w = torch.empty_like(w_packed)
-        d_enc = torch.empty_like(enc)
-        wsb = int(lib().nerf_ngp_workspace_bytes(_addr(net), M))
-        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=x_d.device)
-        check(lib().nerf_ngp_bwd(_addr(net), ptr(w_packed), ptr(enc), enc.stride(0), ptr(x_d), M, ptr(g), ptr(d_enc),
-                                 ptr(d_w), 0, ptr(ws), wsb, stream()), "nerf_ngp_bwd")
+        if x_d.shape[0] == 0:
+            return None, torch.zeros_like(model.xyz_encoder.hash_table), torch.zeros_like(w_packed), None
+        d_enc, d_w = ngp_bwd(model.net_struct, w_packed, enc, x_d, g)
         d_table = None
         if ctx.needs_input_grad[1]:
             d_table = hash_encode_bwd(model.xyz_encoder.grid, x_d, d_enc, ctx.rows, model._aabb_host, model._eps)

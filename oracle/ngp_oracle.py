@@ -82,7 +82,7 @@ def freq_encode(x, n_freq, include_input=True):
     """FrequencyEncoder.torch_forward (models/encodings.py:437-444)."""
     bands = 2.0 ** torch.arange(n_freq, dtype=torch.float32)
     xe = x[..., None] * bands.to(x.dtype)
-    pe = torch.cat([torch.cos(xe), torch.sin(xe)], -1).reshape(*x.shape[:-1], -1)
+    pe = torch.cat([torch.cos(xe), torch.sin(xe)], -1).reshape(*x.shape[:-1], x.shape[-1] * 2 * n_freq)
     return torch.cat([x, pe], -1) if include_input else pe
 
 
