@@ -228,6 +228,44 @@ int nerf_ngp_bwd(const NerfNgpNet* net, const float* w, const float* enc, int en
                  int64_t M, const float* d_rgb_sigma, float* d_enc, float* d_w, int accumulate, void* ws,
                  int64_t ws_bytes, hipStream_t stream);
 
+/* ------------------------------------------------------------------ MoE container */
+
+/* MetaContainer._routing (models/inr/meta_container.py:97-134): distances of x[:, :3] (rows of pitch
+ * x_stride) to K <= 32 centroids (HOST array K x 3) on (y,z) if cluster_2d else (x,y,z).  boundary_margin
+ * > 1: soft inverse-distance weights of the experts within margin x the nearest distance; else one-hot
+ * argmin.  weights (M, K) fp32. */
+int nerf_moe_route(const float* x, int64_t x_stride, int64_t M, const float* centroids, int K, int cluster_2d,
+                   float boundary_margin, float* weights, hipStream_t stream);
+
+/* Order-preserving per-expert dispatch (the `(w[:,k] > 0).nonzero()` of meta_container.py:288-296):
+ * idx (up to M*K int32) receives the rows with weights[m][k] > eps, expert-major and ascending within an
+ * expert; offsets (K+1 int32, device) the exclusive expert offsets.  ws: nerf_moe_dispatch_workspace_bytes. */
+int64_t nerf_moe_dispatch_workspace_bytes(int64_t M, int K);
+int nerf_moe_dispatch(const float* weights, int64_t M, int K, float eps, int32_t* offsets, int32_t* idx, void* ws,
+                      int64_t ws_bytes, hipStream_t stream);
+
+/* dst[i][c] = src[idx[i]][c], c < cols (the expert's x.index_select rows). */
+int nerf_gather_rows(const float* src, int64_t src_stride, const int32_t* idx, int64_t n, int cols, float* dst,
+                     int64_t dst_stride, hipStream_t stream);
+
+/* The mix of expert k (meta_container.py:304-318): out[idx[i]][c] += y[i][c] * weights[idx[i]][k] for the
+ * n rows of the expert (rows unique within a call; call k = 0..K-1 in order for the reference's sum order;
+ * one-hot weights reproduce index_copy_).  Backward: d_y[i][c] = d_out[idx[i]][c] * weights[idx[i]][k]. */
+int nerf_moe_combine(const float* y, int64_t n, int C, const int32_t* idx, const float* weights, int K, int k,
+                     float* out, hipStream_t stream);
+int nerf_moe_combine_bwd(const float* d_out, int64_t n, int C, const int32_t* idx, const float* weights, int K,
+                         int k, float* d_y, hipStream_t stream);
+
+/* MetaContainer.background_color (meta_container.py:334-363, bg_encoding "spherical"): F.normalize(d),
+ * SHEncoder(levels=4), Linear(16,H)-ReLU-Linear(H,3)-Sigmoid, H <= 64.  w packed [W1 (H,16) | b1 (H) |
+ * W2 (3,H) | b2 (3)] (PyTorch layouts).  Backward: d_w (20H+3 floats, overwritten) from d_out (N,3);
+ * per-workgroup slabs + deterministic reduce. */
+int nerf_bg_mlp_fwd(const float* d, int64_t d_stride, int64_t N, const float* w, int H, float* out,
+                    hipStream_t stream);
+int64_t nerf_bg_mlp_workspace_bytes(int64_t N, int H);
+int nerf_bg_mlp_bwd(const float* d, int64_t d_stride, int64_t N, const float* w, int H, const float* d_out,
+                    float* d_w, void* ws, int64_t ws_bytes, hipStream_t stream);
+
 /* Library build identification (string, static). */
 const char* nerf_version(void);
 

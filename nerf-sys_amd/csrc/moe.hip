@@ -1,0 +1,363 @@
+// The MoE container of the reference on gfx950: point routing to K experts,
+// order-preserving per-expert dispatch lists, the weighted mix of expert outputs and the background MLP.
+//
+// Restates (psklavos1/NeRF-Sys adaptive_nerf/):
+//   MetaContainer._routing            models/inr/meta_container.py:97-134
+//   MetaContainer.forward (mix)       models/inr/meta_container.py:266-330  (index_add_ / index_copy_)
+//   MetaContainer.background_color    models/inr/meta_container.py:334-363  (SH -> Linear-ReLU-Linear-Sigmoid)
+//
+// Data layout: routing weights W [M][K] fp32 (one-hot for hard routing), dispatch lists expert-major
+// (rows of expert 0 in ascending order, then expert 1, ...; offsets[K+1]), so expert k evaluates the
+// contiguous gather X[idx[off_k .. off_{k+1})] and the mix adds w * y back in expert order — the
+// reference's summation order, bit for bit.  All kernels are HBM-bound row passes.
+#include "common.hpp"
+
+// the mix must round like the reference's index_add_(y * w): no fma contraction in this file
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int MOE_MAX_K = 32;
+
+struct Cent {
+  float c[MOE_MAX_K][3];
+};
+
+__global__ void route_kernel(const float* __restrict__ x, int64_t xs, int64_t M, Cent cen, int K, int c2d, float bm,
+                             float* __restrict__ W) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  const float px = x[m * xs], py = x[m * xs + 1], pz = x[m * xs + 2];
+  float dist[MOE_MAX_K];
+  float mind = INFINITY;
+  int arg = 0;
+  for (int k = 0; k < K; ++k) {
+    const float dy = py - cen.c[k][1], dz = pz - cen.c[k][2];
+    float s = dy * dy + dz * dz;
+    if (!c2d) {
+      const float dx = px - cen.c[k][0];
+      s = dx * dx + dy * dy + dz * dz;
+    }
+    const float dd = sqrtf(s);
+    dist[k] = dd;
+    if (dd < mind) { mind = dd; arg = k; }  // first minimum, as torch.argmin
+  }
+  float* w = W + m * K;
+  if (bm > 1.0f) {
+    float md = INFINITY;
+    for (int k = 0; k < K; ++k) { dist[k] = fmaxf(dist[k], 1e-6f); md = fminf(md, dist[k]); }
+    const float lim = bm * md;
+    float inv[MOE_MAX_K];
+    float den = 0.f;
+    for (int k = 0; k < K; ++k) {
+      inv[k] = dist[k] <= lim ? 1.0f / dist[k] : 0.f;
+      den += inv[k];
+    }
+    den = fmaxf(den, 1e-6f);
+    for (int k = 0; k < K; ++k) w[k] = inv[k] / den;
+  } else {
+    for (int k = 0; k < K; ++k) w[k] = k == arg ? 1.0f : 0.f;
+  }
+}
+
+// per-block counts of routed rows per expert
+__global__ void dispatch_count_kernel(const float* __restrict__ W, int64_t M, int K, float eps,
+                                      int32_t* __restrict__ bcnt) {
+  __shared__ int cnt[MOE_MAX_K];
+  if (threadIdx.x < MOE_MAX_K) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int k = 0; k < K; ++k) {
+    const bool f = m < M && W[m * K + k] > eps;
+    const uint64_t b = __ballot(f);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&cnt[k], (int)__popcll(b));
+  }
+  __syncthreads();
+  if (threadIdx.x < K) bcnt[(int64_t)blockIdx.x * K + threadIdx.x] = cnt[threadIdx.x];
+}
+
+// one thread per expert: exclusive scan over blocks (expert-major), totals -> offsets
+__global__ void dispatch_scan_kernel(int32_t* __restrict__ bcnt, int64_t nblk, int K, int32_t* __restrict__ offsets) {
+  __shared__ int tot[MOE_MAX_K];
+  const int k = threadIdx.x;
+  if (k < K) {
+    int s = 0;
+    for (int64_t b = 0; b < nblk; ++b) {
+      const int c = bcnt[b * K + k];
+      bcnt[b * K + k] = s;
+      s += c;
+    }
+    tot[k] = s;
+  }
+  __syncthreads();
+  if (k == 0) {
+    int o = 0;
+    offsets[0] = 0;
+    for (int j = 0; j < K; ++j) { o += tot[j]; offsets[j + 1] = o; }
+  }
+  __syncthreads();
+  if (k < K) {
+    const int base = offsets[k];
+    for (int64_t b = 0; b < nblk; ++b) bcnt[b * K + k] += base;
+  }
+}
+
+__global__ void dispatch_write_kernel(const float* __restrict__ W, int64_t M, int K, float eps,
+                                      const int32_t* __restrict__ bbase, int32_t* __restrict__ idx) {
+  __shared__ int wcnt[MOE_MAX_K][4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int k = 0; k < K; ++k) {
+    const bool f = m < M && W[m * K + k] > eps;
+    const uint64_t b = __ballot(f);
+    if (lane == 0) wcnt[k][wave] = (int)__popcll(b);
+  }
+  __syncthreads();
+  for (int k = 0; k < K; ++k) {
+    const bool f = m < M && W[m * K + k] > eps;
+    const uint64_t b = __ballot(f);
+    if (f) {
+      int pos = bbase[(int64_t)blockIdx.x * K + k];
+      for (int w = 0; w < wave; ++w) pos += wcnt[k][w];
+      pos += (int)__popcll(b & ((1ull << lane) - 1ull));
+      idx[pos] = (int32_t)m;
+    }
+  }
+}
+
+__global__ void gather_rows_kernel(const float* __restrict__ src, int64_t ss, const int32_t* __restrict__ idx, int64_t n,
+                                   int cols, float* __restrict__ dst, int64_t ds) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * cols) return;
+  const int64_t i = t / cols;
+  const int c = (int)(t - i * cols);
+  dst[i * ds + c] = src[(int64_t)idx[i] * ss + c];
+}
+
+__global__ void combine_kernel(const float* __restrict__ y, int64_t n, int C, const int32_t* __restrict__ idx,
+                               const float* __restrict__ W, int K, int k, float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * C) return;
+  const int64_t i = t / C;
+  const int c = (int)(t - i * C);
+  const int64_t m = idx[i];
+  out[m * C + c] = out[m * C + c] + y[i * C + c] * W[m * K + k];
+}
+
+__global__ void combine_bwd_kernel(const float* __restrict__ dout, int64_t n, int C, const int32_t* __restrict__ idx,
+                                   const float* __restrict__ W, int K, int k, float* __restrict__ dy) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * C) return;
+  const int64_t i = t / C;
+  const int c = (int)(t - i * C);
+  const int64_t m = idx[i];
+  dy[i * C + c] = dout[m * C + c] * W[m * K + k];
+}
+
+// ------------------------------------------------------------------ background MLP
+
+constexpr int BG_MAXH = 64;
+
+__device__ __forceinline__ void bg_enc(const float* __restrict__ d, int64_t ds, int64_t r, float e[16]) {
+  float x = d[r * ds], y = d[r * ds + 1], z = d[r * ds + 2];
+  // F.normalize (eps 1e-12) then SHEncoder.forward's own normalisation (clamp 1e-9)
+  for (int pass = 0; pass < 2; ++pass) {
+    const float n = fmaxf(sqrtf(x * x + y * y + z * z), pass == 0 ? 1e-12f : 1e-9f);
+    x = x / n; y = y / n; z = z / n;
+  }
+  const float xx = x * x, yy = y * y, zz = z * z;
+  e[0] = 0.28209479177387814f;
+  e[1] = 0.4886025119029199f * y;
+  e[2] = 0.4886025119029199f * z;
+  e[3] = 0.4886025119029199f * x;
+  e[4] = 1.0925484305920792f * x * y;
+  e[5] = 1.0925484305920792f * y * z;
+  e[6] = 0.9461746957575601f * zz - 0.31539156525251999f;
+  e[7] = 1.0925484305920792f * x * z;
+  e[8] = 0.5462742152960396f * (xx - yy);
+  e[9] = 0.5900435899266435f * y * (3.0f * xx - yy);
+  e[10] = 2.890611442640554f * x * y * z;
+  e[11] = 0.4570457994644658f * y * (5.0f * zz - 1.0f);
+  e[12] = 0.3731763325901154f * z * (5.0f * zz - 3.0f);
+  e[13] = 0.4570457994644658f * x * (5.0f * zz - 1.0f);
+  e[14] = 1.445305721320277f * z * (xx - yy);
+  e[15] = 0.5900435899266435f * x * (xx - 3.0f * yy);
+}
+
+// packed weights: W1 [H][16] | b1 [H] | W2 [3][H] | b2 [3]
+__device__ __forceinline__ void bg_forward_row(const float* sw, int H, const float e[16], float h[BG_MAXH], float o[3]) {
+  const float* W1 = sw;
+  const float* b1 = sw + 16 * H;
+  const float* W2 = b1 + H;
+  const float* b2 = W2 + 3 * H;
+  for (int j = 0; j < H; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += W1[j * 16 + i] * e[i];
+    h[j] = fmaxf(s + b1[j], 0.f);
+  }
+  for (int c = 0; c < 3; ++c) {
+    float s = 0.f;
+    for (int j = 0; j < H; ++j) s += W2[c * H + j] * h[j];
+    o[c] = s + b2[c];
+  }
+}
+
+__global__ __launch_bounds__(256) void bg_fwd_kernel(const float* __restrict__ d, int64_t ds, int64_t N,
+                                                     const float* __restrict__ w, int H, float* __restrict__ out) {
+  __shared__ float sw[16 * BG_MAXH + BG_MAXH + 3 * BG_MAXH + 3];
+  const int P = 20 * H + 3;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) sw[i] = w[i];
+  __syncthreads();
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= N) return;
+  float e[16], h[BG_MAXH], o[3];
+  bg_enc(d, ds, r, e);
+  bg_forward_row(sw, H, e, h, o);
+  for (int c = 0; c < 3; ++c) out[r * 3 + c] = 1.0f / (1.0f + expf(-o[c]));
+}
+
+// per-block weight-gradient slab (deterministic: fixed wave / lane reduction order)
+__global__ __launch_bounds__(256) void bg_bwd_kernel(const float* __restrict__ d, int64_t ds, int64_t N,
+                                                     const float* __restrict__ w, int H,
+                                                     const float* __restrict__ gout, float* __restrict__ slab) {
+  __shared__ float sw[16 * BG_MAXH + BG_MAXH + 3 * BG_MAXH + 3];
+  __shared__ float red[4][16 * BG_MAXH + BG_MAXH + 3 * BG_MAXH + 3];
+  const int P = 20 * H + 3;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) sw[i] = w[i];
+  __syncthreads();
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float e[16], h[BG_MAXH], o[3], dz[3] = {0.f, 0.f, 0.f}, dh[BG_MAXH];
+  for (int i = 0; i < 16; ++i) e[i] = 0.f;
+  for (int j = 0; j < H; ++j) { h[j] = 0.f; dh[j] = 0.f; }
+  if (r < N) {
+    bg_enc(d, ds, r, e);
+    bg_forward_row(sw, H, e, h, o);
+    for (int c = 0; c < 3; ++c) {
+      const float s = 1.0f / (1.0f + expf(-o[c]));
+      dz[c] = gout[r * 3 + c] * (s * (1.0f - s));
+    }
+    const float* W2 = sw + 17 * H;
+    for (int j = 0; j < H; ++j) {
+      const float g = W2[j] * dz[0] + W2[H + j] * dz[1] + W2[2 * H + j] * dz[2];
+      dh[j] = h[j] > 0.f ? g : 0.f;
+    }
+  }
+  // contributions, reduced over the wave then over the 4 waves
+  for (int p = 0; p < P; ++p) {
+    float v;
+    if (p < 16 * H) v = dh[p >> 4] * e[p & 15];
+    else if (p < 17 * H) v = dh[p - 16 * H];
+    else if (p < 20 * H) { const int q = p - 17 * H; v = dz[q / H] * h[q % H]; }
+    else v = dz[p - 20 * H];
+    v = wave_sum(v);
+    if (lane == 0) red[wave][p] = v;
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < P; p += blockDim.x)
+    slab[(int64_t)blockIdx.x * P + p] = (red[0][p] + red[1][p]) + (red[2][p] + red[3][p]);
+}
+
+__global__ void bg_reduce_kernel(const float* __restrict__ slab, int nblk, int P, float* __restrict__ dw) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += slab[(int64_t)b * P + p];
+  dw[p] = s;
+}
+
+}  // namespace
+
+extern "C" int nerf_moe_route(const float* x, int64_t x_stride, int64_t M, const float* centroids, int K,
+                              int cluster_2d, float boundary_margin, float* weights, hipStream_t st) {
+  if (M < 0 || K < 1 || K > MOE_MAX_K || x_stride < 3 || !centroids) return NERF_E_ARG;
+  if (M == 0) return NERF_OK;
+  if (!x || !weights) return NERF_E_ARG;
+  Cent c{};
+  for (int k = 0; k < K; ++k)
+    for (int j = 0; j < 3; ++j) c.c[k][j] = centroids[3 * k + j];
+  route_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(x, x_stride, M, c, K, cluster_2d, boundary_margin,
+                                                            weights);
+  return nerf_launch_status();
+}
+
+extern "C" int64_t nerf_moe_dispatch_workspace_bytes(int64_t M, int K) {
+  if (M < 0 || K < 1 || K > MOE_MAX_K) return NERF_E_ARG;
+  return nerf_cdiv(M < 1 ? 1 : M, 256) * K * 4 + 256;
+}
+
+extern "C" int nerf_moe_dispatch(const float* weights, int64_t M, int K, float eps, int32_t* offsets, int32_t* idx,
+                                 void* ws, int64_t ws_bytes, hipStream_t st) {
+  if (M < 0 || K < 1 || K > MOE_MAX_K || !offsets) return NERF_E_ARG;
+  if (M == 0) {
+    (void)hipMemsetAsync(offsets, 0, (K + 1) * sizeof(int32_t), st);
+    return nerf_launch_status();
+  }
+  if (!weights || !idx || !ws) return NERF_E_ARG;
+  const int64_t nblk = nerf_cdiv(M, 256);
+  if (ws_bytes < nblk * K * 4) return NERF_E_WORKSPACE;
+  int32_t* bcnt = reinterpret_cast<int32_t*>(ws);
+  dispatch_count_kernel<<<(unsigned)nblk, 256, 0, st>>>(weights, M, K, eps, bcnt);
+  dispatch_scan_kernel<<<1, 64, 0, st>>>(bcnt, nblk, K, offsets);
+  dispatch_write_kernel<<<(unsigned)nblk, 256, 0, st>>>(weights, M, K, eps, bcnt, idx);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_gather_rows(const float* src, int64_t src_stride, const int32_t* idx, int64_t n, int cols,
+                                float* dst, int64_t dst_stride, hipStream_t st) {
+  if (n < 0 || cols < 1 || src_stride < cols || dst_stride < cols) return NERF_E_ARG;
+  if (n == 0) return NERF_OK;
+  if (!src || !idx || !dst) return NERF_E_ARG;
+  gather_rows_kernel<<<(unsigned)nerf_cdiv(n * cols, 256), 256, 0, st>>>(src, src_stride, idx, n, cols, dst, dst_stride);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_moe_combine(const float* y, int64_t n, int C, const int32_t* idx, const float* weights, int K,
+                                int k, float* out, hipStream_t st) {
+  if (n < 0 || C < 1 || K < 1 || k < 0 || k >= K) return NERF_E_ARG;
+  if (n == 0) return NERF_OK;
+  if (!y || !idx || !weights || !out) return NERF_E_ARG;
+  combine_kernel<<<(unsigned)nerf_cdiv(n * C, 256), 256, 0, st>>>(y, n, C, idx, weights, K, k, out);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_moe_combine_bwd(const float* d_out, int64_t n, int C, const int32_t* idx, const float* weights,
+                                    int K, int k, float* d_y, hipStream_t st) {
+  if (n < 0 || C < 1 || K < 1 || k < 0 || k >= K) return NERF_E_ARG;
+  if (n == 0) return NERF_OK;
+  if (!d_out || !idx || !weights || !d_y) return NERF_E_ARG;
+  combine_bwd_kernel<<<(unsigned)nerf_cdiv(n * C, 256), 256, 0, st>>>(d_out, n, C, idx, weights, K, k, d_y);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_bg_mlp_fwd(const float* d, int64_t d_stride, int64_t N, const float* w, int H, float* out,
+                               hipStream_t st) {
+  if (N < 0 || H < 1 || H > BG_MAXH || d_stride < 3) return NERF_E_ARG;
+  if (N == 0) return NERF_OK;
+  if (!d || !w || !out) return NERF_E_ARG;
+  bg_fwd_kernel<<<(unsigned)nerf_cdiv(N, 256), 256, 0, st>>>(d, d_stride, N, w, H, out);
+  return nerf_launch_status();
+}
+
+extern "C" int64_t nerf_bg_mlp_workspace_bytes(int64_t N, int H) {
+  if (N < 0 || H < 1 || H > BG_MAXH) return NERF_E_ARG;
+  return nerf_cdiv(N < 1 ? 1 : N, 256) * (20 * H + 3) * 4 + 256;
+}
+
+extern "C" int nerf_bg_mlp_bwd(const float* d, int64_t d_stride, int64_t N, const float* w, int H,
+                               const float* d_out, float* d_w, void* ws, int64_t ws_bytes, hipStream_t st) {
+  if (N < 0 || H < 1 || H > BG_MAXH || d_stride < 3 || !d_w) return NERF_E_ARG;
+  const int P = 20 * H + 3;
+  if (N == 0) {
+    (void)hipMemsetAsync(d_w, 0, P * sizeof(float), st);
+    return nerf_launch_status();
+  }
+  if (!d || !w || !d_out || !ws) return NERF_E_ARG;
+  const int64_t nblk = nerf_cdiv(N, 256);
+  if (ws_bytes < nblk * P * 4) return NERF_E_WORKSPACE;
+  float* slab = reinterpret_cast<float*>(ws);
+  bg_bwd_kernel<<<(unsigned)nblk, 256, 0, st>>>(d, d_stride, N, w, H, d_out, slab);
+  bg_reduce_kernel<<<(unsigned)nerf_cdiv(P, 256), 256, 0, st>>>(slab, (int)nblk, P, d_w);
+  return nerf_launch_status();
+}

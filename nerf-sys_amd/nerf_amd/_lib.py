@@ -56,6 +56,15 @@ def lib():
             "nerf_ngp_workspace_bytes": [P, I64],
             "nerf_ngp_fwd": [P, P, P, I, P, I64, P, P],
             "nerf_ngp_bwd": [P, P, P, I, P, I64, P, P, P, I, P, I64, P],
+            "nerf_moe_route": [P, I64, I64, P, I, I, F, P, P],
+            "nerf_moe_dispatch_workspace_bytes": [I64, I],
+            "nerf_moe_dispatch": [P, I64, I, F, P, P, P, I64, P],
+            "nerf_gather_rows": [P, I64, P, I64, I, P, I64, P],
+            "nerf_moe_combine": [P, I64, I, P, P, I, I, P, P],
+            "nerf_moe_combine_bwd": [P, I64, I, P, P, I, I, P, P],
+            "nerf_bg_mlp_fwd": [P, I64, I64, P, I, P, P],
+            "nerf_bg_mlp_workspace_bytes": [I64, I],
+            "nerf_bg_mlp_bwd": [P, I64, I64, P, I, P, P, P, I64, P],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -67,6 +76,8 @@ def lib():
         L.nerf_version.restype = ctypes.c_char_p
         L.nerf_ngp_layout.restype = c_int64
         L.nerf_ngp_workspace_bytes.restype = c_int64
+        L.nerf_moe_dispatch_workspace_bytes.restype = c_int64
+        L.nerf_bg_mlp_workspace_bytes.restype = c_int64
         _lib = L
     return _lib
 
@@ -77,7 +88,9 @@ EXPORTS = ("nerf_rays_gen", "nerf_pick_pixels", "nerf_clamp_near_far", "nerf_ray
            "nerf_mlp_workspace_bytes_bf16", "nerf_mlp_fwd_bf16", "nerf_mlp_bwd_bf16",
            "nerf_composite_fwd", "nerf_composite_bwd", "nerf_grad_sqnorm", "nerf_adam", "nerf_version",
            "nerf_hash_encode", "nerf_hash_encode_bwd", "nerf_sh_encode", "nerf_ngp_layout",
-           "nerf_ngp_workspace_bytes", "nerf_ngp_fwd", "nerf_ngp_bwd")
+           "nerf_ngp_workspace_bytes", "nerf_ngp_fwd", "nerf_ngp_bwd", "nerf_moe_route",
+           "nerf_moe_dispatch_workspace_bytes", "nerf_moe_dispatch", "nerf_gather_rows", "nerf_moe_combine",
+           "nerf_moe_combine_bwd", "nerf_bg_mlp_fwd", "nerf_bg_mlp_workspace_bytes", "nerf_bg_mlp_bwd")
 
 
 def check(status: int, what: str) -> None:

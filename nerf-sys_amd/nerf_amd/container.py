@@ -1,0 +1,271 @@
+"""The reference's Mixture-of-Experts container on the HIP kernels.
+
+Mirrors ``MetaContainer`` (models/inr/meta_container.py:21-503): the same constructor, parameter names
+(``submodules.{k}.*``, ``bg_mlp.0.*``, ``bg_mlp.2.*``), ``forward(x, params=None, active_module=None)``
+with soft (boundary_margin > 1) or hard routing, ``background_color(d)``, ``get_param_groups()`` and the
+fast-weights surface.  Compute per call:
+
+  nerf_moe_route (weights (M,K)) -> nerf_moe_dispatch (expert-major row lists; ONE host read of the K+1
+  offsets, as the reference's .nonzero() syncs) -> per expert: nerf_gather_rows -> expert forward (HIP
+  expert kernels) -> nerf_moe_combine in expert order (the reference's index_add_ summation order);
+  backward: nerf_moe_combine_bwd per expert (routing is no-grad in the reference too).
+  background_color: nerf_bg_mlp_fwd / nerf_bg_mlp_bwd (SH + 2-layer MLP fused, one thread per ray).
+
+Not mirrored: the occupancy-grid methods (premark / update / occ_ready) and the
+``density`` / ``color`` split queries used only by the occupancy renderer; ``bg_encoding="fourier"``
+fails in the reference's constructor (FrequencyEncoder without in_dim) and raises here.
+"""
+from __future__ import annotations
+
+import ctypes
+import re
+import warnings
+from collections import OrderedDict
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+from torch.autograd.function import once_differentiable
+
+from ._lib import check, lib, ptr, stream
+from .ngp import InstantNGP, SHEncoder
+from .vanilla import VanillaNeRF
+
+
+def build_expert(nerf_variant: str, **nerf_kwargs) -> nn.Module:
+    """meta_container.py:14-18."""
+    if nerf_variant == "instant":
+        return InstantNGP(**nerf_kwargs)
+    return VanillaNeRF()
+
+
+# ------------------------------------------------------------------ kernel wrappers
+
+def moe_route(x, centroids_host, boundary_margin, cluster_2d):
+    M, K = x.shape[0], len(centroids_host) // 3
+    W = torch.empty((M, K), dtype=torch.float32, device=x.device)
+    c = (ctypes.c_float * len(centroids_host))(*centroids_host)
+    check(lib().nerf_moe_route(ptr(x), x.stride(0), M, c, K, int(cluster_2d), float(boundary_margin), ptr(W),
+                               stream()), "nerf_moe_route")
+    return W
+
+
+def moe_dispatch(W, eps=0.0):
+    """-> (offsets (K+1) host list, idx (device int32, expert-major))."""
+    M, K = W.shape
+    offs = torch.empty(K + 1, dtype=torch.int32, device=W.device)
+    idx = torch.empty(max(M * K, 1), dtype=torch.int32, device=W.device)
+    wsb = int(lib().nerf_moe_dispatch_workspace_bytes(M, K))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=W.device)
+    check(lib().nerf_moe_dispatch(ptr(W), M, K, float(eps), ptr(offs), ptr(idx), ptr(ws), wsb, stream()),
+          "nerf_moe_dispatch")
+    return offs.cpu().tolist(), idx
+
+
+def gather_rows(src, idx, cols=None):
+    n = idx.numel()
+    cols = cols or src.shape[1]
+    dst = torch.empty((n, cols), dtype=torch.float32, device=src.device)
+    check(lib().nerf_gather_rows(ptr(src), src.stride(0), ptr(idx), n, cols, ptr(dst), cols, stream()),
+          "nerf_gather_rows")
+    return dst
+
+
+class _MixFn(torch.autograd.Function):
+    """out = sum_k (in expert order) index_add(sel_k, y_k * W[sel_k, k])."""
+
+    @staticmethod
+    def forward(ctx, W, N, C, sels, ks, *ys):
+        out = torch.zeros((N, C), dtype=torch.float32, device=W.device)
+        K = W.shape[1]
+        for k, sel, y in zip(ks, sels, ys):
+            y = y.contiguous().float()
+            check(lib().nerf_moe_combine(ptr(y), y.shape[0], C, ptr(sel), ptr(W), K, k, ptr(out), stream()),
+                  "nerf_moe_combine")
+        ctx.save_for_backward(W, *sels)
+        ctx.ks, ctx.C = ks, C
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g):
+        W, *sels = ctx.saved_tensors
+        g = g.contiguous().float()
+        K = W.shape[1]
+        grads = []
+        for k, sel in zip(ctx.ks, sels):
+            dy = torch.empty((sel.numel(), ctx.C), dtype=torch.float32, device=g.device)
+            check(lib().nerf_moe_combine_bwd(ptr(g), sel.numel(), ctx.C, ptr(sel), ptr(W), K, k, ptr(dy), stream()),
+                  "nerf_moe_combine_bwd")
+            grads.append(dy)
+        return (None, None, None, None, None, *grads)
+
+
+class _BgFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, d, w_packed, H):
+        d = d.contiguous().float()
+        N = d.shape[0]
+        out = torch.empty((N, 3), dtype=torch.float32, device=d.device)
+        check(lib().nerf_bg_mlp_fwd(ptr(d), d.stride(0), N, ptr(w_packed), H, ptr(out), stream()), "nerf_bg_mlp_fwd")
+        ctx.save_for_backward(d, w_packed)
+        ctx.H = H
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g):
+        d, w = ctx.saved_tensors
+        N = d.shape[0]
+        dw = torch.empty_like(w)
+        wsb = int(lib().nerf_bg_mlp_workspace_bytes(N, ctx.H))
+        ws = torch.empty(wsb, dtype=torch.uint8, device=d.device)
+        check(lib().nerf_bg_mlp_bwd(ptr(d), d.stride(0), N, ptr(w), ctx.H, ptr(g.contiguous().float()), ptr(dw),
+                                    ptr(ws), wsb, stream()), "nerf_bg_mlp_bwd")
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError("background MLP (HIP): no gradient w.r.t. directions")
+        return None, dw, None
+
+
+# ------------------------------------------------------------------ the container
+
+
+class MetaContainer(nn.Module):
+    def __init__(self, num_submodules: int, centroids: torch.Tensor, aabb: torch.Tensor,
+                 nerf_variant: str = "instant", boundary_margin: float = 1.0, cluster_2d: bool = True,
+                 joint_training: bool = False, use_bg_nerf: bool = True, bg_hidden: int = 32,
+                 bg_encoding: str = "spherical", occ_conf: Optional[Dict] = None, **nerf_kwargs):
+        super().__init__()
+        assert num_submodules > 0
+        assert centroids.ndim == 2 and centroids.size(0) == num_submodules
+        assert boundary_margin >= 1.0
+        if num_submodules > 32:
+            raise ValueError("at most 32 experts (nerf_moe_route)")
+        occ_conf = occ_conf or {}
+        aabb = torch.as_tensor(aabb, dtype=torch.float32)
+        self.register_buffer("scene_aabb_vec", torch.cat([aabb[0], aabb[1]], dim=0).float(), persistent=True)
+        self.register_buffer("centroids", torch.as_tensor(centroids).to(torch.float32), persistent=True)
+        self._cent_host = [float(v) for v in self.centroids[:, :3].reshape(-1).tolist()]
+        self.use_occ = bool(occ_conf.get("use_occ", False))
+        self.boundary_margin = float(boundary_margin)
+        self.cluster_2d = bool(cluster_2d)
+        self.joint_training = bool(joint_training)
+        self._coord_idx = (1, 2) if self.cluster_2d else (0, 1, 2)
+        self.nerf_variant = nerf_variant
+        self.dim_out = 4
+        boxes = nerf_kwargs.pop("expert_box_list")
+        base = {**nerf_kwargs, "occ_conf": occ_conf}
+        self.submodules = nn.ModuleList([build_expert(nerf_variant, **{**base, "scene_box": b}) for b in boxes])
+        self.use_bg_nerf = bool(use_bg_nerf)
+        if self.use_bg_nerf:
+            if bg_encoding != "spherical":
+                raise ValueError("bg_encoding='fourier' is broken in the reference (FrequencyEncoder without "
+                                 "in_dim, meta_container.py:83-86); use 'spherical'")
+            self.bg_dir_enc = SHEncoder(levels=4, implementation="tcnn")
+            self.bg_hidden_dim = int(bg_hidden)
+            if not 1 <= self.bg_hidden_dim <= 64:
+                raise ValueError("bg_hidden must be in [1, 64] (nerf_bg_mlp_fwd)")
+            self.bg_mlp = nn.Sequential(nn.Linear(self.bg_dir_enc.out_dim, self.bg_hidden_dim, bias=True), nn.ReLU(),
+                                        nn.Linear(self.bg_hidden_dim, 3, bias=True), nn.Sigmoid())
+        self._subdict_cache = {}
+
+    # ---- routing (meta_container.py:97-134)
+    def _routing(self, pts: torch.Tensor):
+        assert pts.dim() == 2 and pts.shape[-1] == 3, "pts must be (N,3)"
+        W = moe_route(pts.contiguous().float(), self._cent_host, self.boundary_margin, self.cluster_2d)
+        if self.boundary_margin > 1.0:
+            return W, None
+        return None, W.argmax(dim=1)
+
+    # ---- forward (meta_container.py:266-330)
+    def forward(self, x: torch.Tensor, params: Optional[OrderedDict] = None,
+                active_module: Optional[int] = None) -> torch.Tensor:
+        assert x.dim() == 2 and x.shape[-1] >= 6, "x must be (N,D>=6)"
+        K = len(self.submodules)
+        sub_params = ([self.get_subdict(params, f"submodules.{k}") for k in range(K)] if params is not None
+                      else [None] * K)
+        if active_module is not None:
+            return self.submodules[active_module](x, params=sub_params[active_module])
+        x = x.contiguous().float()
+        N = x.shape[0]
+        with torch.no_grad():
+            W = moe_route(x, self._cent_host, self.boundary_margin, self.cluster_2d)
+            offs, idx = moe_dispatch(W, 0.0)
+        ks, sels, ys = [], [], []
+        for k, sub in enumerate(self.submodules):
+            n_k = offs[k + 1] - offs[k]
+            if n_k == 0:
+                if self.joint_training:
+                    _ = sub(x[:0], params=sub_params[k])
+                continue
+            sel = idx[offs[k]:offs[k + 1]]
+            yk = sub(gather_rows(x, sel, 6), params=sub_params[k])
+            ks.append(k)
+            sels.append(sel)
+            ys.append(yk)
+        if not ys:
+            return x.new_zeros(N, self.dim_out)
+        return _MixFn.apply(W, N, ys[0].shape[-1], sels, ks, *ys)
+
+    # ---- background (meta_container.py:334-363)
+    def _bg_packed(self):
+        l0, l2 = self.bg_mlp[0], self.bg_mlp[2]
+        return torch.cat([l0.weight.reshape(-1), l0.bias, l2.weight.reshape(-1), l2.bias]).float()
+
+    def background_color(self, d: torch.Tensor) -> torch.Tensor:
+        if not self.use_bg_nerf:
+            raise RuntimeError("background_color called but use_bg_nerf=False")
+        if d.dim() not in (2, 3):
+            raise ValueError(f"background_color expects (N,3) or (B,N,3), got {tuple(d.shape)}")
+        flat = d.reshape(-1, 3)
+        rgb = _BgFn.apply(flat, self._bg_packed(), self.bg_hidden_dim)
+        return rgb.view(*d.shape[:-1], 3)
+
+    # ---- occupancy surface (not built)
+    @property
+    def occ_ready(self) -> bool:
+        return all(getattr(sub, "occ_ready", False) for sub in self.submodules)
+
+    def maybe_update_expert_occupancies(self, step: int, params=None) -> None:
+        if self.use_occ:
+            raise NotImplementedError("occupancy grids are SURVEY §8f row 2 (not built)")
+
+    # ---- MetaModule surface
+    def meta_named_parameters(self, prefix: str = "", recurse: bool = True):
+        for k, sub in enumerate(self.submodules):
+            for n, p in sub.meta_named_parameters(prefix=f"{prefix}submodules.{k}"):
+                yield n, p
+
+    def meta_parameters(self, recurse: bool = True):
+        for _, p in self.meta_named_parameters(recurse=recurse):
+            yield p
+
+    get_subdict = VanillaNeRF.get_subdict
+
+    def get_param_groups(self) -> Dict[str, Dict]:
+        """meta_container.py:458-503."""
+        enc: List = []
+        sig: List = []
+        col: List = []
+        bg: List = []
+        for sub in self.submodules:
+            if hasattr(sub, "get_param_groups"):
+                g = sub.get_param_groups()
+                enc += list(g.get("encoding", {}).get("params", []))
+                sig += list(g.get("sigma", {}).get("params", []))
+                col += list(g.get("color", {}).get("params", []))
+            else:
+                sig += list(sub.parameters())
+        if self.use_bg_nerf:
+            bg += list(self.bg_dir_enc.parameters()) + list(self.bg_mlp.parameters())
+        groups = {}
+        for name, ps in (("encoding", enc), ("sigma", sig), ("color", col), ("background", bg)):
+            if ps:
+                groups[name] = {"params": ps}
+        return groups
+
+    def load_reference_state(self, state: Dict[str, torch.Tensor]):
+        with torch.no_grad():
+            for n, p in self.named_parameters():
+                p.copy_(state[n].to(p.device, p.dtype))
+        return self

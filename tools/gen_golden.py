@@ -12,7 +12,7 @@ renderer), ``jaxtyping`` (scene_box.py:3, a type annotation), ``viser.transforms
 MetaNeRF's (x,d,params)->dict forward is wrapped in a 6-line adapter to the container
 contract expert(x_d (M,6), params) -> (M,4) (SURVEY.md §0 defect 2).
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--only-ngp]
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--only-ngp | --only-moe]
 """
 import os
 import sys
@@ -202,6 +202,7 @@ def main():
     np.savez_compressed(os.path.join(OUT, "train_step.npz"), gt=gt.numpy(), loss=np.float32(loss.item()),
                         gnorm=np.float32(gnorm.item()), lr=np.float32(2e-3), **after)
     gen_ngp()
+    gen_moe()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 
@@ -277,13 +278,75 @@ def gen_ngp():
     np.savez_compressed(os.path.join(OUT, "ngp.npz"), **arr)
 
 
+def gen_moe():
+    """MetaContainer fixtures: routing weights, the routed expert mix (soft margin
+    1.05 on (y,z), hard argmin on xyz) with every parameter gradient, and background_color + grads."""
+    from models.inr.meta_container import MetaContainer        # noqa: E402
+    from nerfs.scene_box import SceneBox                       # noqa: E402
+    g = torch.Generator().manual_seed(777)
+    arr = {}
+    K = 3
+    boxes = [torch.tensor([[-1.5, -1.5, -1.5], [0.2, 1.5, 1.5]]),
+             torch.tensor([[-0.2, -1.5, -1.5], [1.5, 0.2, 1.5]]),
+             torch.tensor([[-0.2, -0.2, -1.5], [1.5, 1.5, 1.5]])]
+    cents = torch.tensor([[-0.7, -0.4, 0.3], [0.6, -0.8, -0.2], [0.7, 0.7, 0.1]])
+    gaabb = torch.tensor([[-1.5, -1.5, -1.5], [1.5, 1.5, 1.5]])
+    M = 600
+    x = torch.rand(M, 3, generator=g) * 3 - 1.5
+    dd = torch.randn(M, 3, generator=g)
+    x_d = torch.cat([x, dd], -1)
+    arr["centroids"] = cents.numpy()
+    arr["x_d"] = x_d.numpy()
+    for i, b in enumerate(boxes):
+        arr[f"box{i}"] = b.numpy()
+    kw = dict(hidden=32, sigma_depth=1, color_hidden=32, color_depth=1, dir_encoding="spherical",
+              hash_enc_conf=dict(levels=4, features_per_level=2, log2_hashmap_size=10, min_res=8, max_res=128,
+                                 interpolation="Linear"))
+    for tag, bm, c2d in (("soft", 1.05, True), ("hard", 1.0, False)):
+        torch.manual_seed(11)
+        mc = MetaContainer(num_submodules=K, centroids=cents.clone(), aabb=gaabb.clone(), nerf_variant="instant",
+                           boundary_margin=bm, cluster_2d=c2d, use_bg_nerf=True, bg_hidden=32,
+                           bg_encoding="spherical", occ_conf={},
+                           expert_box_list=[SceneBox(aabb=b.clone()) for b in boxes], **kw)
+        with torch.no_grad():
+            for sub in mc.submodules:
+                sub.xyz_encoder.hash_table.copy_(torch.randn(sub.xyz_encoder.hash_table.shape, generator=g) * 0.5)
+        w, hard = mc._routing(x_d[:, :3])
+        out = mc(x_d)
+        gup = torch.randn(M, 4, generator=g)
+        names = [n for n, _ in mc.named_parameters()]
+        grads = torch.autograd.grad((out * gup).sum(), list(mc.parameters()), allow_unused=True)
+        arr[f"{tag}_route"] = (w if w is not None else torch.nn.functional.one_hot(hard, K).float()).numpy()
+        arr[f"{tag}_out"] = out.detach().numpy()
+        arr[f"{tag}_gup"] = gup.numpy()
+        for n, p in mc.named_parameters():
+            arr[f"{tag}_w/{n}"] = p.detach().numpy()
+        for n, gr in zip(names, grads):
+            if gr is not None:
+                arr[f"{tag}_g/{n}"] = gr.numpy()
+        groups = mc.get_param_groups()
+        arr[f"{tag}_groups"] = np.array([len(groups[k]["params"]) for k in ("encoding", "sigma", "color", "background")])
+        if tag == "soft":
+            dirs = torch.randn(300, 3, generator=g)
+            bg = mc.background_color(dirs)
+            gb = torch.randn(300, 3, generator=g)
+            bgn = [n for n, _ in mc.named_parameters() if n.startswith("bg_mlp")]
+            bgg = torch.autograd.grad((bg * gb).sum(), [dict(mc.named_parameters())[n] for n in bgn])
+            arr["bg_d"] = dirs.numpy()
+            arr["bg_out"] = bg.detach().numpy()
+            arr["bg_gup"] = gb.numpy()
+            for n, gr in zip(bgn, bgg):
+                arr[f"bg_g/{n}"] = gr.numpy()
+    np.savez_compressed(os.path.join(OUT, "moe.npz"), **arr)
+
+
 if __name__ == "__main__":
-    if "--only-ngp" in sys.argv:
+    if "--only-ngp" in sys.argv or "--only-moe" in sys.argv:
         sys.dont_write_bytecode = True
         _install_stubs()
         sys.path.insert(0, REF)
         torch.set_num_threads(8)
-        gen_ngp()
+        gen_ngp() if "--only-ngp" in sys.argv else gen_moe()
     else:
         main()
 
