@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""BASELINE.json configs[4]: "8-scene nerf_synthetic sweep, 4096-ray batches, 8xMI355X, report mean PSNR +
+aggregate rays/sec vs roofline".
+
+Eight Lego-style synthetic scenes (seeds 0..7 of nerf_amd.scene: different seeded sphere layouts and
+hemisphere poses; nerf_synthetic itself is not in the image) are trained independently with the
+benchmarked train step (4096 rays/step, 64 coarse + 128 fine, two 8x256 networks).  Under torchrun with W
+ranks, rank r trains scenes r, r+W, ... on its own GPU — the scenes are independent, so there is no
+collective on the data path; the per-scene results are gathered once at the end.  On one GPU the eight
+scenes run back to back.
+
+  python tools/sweep_scenes.py [--steps 1000] [--precision fp32|bf16] [--scenes 8]
+  torchrun --nproc-per-node 8 tools/sweep_scenes.py ...
+
+Prints one JSON line per scene and a summary: mean PSNR, aggregate rays/s (sum over GPUs of each GPU's
+training throughput), and the aggregate MFMA-roofline fraction (FLOP/ray of SURVEY §8d).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "nerf-sys_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FLOP_PER_RAY = 769327104
+PEAK = {"fp32": 157.3e12, "bf16": 2500e12}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scenes", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--lr", type=float, default=2e-3)
+    ap.add_argument("--train-views", type=int, default=100)
+    ap.add_argument("--test-views", type=int, default=2)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
+    a = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")  # only the final result gather crosses ranks
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    from nerf_amd.losses import image_psnr
+    from nerf_amd.ray_rendering import render_image
+    from nerf_amd.scene import make_blender_scene
+    from nerf_amd.trainer import NeRFTrainer, RayBatcher
+    from nerf_amd.vanilla import VanillaNeRF
+
+    results = []
+    for sid in range(rank, a.scenes, world):
+        torch.manual_seed(sid)
+        scene = make_blender_scene(n_train=a.train_views, n_test=a.test_views, seed=sid, device=dev)
+        coarse, fine = VanillaNeRF().to(dev), VanillaNeRF().to(dev)
+        tr = NeRFTrainer(coarse, fine, n_samples=64, n_importance=128, lr_sigma=a.lr, lr_color=a.lr, device=dev,
+                         precision=a.precision)
+        rb = RayBatcher(scene, dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for step in range(a.steps):
+            rays, gt = rb.batch(a.batch, seed=step)
+            loss = tr.step(rays, gt, seed=step)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        tr.sync_to_modules()
+        coarse.eval(), fine.eval()
+        fx, fy, cx, cy = scene.intrinsics
+        ps = []
+        for v in range(scene.test_poses.shape[0]):
+            img, _, _ = render_image(coarse, H=scene.H, W=scene.W, fx=fx, fy=fy, cx=cx, cy=cy, c2w=scene.test_poses[v],
+                                     near=scene.near, far=scene.far, ray_samples=64, n_importance=128, fine_model=fine)
+            ps.append(image_psnr(img, scene.test_images[v], "linear"))
+        rec = {"scene_seed": sid, "rank": rank, "steps": a.steps, "train_s": round(el, 2),
+               "rays_per_s": round(a.steps * a.batch / el, 1), "loss": round(float(loss.item()), 6),
+               "psnr": round(sum(ps) / len(ps), 3)}
+        print(json.dumps(rec), flush=True)
+        results.append(rec)
+        del tr, coarse, fine, scene, rb
+        torch.cuda.empty_cache()
+    if world > 1:
+        allr = [None] * world
+        dist.all_gather_object(allr, results)
+        results = [r for rr in allr for r in rr]
+    if rank == 0:
+        per_gpu = {}
+        for r in results:
+            per_gpu.setdefault(r["rank"], []).append(r)
+        # aggregate throughput: every GPU trains concurrently; each GPU's rate = its rays / its training time
+        agg = sum(sum(x["steps"] for x in rs) * a.batch / sum(x["train_s"] for x in rs) for rs in per_gpu.values())
+        summary = {"config": "configs[4]: 8-scene synthetic sweep, 4096-ray batches, 64+128, 2 x (8x256 MLP)",
+                   "precision": a.precision, "n_gpus": world, "scenes": len(results),
+                   "mean_psnr": round(sum(r["psnr"] for r in results) / len(results), 3),
+                   "aggregate_rays_per_s": round(agg, 1),
+                   "aggregate_mfma_frac": round(agg * FLOP_PER_RAY / (world * PEAK[a.precision]), 4),
+                   "data": "synthetic (seeded analytic scenes 0..7; nerf_synthetic not in the image)"}
+        print(json.dumps(summary), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
