@@ -1,0 +1,553 @@
+// Occupancy-grid rendering for the Instant-NGP expert on gfx950: the nerfacc pieces
+// the reference calls (nerfacc 0.5.3, requirements.txt:6; call sites nerfs/ray_rendering.py:349-558 and
+// models/inr/meta_ngp.py:108-145, 318-443) rebuilt as HIP kernels.  nerfacc's source is not in the image:
+// the algorithms are the published ones, restated in oracle/occ_oracle.py (PARITY UNPINNED):
+//
+//   OccGridEstimator.sampling            nerf_occ_march (count pass + write pass over a device-side scan)
+//   render_visibility_from_density       nerf_packed_visibility (+ nerf_packed_compact)
+//   render_weight_from_density +
+//   accumulate_along_rays (+ background) nerf_packed_composite_fwd / _bwd (one wave per ray, wave scans)
+//   OccGridEstimator.update_every_n_steps nerf_occ_cell_points -> (density) -> nerf_occ_update ->
+//                                        nerf_occ_threshold -> nerf_occ_binarize (no host sync)
+//   OccGridEstimator.mark_invisible_cells nerf_occ_mark_invisible
+//
+// Grid layout: levels x R^3 cells, cell id = l*R^3 + (ix*R + iy)*R + iz (meshgrid 'ij' order); level l
+// covers the ROI box scaled by 2^l about its centre; occs fp32 (-1 = invisible), binaries uint8.
+// Packed samples are ray-major: offsets[N+1] (int32), ray_idx / t0 / t1 per sample.
+#include "common.hpp"
+
+namespace {
+
+struct Grid {
+  int L, R;
+  float c[3], h[3];  // ROI centre and half size
+};
+
+Grid make_grid(const NerfOccGrid* g) {
+  Grid G{};
+  G.L = g->levels;
+  G.R = g->resolution;
+  for (int a = 0; a < 3; ++a) {
+    G.c[a] = 0.5f * (g->roi[a] + g->roi[3 + a]);
+    G.h[a] = 0.5f * (g->roi[3 + a] - g->roi[a]);
+  }
+  return G;
+}
+
+// level and cell of point p; returns -1 outside the outermost level
+__device__ __forceinline__ int64_t cell_of(const Grid& G, float px, float py, float pz, int* lvl_out, float cmin[3],
+                                           float csz[3]) {
+  const float p[3] = {px, py, pz};
+  float s = 0.f;
+  for (int a = 0; a < 3; ++a) s = fmaxf(s, fabsf(p[a] - G.c[a]) / G.h[a]);
+  int l = 0;
+  if (s > 1.0f) l = (int)ceilf(log2f(s));
+  if (l >= G.L) return -1;
+  const float scale = (float)(1 << l);
+  int64_t id = 0;
+  int ci[3];
+  for (int a = 0; a < 3; ++a) {
+    const float mn = G.c[a] - G.h[a] * scale;
+    const float sz = 2.0f * G.h[a] * scale;
+    int k = (int)floorf((p[a] - mn) / sz * (float)G.R);
+    k = k < 0 ? 0 : (k >= G.R ? G.R - 1 : k);
+    ci[a] = k;
+    csz[a] = sz / (float)G.R;
+    cmin[a] = mn + (float)k * csz[a];
+  }
+  *lvl_out = l;
+  id = (int64_t)l * G.R * G.R * G.R + ((int64_t)ci[0] * G.R + ci[1]) * G.R + ci[2];
+  return id;
+}
+
+// One thread per ray.  count pass (offsets == nullptr): counts[r] = #samples; write pass: fills the packed
+// arrays from offsets[r].
+__global__ void march_kernel(Grid G, const uint8_t* __restrict__ bin, const float* __restrict__ rays, int64_t N,
+                             float near_plane, float far_plane, float step, float cone, int stratified,
+                             const float* __restrict__ u, uint64_t seed, int max_steps, int32_t* __restrict__ counts,
+                             const int32_t* __restrict__ offsets, int32_t* __restrict__ ray_idx,
+                             float* __restrict__ t0, float* __restrict__ t1) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= N) return;
+  const float* ry = rays + r * 8;
+  const float o[3] = {ry[0], ry[1], ry[2]}, d[3] = {ry[3], ry[4], ry[5]};
+  float t = fmaxf(near_plane, ry[6]);
+  float tf = fminf(far_plane, ry[7]);
+  if (stratified) t += (u ? u[r] : nerf_uniform(seed, 0x0CC, (uint64_t)r)) * step;
+  // clip to the outermost level box
+  const float big = (float)(1 << (G.L - 1));
+  for (int a = 0; a < 3; ++a) {
+    const float lo = G.c[a] - G.h[a] * big, hi = G.c[a] + G.h[a] * big;
+    if (fabsf(d[a]) < 1e-12f) {
+      if (o[a] < lo || o[a] > hi) tf = -1.0f;
+      continue;
+    }
+    const float ta = (lo - o[a]) / d[a], tb = (hi - o[a]) / d[a];
+    t = fmaxf(t, fminf(ta, tb));
+    tf = fminf(tf, fmaxf(ta, tb));
+  }
+  int n = 0, it = 0;
+  int64_t w = offsets ? offsets[r] : 0;
+  while (t < tf && it < max_steps) {
+    ++it;
+    const float dt = fminf(fmaxf(t * cone, step), 1e10f);
+    const float mid = t + 0.5f * dt;
+    if (mid >= tf) break;
+    int lvl;
+    float cmin[3], csz[3];
+    const int64_t id = cell_of(G, o[0] + d[0] * mid, o[1] + d[1] * mid, o[2] + d[2] * mid, &lvl, cmin, csz);
+    if (id < 0) break;
+    if (bin[id]) {
+      if (offsets) {
+        ray_idx[w] = (int32_t)r;
+        t0[w] = t;
+        t1[w] = t + dt;
+        ++w;
+      }
+      ++n;
+      t = t + dt;
+    } else {
+      float te = INFINITY;
+      for (int a = 0; a < 3; ++a)
+        if (fabsf(d[a]) > 1e-12f) te = fminf(te, ((d[a] > 0.f ? cmin[a] + csz[a] : cmin[a]) - o[a]) / d[a]);
+      const float k = fmaxf(1.0f, ceilf((te - t) / dt));
+      t = t + k * dt;
+    }
+  }
+  if (!offsets) counts[r] = n;
+}
+
+// ---- exclusive scan of int32 (n+1 outputs): block sums -> one-thread scan of the sums -> add
+__global__ void scan_block_kernel(const int32_t* __restrict__ in, int64_t n, int32_t* __restrict__ out,
+                                  int32_t* __restrict__ bsum) {
+  __shared__ int32_t ws[4];
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int v = i < n ? in[i] : 0;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) ws[wave] = x;
+  __syncthreads();
+  int base = 0;
+  for (int k = 0; k < wave; ++k) base += ws[k];
+  if (i < n) out[i] = base + x - v;  // exclusive within the block
+  if (threadIdx.x == 255) bsum[blockIdx.x] = base + x;
+}
+
+__global__ void scan_sums_kernel(int32_t* __restrict__ bsum, int64_t nb, int32_t* __restrict__ out, int64_t n) {
+  if (threadIdx.x != 0) return;
+  int s = 0;
+  for (int64_t b = 0; b < nb; ++b) {
+    const int c = bsum[b];
+    bsum[b] = s;
+    s += c;
+  }
+  out[n] = s;
+}
+
+__global__ void scan_add_kernel(int32_t* __restrict__ out, int64_t n, const int32_t* __restrict__ bsum) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] += bsum[blockIdx.x];
+}
+
+// ---- packed compositing: one wave per ray, 64-sample chunks with a carried exclusive sum of sigma*dt
+__global__ void packed_fwd_kernel(const float* __restrict__ rs, const float* __restrict__ t0,
+                                  const float* __restrict__ t1, const int32_t* __restrict__ off, int64_t N,
+                                  const float* __restrict__ bg, float* __restrict__ rgb, float* __restrict__ depth,
+                                  float* __restrict__ accum, float* __restrict__ wout) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= N) return;
+  const int lane = threadIdx.x & 63;
+  const int s0 = off[r], s1 = off[r + 1];
+  float S = 0.f, cr = 0.f, cg = 0.f, cb = 0.f, dep = 0.f, a = 0.f;
+  for (int base = s0; base < s1; base += 64) {
+    const int j = base + lane;
+    float sdt = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f, tm = 0.f;
+    if (j < s1) {
+      const float4 v = reinterpret_cast<const float4*>(rs)[j];
+      const float a0 = t0[j], a1 = t1[j];
+      sdt = v.w * (a1 - a0);
+      c0 = v.x; c1 = v.y; c2 = v.z;
+      tm = 0.5f * (a0 + a1);
+    }
+    const float inc = wave_incl_sum(sdt);
+    const float T = expf(-(S + inc - sdt));
+    const float w = T * (1.0f - expf(-sdt));
+    if (j < s1) {
+      wout[j] = w;
+      cr += w * c0; cg += w * c1; cb += w * c2; dep += w * tm; a += w;
+    }
+    S += __shfl(inc, 63, 64);
+  }
+  cr = wave_sum(cr); cg = wave_sum(cg); cb = wave_sum(cb); dep = wave_sum(dep); a = wave_sum(a);
+  if (lane == 0) {
+    if (bg) {
+      cr += (1.0f - a) * bg[r * 3];
+      cg += (1.0f - a) * bg[r * 3 + 1];
+      cb += (1.0f - a) * bg[r * 3 + 2];
+    }
+    rgb[r * 3] = cr; rgb[r * 3 + 1] = cg; rgb[r * 3 + 2] = cb;
+    depth[r] = dep;
+    accum[r] = a;
+  }
+}
+
+// dL/dw_k = <g_rgb, c_k - bg> + g_depth t_mid_k + g_acc + g_w_k ;  dL/d(sdt_i) = g_i T_{i+1} - sum_{k>i} g_k w_k
+__global__ void packed_bwd_kernel(const float* __restrict__ rs, const float* __restrict__ t0,
+                                  const float* __restrict__ t1, const int32_t* __restrict__ off, int64_t N,
+                                  const float* __restrict__ bg, const float* __restrict__ grgb,
+                                  const float* __restrict__ gdep, const float* __restrict__ gacc,
+                                  const float* __restrict__ gw, float* __restrict__ drs) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= N) return;
+  const int lane = threadIdx.x & 63;
+  const int s0 = off[r], s1 = off[r + 1];
+  const float g0 = grgb[r * 3], g1 = grgb[r * 3 + 1], g2 = grgb[r * 3 + 2];
+  const float gd = gdep ? gdep[r] : 0.f;
+  float ga = gacc ? gacc[r] : 0.f;
+  if (bg) ga -= g0 * bg[r * 3] + g1 * bg[r * 3 + 1] + g2 * bg[r * 3 + 2];
+  // pass 1: total sum of g_k w_k
+  float S = 0.f, tot = 0.f;
+  for (int base = s0; base < s1; base += 64) {
+    const int j = base + lane;
+    float sdt = 0.f, gk = 0.f;
+    if (j < s1) {
+      const float4 v = reinterpret_cast<const float4*>(rs)[j];
+      sdt = v.w * (t1[j] - t0[j]);
+      gk = g0 * v.x + g1 * v.y + g2 * v.z + gd * 0.5f * (t0[j] + t1[j]) + ga + (gw ? gw[j] : 0.f);
+    }
+    const float inc = wave_incl_sum(sdt);
+    const float w = expf(-(S + inc - sdt)) * (1.0f - expf(-sdt));
+    tot += j < s1 ? gk * w : 0.f;
+    S += __shfl(inc, 63, 64);
+  }
+  tot = wave_sum(tot);
+  // pass 2: prefix of g_k w_k -> suffix = tot - inclusive prefix
+  S = 0.f;
+  float P = 0.f;
+  for (int base = s0; base < s1; base += 64) {
+    const int j = base + lane;
+    float sdt = 0.f, gk = 0.f, dt = 0.f;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (j < s1) {
+      v = reinterpret_cast<const float4*>(rs)[j];
+      dt = t1[j] - t0[j];
+      sdt = v.w * dt;
+      gk = g0 * v.x + g1 * v.y + g2 * v.z + gd * 0.5f * (t0[j] + t1[j]) + ga + (gw ? gw[j] : 0.f);
+    }
+    const float inc = wave_incl_sum(sdt);
+    const float Ti = expf(-(S + inc - sdt));
+    const float Tn = expf(-(S + inc));
+    const float w = Ti * (1.0f - expf(-sdt));
+    const float gwk = j < s1 ? gk * w : 0.f;
+    const float pin = wave_incl_sum(gwk);
+    const float suffix = tot - (P + pin);
+    if (j < s1) {
+      const float dsdt = gk * Tn - suffix;
+      reinterpret_cast<float4*>(drs)[j] = make_float4(w * g0, w * g1, w * g2, dsdt * dt);
+    }
+    S += __shfl(inc, 63, 64);
+    P += __shfl(pin, 63, 64);
+  }
+}
+
+// keep[j] = T_j >= eps && alpha_j >= alpha_thre  (one wave per ray)
+__global__ void packed_vis_kernel(const float* __restrict__ t0, const float* __restrict__ t1,
+                                  const float* __restrict__ sig, const int32_t* __restrict__ off, int64_t N,
+                                  float eps, float athr, int32_t* __restrict__ keep) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= N) return;
+  const int lane = threadIdx.x & 63;
+  const int s0 = off[r], s1 = off[r + 1];
+  float S = 0.f;
+  for (int base = s0; base < s1; base += 64) {
+    const int j = base + lane;
+    const float sdt = j < s1 ? sig[j] * (t1[j] - t0[j]) : 0.f;
+    const float inc = wave_incl_sum(sdt);
+    const float T = expf(-(S + inc - sdt));
+    const float al = 1.0f - expf(-sdt);
+    if (j < s1) keep[j] = (T >= eps && (athr <= 0.f || al >= athr)) ? 1 : 0;
+    S += __shfl(inc, 63, 64);
+  }
+}
+
+// compaction of kept samples: pos = exclusive scan of keep
+__global__ void compact_kernel(const int32_t* __restrict__ keep, const int32_t* __restrict__ pos, int64_t M,
+                               const int32_t* __restrict__ ri, const float* __restrict__ t0,
+                               const float* __restrict__ t1, int32_t* __restrict__ ri_o, float* __restrict__ t0_o,
+                               float* __restrict__ t1_o, int32_t* __restrict__ cnt_ray) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= M || !keep[j]) return;
+  const int p = pos[j];
+  ri_o[p] = ri[j];
+  t0_o[p] = t0[j];
+  t1_o[p] = t1[j];
+  atomicAdd(&cnt_ray[ri[j]], 1);
+}
+
+// ---- occupancy update
+__global__ void cell_points_kernel(Grid G, const int32_t* __restrict__ cells, int64_t n, uint64_t seed,
+                                   float* __restrict__ x) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t cpl = (int64_t)G.R * G.R * G.R;
+  const int64_t id = cells[i];
+  const int l = (int)(id / cpl);
+  const int64_t q = id - l * cpl;
+  const int ci[3] = {(int)(q / ((int64_t)G.R * G.R)), (int)((q / G.R) % G.R), (int)(q % G.R)};
+  const float scale = (float)(1 << l);
+  for (int a = 0; a < 3; ++a) {
+    const float f = ((float)ci[a] + nerf_uniform(seed, (uint64_t)i, (uint64_t)a)) / (float)G.R;
+    const float mn = G.c[a] - G.h[a] * scale;
+    x[i * 3 + a] = mn + f * (2.0f * G.h[a] * scale);
+  }
+}
+
+__global__ void occ_update_kernel(float* __restrict__ occs, const int32_t* __restrict__ cells,
+                                  const float* __restrict__ val, int64_t n, float decay) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t id = cells[i];
+  const float o = occs[id];
+  if (o >= 0.f) occs[id] = fmaxf(o * decay, val[i]);
+}
+
+// mean of the visible occupancies (occs >= 0), clamped to occ_thre -> thre[0]; also the mean over all cells ->
+// thre[1] (nerfacc caps alpha_thre at occs.mean()).  Single workgroup, fixed order: deterministic.
+__global__ void occ_thre_kernel(const float* __restrict__ occs, int64_t n, float occ_thre, float* __restrict__ thre) {
+  __shared__ double s1[256], s2[256];
+  __shared__ int64_t c1[256];
+  double a = 0.0, b = 0.0;
+  int64_t c = 0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) {
+    const float o = occs[i];
+    b += o;
+    if (o >= 0.f) { a += o; ++c; }
+  }
+  s1[threadIdx.x] = a; s2[threadIdx.x] = b; c1[threadIdx.x] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double A = 0.0, B = 0.0;
+    int64_t C = 0;
+    for (int k = 0; k < 256; ++k) { A += s1[k]; B += s2[k]; C += c1[k]; }
+    const float mean = C ? (float)(A / (double)C) : 0.f;
+    thre[0] = fminf(mean, occ_thre);
+    thre[1] = n ? (float)(B / (double)n) : 0.f;
+  }
+}
+
+__global__ void binarize_kernel(const float* __restrict__ occs, int64_t n, const float* __restrict__ thre,
+                                uint8_t* __restrict__ bin) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bin[i] = occs[i] > thre[0] ? 1 : 0;
+}
+
+// cells whose centre no camera sees (in front of near_plane and inside the image) -> occs = -1.
+// K (n_cam, 3, 3) row-major, c2w (n_cam, 3, 4) with RDF camera axes (meta_ngp.py:284-317).
+__global__ void mark_invisible_kernel(Grid G, const float* __restrict__ K, const float* __restrict__ c2w, int n_cam,
+                                      int W, int H, float near_plane, float* __restrict__ occs) {
+  const int64_t cpl = (int64_t)G.R * G.R * G.R;
+  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= cpl * G.L) return;
+  const int l = (int)(id / cpl);
+  const int64_t q = id - l * cpl;
+  const int ci[3] = {(int)(q / ((int64_t)G.R * G.R)), (int)((q / G.R) % G.R), (int)(q % G.R)};
+  const float scale = (float)(1 << l);
+  float x[3];
+  for (int a = 0; a < 3; ++a)
+    x[a] = G.c[a] - G.h[a] * scale + ((float)ci[a] + 0.5f) / (float)G.R * (2.0f * G.h[a] * scale);
+  bool vis = false;
+  for (int c = 0; c < n_cam && !vis; ++c) {
+    const float* P = c2w + c * 12;
+    const float dx = x[0] - P[3], dy = x[1] - P[7], dz = x[2] - P[11];
+    // camera coordinates: R^T (x - t)
+    const float xc = P[0] * dx + P[4] * dy + P[8] * dz;
+    const float yc = P[1] * dx + P[5] * dy + P[9] * dz;
+    const float zc = P[2] * dx + P[6] * dy + P[10] * dz;
+    if (zc <= near_plane) continue;
+    const float* k = K + c * 9;
+    const float u = (k[0] * xc + k[1] * yc + k[2] * zc) / zc;
+    const float v = (k[3] * xc + k[4] * yc + k[5] * zc) / zc;
+    vis = u >= 0.f && u < (float)W && v >= 0.f && v < (float)H;
+  }
+  if (!vis) occs[id] = -1.0f;
+}
+
+__global__ void ray_counts_kernel(const int32_t* __restrict__ ri, int64_t M, int32_t* __restrict__ counts) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < M) atomicAdd(&counts[ri[j]], 1);
+}
+
+__global__ void packed_points_kernel(const float* __restrict__ rays, const int32_t* __restrict__ ri,
+                                     const float* __restrict__ t0, const float* __restrict__ t1, int64_t M,
+                                     float* __restrict__ xd) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= M) return;
+  const float* r = rays + (int64_t)ri[j] * 8;
+  const float tm = 0.5f * (t0[j] + t1[j]);
+  float* o = xd + j * 6;
+  o[0] = r[0] + r[3] * tm;
+  o[1] = r[1] + r[4] * tm;
+  o[2] = r[2] + r[5] * tm;
+  o[3] = r[3];
+  o[4] = r[4];
+  o[5] = r[5];
+}
+
+bool grid_ok(const NerfOccGrid* g) {
+  if (!g || g->levels < 1 || g->levels > 8 || g->resolution < 1 || g->resolution > 512) return false;
+  for (int a = 0; a < 3; ++a)
+    if (!(g->roi[3 + a] > g->roi[a])) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" int nerf_occ_march(const NerfOccGrid* grid, const uint8_t* binaries, const float* rays, int64_t N,
+                              float near_plane, float far_plane, float step, float cone_angle, int stratified,
+                              const float* u, uint64_t seed, int max_steps, int32_t* counts, const int32_t* offsets,
+                              int32_t* ray_idx, float* t0, float* t1, hipStream_t st) {
+  if (!grid_ok(grid) || N < 0 || !(step > 0.f) || max_steps < 1) return NERF_E_ARG;
+  if (N == 0) return NERF_OK;
+  if (!binaries || !rays) return NERF_E_ARG;
+  if (!offsets && !counts) return NERF_E_ARG;
+  if (offsets && (!ray_idx || !t0 || !t1)) return NERF_E_ARG;
+  march_kernel<<<(unsigned)nerf_cdiv(N, 128), 128, 0, st>>>(make_grid(grid), binaries, rays, N, near_plane, far_plane,
+                                                            step, cone_angle, stratified, u, seed, max_steps, counts,
+                                                            offsets, ray_idx, t0, t1);
+  return nerf_launch_status();
+}
+
+extern "C" int64_t nerf_scan_workspace_bytes(int64_t n) {
+  if (n < 0) return NERF_E_ARG;
+  return nerf_cdiv(n < 1 ? 1 : n, 256) * 4 + 256;
+}
+
+extern "C" int nerf_exclusive_scan_i32(const int32_t* in, int64_t n, int32_t* out, void* ws, int64_t ws_bytes,
+                                       hipStream_t st) {
+  if (n < 0 || !out) return NERF_E_ARG;
+  if (n == 0) {
+    (void)hipMemsetAsync(out, 0, sizeof(int32_t), st);
+    return nerf_launch_status();
+  }
+  if (!in || !ws) return NERF_E_ARG;
+  const int64_t nb = nerf_cdiv(n, 256);
+  if (ws_bytes < nb * 4) return NERF_E_WORKSPACE;
+  int32_t* bs = reinterpret_cast<int32_t*>(ws);
+  scan_block_kernel<<<(unsigned)nb, 256, 0, st>>>(in, n, out, bs);
+  scan_sums_kernel<<<1, 64, 0, st>>>(bs, nb, out, n);
+  scan_add_kernel<<<(unsigned)nb, 256, 0, st>>>(out, n, bs);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_packed_composite_fwd(const float* rgb_sigma, const float* t0, const float* t1,
+                                         const int32_t* offsets, int64_t N, const float* bg, float* rgb, float* depth,
+                                         float* acc, float* weights, hipStream_t st) {
+  if (N < 0) return NERF_E_ARG;
+  if (N == 0) return NERF_OK;
+  if (!rgb_sigma || !t0 || !t1 || !offsets || !rgb || !depth || !acc || !weights) return NERF_E_ARG;
+  if (!nerf_aligned16(rgb_sigma)) return NERF_E_ALIGN;
+  packed_fwd_kernel<<<(unsigned)nerf_cdiv(N, 4), 256, 0, st>>>(rgb_sigma, t0, t1, offsets, N, bg, rgb, depth, acc,
+                                                               weights);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_packed_composite_bwd(const float* rgb_sigma, const float* t0, const float* t1,
+                                         const int32_t* offsets, int64_t N, const float* bg, const float* g_rgb,
+                                         const float* g_depth, const float* g_acc, const float* g_weights,
+                                         float* d_rgb_sigma, hipStream_t st) {
+  if (N < 0) return NERF_E_ARG;
+  if (N == 0) return NERF_OK;
+  if (!rgb_sigma || !t0 || !t1 || !offsets || !g_rgb || !d_rgb_sigma) return NERF_E_ARG;
+  if (!nerf_aligned16(rgb_sigma) || !nerf_aligned16(d_rgb_sigma)) return NERF_E_ALIGN;
+  packed_bwd_kernel<<<(unsigned)nerf_cdiv(N, 4), 256, 0, st>>>(rgb_sigma, t0, t1, offsets, N, bg, g_rgb, g_depth,
+                                                               g_acc, g_weights, d_rgb_sigma);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_packed_visibility(const float* t0, const float* t1, const float* sigmas, const int32_t* offsets,
+                                      int64_t N, float early_stop_eps, float alpha_thre, int32_t* keep,
+                                      hipStream_t st) {
+  if (N < 0) return NERF_E_ARG;
+  if (N == 0) return NERF_OK;
+  if (!t0 || !t1 || !sigmas || !offsets || !keep) return NERF_E_ARG;
+  packed_vis_kernel<<<(unsigned)nerf_cdiv(N, 4), 256, 0, st>>>(t0, t1, sigmas, offsets, N, early_stop_eps, alpha_thre,
+                                                               keep);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_packed_compact(const int32_t* keep, const int32_t* pos, int64_t M, const int32_t* ray_idx,
+                                   const float* t0, const float* t1, int32_t* ray_idx_out, float* t0_out,
+                                   float* t1_out, int32_t* counts_out, hipStream_t st) {
+  if (M < 0) return NERF_E_ARG;
+  if (M == 0) return NERF_OK;
+  if (!keep || !pos || !ray_idx || !t0 || !t1 || !ray_idx_out || !t0_out || !t1_out || !counts_out) return NERF_E_ARG;
+  compact_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(keep, pos, M, ray_idx, t0, t1, ray_idx_out, t0_out, t1_out,
+                                                              counts_out);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_occ_cell_points(const NerfOccGrid* grid, const int32_t* cells, int64_t n, uint64_t seed, float* x,
+                                    hipStream_t st) {
+  if (!grid_ok(grid) || n < 0) return NERF_E_ARG;
+  if (n == 0) return NERF_OK;
+  if (!cells || !x) return NERF_E_ARG;
+  cell_points_kernel<<<(unsigned)nerf_cdiv(n, 256), 256, 0, st>>>(make_grid(grid), cells, n, seed, x);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_occ_update(float* occs, const int32_t* cells, const float* values, int64_t n, float ema_decay,
+                               hipStream_t st) {
+  if (n < 0) return NERF_E_ARG;
+  if (n == 0) return NERF_OK;
+  if (!occs || !cells || !values) return NERF_E_ARG;
+  occ_update_kernel<<<(unsigned)nerf_cdiv(n, 256), 256, 0, st>>>(occs, cells, values, n, ema_decay);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_occ_threshold(const float* occs, int64_t n, float occ_thre, float* thre_out, hipStream_t st) {
+  if (n < 0 || !occs || !thre_out) return NERF_E_ARG;
+  occ_thre_kernel<<<1, 256, 0, st>>>(occs, n, occ_thre, thre_out);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_occ_binarize(const float* occs, int64_t n, const float* thre, uint8_t* binaries, hipStream_t st) {
+  if (n < 0) return NERF_E_ARG;
+  if (n == 0) return NERF_OK;
+  if (!occs || !thre || !binaries) return NERF_E_ARG;
+  binarize_kernel<<<(unsigned)nerf_cdiv(n, 256), 256, 0, st>>>(occs, n, thre, binaries);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_occ_mark_invisible(const NerfOccGrid* grid, const float* K, const float* c2w, int n_cam, int W,
+                                       int H, float near_plane, float* occs, hipStream_t st) {
+  if (!grid_ok(grid) || n_cam < 0 || W < 1 || H < 1) return NERF_E_ARG;
+  if (!occs || (n_cam > 0 && (!K || !c2w))) return NERF_E_ARG;
+  const int64_t n = (int64_t)grid->levels * grid->resolution * grid->resolution * grid->resolution;
+  mark_invisible_kernel<<<(unsigned)nerf_cdiv(n, 256), 256, 0, st>>>(make_grid(grid), K, c2w, n_cam, W, H, near_plane,
+                                                                     occs);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_ray_counts(const int32_t* ray_idx, int64_t M, int64_t N, int32_t* counts, hipStream_t st) {
+  if (M < 0 || N < 0 || !counts) return NERF_E_ARG;
+  (void)hipMemsetAsync(counts, 0, (N < 1 ? 1 : N) * sizeof(int32_t), st);
+  if (M == 0) return nerf_launch_status();
+  if (!ray_idx) return NERF_E_ARG;
+  ray_counts_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(ray_idx, M, counts);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_packed_points(const float* rays, const int32_t* ray_idx, const float* t0, const float* t1,
+                                  int64_t M, float* x_d, hipStream_t st) {
+  if (M < 0) return NERF_E_ARG;
+  if (M == 0) return NERF_OK;
+  if (!rays || !ray_idx || !t0 || !t1 || !x_d) return NERF_E_ARG;
+  packed_points_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(rays, ray_idx, t0, t1, M, x_d);
+  return nerf_launch_status();
+}

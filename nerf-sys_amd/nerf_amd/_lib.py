@@ -65,6 +65,20 @@ def lib():
             "nerf_bg_mlp_fwd": [P, I64, I64, P, I, P, P],
             "nerf_bg_mlp_workspace_bytes": [I64, I],
             "nerf_bg_mlp_bwd": [P, I64, I64, P, I, P, P, P, I64, P],
+            "nerf_occ_march": [P, P, P, I64, F, F, F, F, I, P, U64, I, P, P, P, P, P, P],
+            "nerf_scan_workspace_bytes": [I64],
+            "nerf_exclusive_scan_i32": [P, I64, P, P, I64, P],
+            "nerf_packed_composite_fwd": [P, P, P, P, I64, P, P, P, P, P, P],
+            "nerf_packed_composite_bwd": [P, P, P, P, I64, P, P, P, P, P, P, P],
+            "nerf_packed_visibility": [P, P, P, P, I64, F, F, P, P],
+            "nerf_packed_compact": [P, P, I64, P, P, P, P, P, P, P, P],
+            "nerf_occ_cell_points": [P, P, I64, U64, P, P],
+            "nerf_occ_update": [P, P, P, I64, F, P],
+            "nerf_occ_threshold": [P, I64, F, P, P],
+            "nerf_occ_binarize": [P, I64, P, P, P],
+            "nerf_occ_mark_invisible": [P, P, P, I, I, I, F, P, P],
+            "nerf_ray_counts": [P, I64, I64, P, P],
+            "nerf_packed_points": [P, P, P, P, I64, P, P],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -78,6 +92,7 @@ def lib():
         L.nerf_ngp_workspace_bytes.restype = c_int64
         L.nerf_moe_dispatch_workspace_bytes.restype = c_int64
         L.nerf_bg_mlp_workspace_bytes.restype = c_int64
+        L.nerf_scan_workspace_bytes.restype = c_int64
         _lib = L
     return _lib
 
@@ -90,7 +105,11 @@ EXPORTS = ("nerf_rays_gen", "nerf_pick_pixels", "nerf_clamp_near_far", "nerf_ray
            "nerf_hash_encode", "nerf_hash_encode_bwd", "nerf_sh_encode", "nerf_ngp_layout",
            "nerf_ngp_workspace_bytes", "nerf_ngp_fwd", "nerf_ngp_bwd", "nerf_moe_route",
            "nerf_moe_dispatch_workspace_bytes", "nerf_moe_dispatch", "nerf_gather_rows", "nerf_moe_combine",
-           "nerf_moe_combine_bwd", "nerf_bg_mlp_fwd", "nerf_bg_mlp_workspace_bytes", "nerf_bg_mlp_bwd")
+           "nerf_moe_combine_bwd", "nerf_bg_mlp_fwd", "nerf_bg_mlp_workspace_bytes", "nerf_bg_mlp_bwd",
+           "nerf_occ_march", "nerf_scan_workspace_bytes", "nerf_exclusive_scan_i32", "nerf_packed_composite_fwd",
+           "nerf_packed_composite_bwd", "nerf_packed_visibility", "nerf_packed_compact", "nerf_occ_cell_points",
+           "nerf_occ_update", "nerf_occ_threshold", "nerf_occ_binarize", "nerf_occ_mark_invisible", "nerf_ray_counts",
+           "nerf_packed_points")
 
 
 def check(status: int, what: str) -> None:

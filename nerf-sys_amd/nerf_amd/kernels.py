@@ -226,3 +226,12 @@ def adam(p, g, m, v, seg_off: Sequence[int], seg_lr: Sequence[float], step, beta
     lr = (ctypes.c_double * len(seg_lr))(*seg_lr)
     check(lib().nerf_adam(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), off, lr, len(seg_lr), betas[0], betas[1], eps,
                           weight_decay, step, ptr(partials), max_norm, stream()), "nerf_adam")
+
+
+def packed_points(rays, ray_idx, t0, t1):
+    """nerf_packed_points: x_d (M,6) = [o + d (t0+t1)/2, d] of packed intervals."""
+    M = ray_idx.numel()
+    xd = torch.empty((M, 6), dtype=F32, device=rays.device)
+    check(lib().nerf_packed_points(ptr(rays), ptr(ray_idx.to(torch.int32).contiguous()), ptr(t0), ptr(t1), M, ptr(xd),
+                                   stream()), "nerf_packed_points")
+    return xd

@@ -14,8 +14,9 @@ MetaModule, metamodule.py:20-30).
 Compute: ``nerf_hash_encode`` (gather, world->unit mapping fused) -> ``nerf_ngp_fwd`` (all MLP layers in
 one fused fp32-MFMA kernel) ; backward ``nerf_ngp_bwd`` (forward recomputed on chip, weight gradients
 reduced per workgroup) -> ``nerf_hash_encode_bwd`` (fp32 atomics into the table gradient).  No CPU
-fallback: every op requires HIP tensors.  The occupancy renderer (``use_occ``) is §8f row 2 and not built:
-requesting it raises.
+fallback: every op requires HIP tensors.  ``use_occ`` builds an occupancy grid (``occupancy.OccGridEstimator``,
+§8f row 2) with MetaNGP's marching / update / premark methods; ``render_rays`` then takes the packed
+occupancy renderer once ``occ_ready``.
 """
 from __future__ import annotations
 
@@ -319,9 +320,6 @@ class InstantNGP(nn.Module):
                  hash_enc_conf: Optional[Dict] = None, dir_encoding: str = "spherical", **kwargs) -> None:
         super().__init__()
         occ_conf = occ_conf or {}
-        if bool(occ_conf.get("use_occ", False)):
-            raise NotImplementedError("the occupancy renderer (nerfacc OccGridEstimator) is SURVEY §8f row 2 "
-                                      "and not built yet; use use_occ=False (stratified render_rays)")
         aabb = scene_box.aabb if hasattr(scene_box, "aabb") else scene_box
         aabb = torch.as_tensor(aabb, dtype=torch.float32).reshape(2, 3).cpu()
         if not bool((aabb[0] < aabb[1]).all()):
@@ -331,7 +329,7 @@ class InstantNGP(nn.Module):
         self._aabb_host = [float(v) for v in aabb.reshape(-1).tolist()]
         self._eps = float(torch.tensor(1e-6, dtype=torch.float32))
         self.scene_box = scene_box
-        self.use_occ = False
+        self.use_occ = bool(occ_conf.get("use_occ", False))
         self.occ_ready = False
         self.use_bg_nerf = False
         self.dim_out = 4
@@ -379,6 +377,98 @@ class InstantNGP(nn.Module):
         shapes = OrderedDict((n, tuple(p.shape)) for n, p in self.named_parameters() if not n.startswith("xyz_encoder."))
         self.layout = NgpLayout(net, shapes, self.sigma_depth, self.color_depth)
         self._subdict_cache = {}
+        if self.use_occ:  # meta_ngp.py:108-145
+            from .occupancy import OccGridEstimator
+            diag = float((aabb[1] - aabb[0]).norm())
+            rss = occ_conf.get("render_step_size")
+            self.render_step_size = float(rss) if rss is not None else diag / 1000.0
+            self.occ_thre = float(occ_conf.get("occ_thre", 1e-2))
+            self.alpha_thre = float(occ_conf.get("alpha_thre", 1e-2))
+            self.cone_angle = float(occ_conf.get("cone_angle", 1.0 / 256.0))
+            self.near_plane = float(occ_conf.get("near_plane", 0.05))
+            self.far_plane = float(occ_conf.get("far_plane", 1e3))
+            self.occ_update_interval = int(occ_conf.get("update_interval", 16))
+            self.occ_warmup_steps = int(occ_conf.get("warmup_steps", 256))
+            self.occ_cosine_anneal = bool(occ_conf.get("cosine_anneal", True))
+            self.occ_alpha_thre_start = float(occ_conf.get("alpha_thre_start", 0.0))
+            self.occ_alpha_thre_end = float(occ_conf.get("alpha_thre_end", self.alpha_thre))
+            self.occ_ema_decay = float(occ_conf.get("ema_decay", 0.95))
+            self.occ_resolution = int(occ_conf.get("resolution", 128))
+            self.occ_levels = int(occ_conf.get("levels", 4))
+            self.register_buffer("scene_aabb", torch.cat([aabb[0], aabb[1]]).flatten())
+            self.occ_grid = OccGridEstimator(roi_aabb=self.scene_aabb, resolution=self.occ_resolution,
+                                             levels=self.occ_levels)
+            self.occ_frozen = bool(occ_conf.get("occ_frozen", False))
+            self.occ_ready = bool(occ_conf.get("occ_ready", False))
+            self.num_occ_updates = 0
+            self.occ_premarked = False
+
+    # ---- density / occupancy (meta_ngp.py:203-239, 245-258, 318-443)
+    def density(self, x: torch.Tensor, params=None, return_feats: bool = False):
+        """sigma (...,1) at world points (the fused kernel evaluates the whole network; directions are unused
+        by sigma).  return_feats is not supported (geo features stay on chip)."""
+        if return_feats:
+            raise NotImplementedError("density(return_feats=True): geo features are not materialised")
+        shp = x.shape[:-1]
+        xd = torch.cat([x.reshape(-1, 3).float(), torch.zeros_like(x.reshape(-1, 3).float())], -1)
+        xd[:, 5] = 1.0
+        return self.forward(xd, params=params)[:, 3:4].view(*shp, 1)
+
+    def _anneal_alpha_thre(self, step: int) -> None:
+        if step < self.occ_warmup_steps:
+            t = step / max(1, self.occ_warmup_steps - 1)
+            if self.occ_cosine_anneal:
+                c = 0.5 * (1 - math.cos(math.pi * t))
+                self.alpha_thre = (1 - c) * self.occ_alpha_thre_start + c * self.occ_alpha_thre_end
+            else:
+                self.alpha_thre = (1 - t) * self.occ_alpha_thre_start + t * self.occ_alpha_thre_end
+        else:
+            self.alpha_thre = self.occ_alpha_thre_end
+
+    @torch.no_grad()
+    def maybe_update_occ_grid(self, step: int, params=None) -> None:
+        if not (self.training and self.use_occ and not self.occ_frozen):
+            return
+        self.occ_ready = step >= self.occ_warmup_steps
+        self._anneal_alpha_thre(step)
+        self.occ_grid.update_every_n_steps(
+            step=step, occ_eval_fn=lambda x: self.density(x, params=params).squeeze(-1) * self.render_step_size,
+            occ_thre=self.occ_thre, ema_decay=self.occ_ema_decay, warmup_steps=self.occ_warmup_steps,
+            n=self.occ_update_interval)
+        self.num_occ_updates += 1
+
+    @torch.no_grad()
+    def premark_invisible_cells_from(self, K, c2w_rdf, width: int, height: int, near_plane: float = 0.05) -> None:
+        """premark_invisible_cells (meta_ngp.py:318-347) from stacked intrinsics (n,3,3) and RDF c2w (n,3,4)."""
+        if not self.use_occ or self.occ_premarked:
+            return
+        self.occ_grid.mark_invisible_cells(K=K, c2w=c2w_rdf, width=width, height=height, near_plane=near_plane)
+        self.occ_premarked = True
+
+    @torch.no_grad()
+    def occupancy_marching_packed(self, rays, *, params=None, render_step_size=None, alpha_thre=None,
+                                  cone_angle=None):
+        """occupancy_marching (meta_ngp.py:384-443) -> (ray_idx int32, t0, t1, offsets int32 (N+1))."""
+        if getattr(self, "occ_grid", None) is None:
+            raise RuntimeError("MetaNGP: occ_grid missing")
+        rays = rays.contiguous().float()
+        o, d = rays[:, :3], rays[:, 3:6]
+        sigma_fn = None
+        if self.training:
+            def sigma_fn(t_starts, t_ends, ray_indices):
+                mids = 0.5 * (t_starts + t_ends)
+                x = o[ray_indices] + d[ray_indices] * mids[:, None]
+                return self.density(x, params=params).squeeze(-1)
+        return self.occ_grid.sampling_packed(
+            o, d, sigma_fn=sigma_fn, near_plane=self.near_plane, far_plane=self.far_plane, t_min=rays[:, 6],
+            t_max=rays[:, 7], render_step_size=self.render_step_size if render_step_size is None else render_step_size,
+            stratified=self.training, cone_angle=self.cone_angle if cone_angle is None else cone_angle,
+            alpha_thre=self.alpha_thre if alpha_thre is None else alpha_thre)
+
+    def occupancy_marching(self, rays, *, params=None, render_step_size=None, alpha_thre=None, cone_angle=None):
+        ri, t0, t1, _ = self.occupancy_marching_packed(rays, params=params, render_step_size=render_step_size,
+                                                       alpha_thre=alpha_thre, cone_angle=cone_angle)
+        return ri.long(), t0, t1
 
     # ---- MetaModule surface (models/metamodule/metamodule.py:20-69): the hash table is not a meta parameter
     def meta_named_parameters(self, prefix: str = "", recurse: bool = True):

@@ -8,8 +8,8 @@ and error behaviour):
 Extensions (absent in the reference, parity pinned against the CPU oracle only): hierarchical
 sampling through ``sample_pdf`` (canonical NeRF) via the ``n_importance`` keyword, which renders the
 fine pass with ``fine_model`` (or ``model.fine``, or the same expert) and returns the coarse outputs
-in ``extras`` when ``return_extras=True``.  The occupancy / MoE renderer (render_rays_occ, :349-558)
-is out of this round's scope and raises.
+in ``extras`` when ``return_extras=True``.  The occupancy renderer (render_rays_occ / render_expert_occ,
+:349-558) runs on the packed HIP kernels for single experts (and containers with ``active_module``).
 """
 from __future__ import annotations
 
@@ -166,10 +166,44 @@ def render_rays_stratified(model, rays: Tensor, ray_samples: int, params=None, a
     return out
 
 
+def render_expert_occ(model, rays: Tensor, *, params=None, bg_color_default: str = "white", chunk: int = 1_000_000,
+                      render_step_size=None, alpha_thre=None, cone_angle=None, **kwargs):
+    """ray_rendering.py:484-558: occupancy marching -> expert at the interval midpoints -> packed
+    integration (nerfacc render_weight_from_density + accumulate_along_rays) + background, as ONE fused
+    kernel.  Returns rgb (N,3), depth (N,), weights (M,1) packed, acc (N,)."""
+    from .occupancy import render_packed
+    rays = rays.contiguous().float()
+    N = rays.shape[0]
+    d = rays[:, 3:6]
+    ri, t0, t1, offs = model.occupancy_marching_packed(rays, params=params, render_step_size=render_step_size,
+                                                       alpha_thre=alpha_thre, cone_angle=cone_angle)
+    if t0.numel() == 0:
+        acc = rays.new_zeros(N)
+        bg_rgb = _get_bg_rgb(model, d, params, rays, N, bg_color_default)
+        return bg_rgb, acc.clone(), torch.zeros(1, 1, device=rays.device, dtype=rays.dtype), acc
+    xd = K.packed_points(rays, ri, t0, t1)
+    outs = [model(xd[s:s + chunk], params=params) for s in range(0, xd.shape[0], chunk)]
+    rgb_sigma = torch.cat(outs, 0)
+    bg = _get_bg_rgb(model, d, params, rays, N, bg_color_default)  # device/dtype source; 'last_sample' raises
+    rgb, depth, w, acc = render_packed(rgb_sigma, t0, t1, offs, bg)
+    return rgb, depth, w[:, None], acc
+
+
+def render_rays_occ(model, rays: Tensor, *, params=None, active_module: Optional[int] = None, **kwargs):
+    """ray_rendering.py:349-481.  Single experts (and a container with active_module) render through
+    render_expert_occ; the full-container soft-MoE union path is not built yet."""
+    if active_module is not None:
+        return render_expert_occ(model.submodules[active_module], rays, params=params, **kwargs)
+    if getattr(model, "occ_grid", None) is not None:
+        return render_expert_occ(model, rays, params=params, **kwargs)
+    raise NotImplementedError("occupancy rendering of a full MoE container (segment union + soft mix) is not "
+                              "built yet; pass active_module=k or use_occ=False")
+
+
 def render_rays(model, rays, *args, **kwargs):
     """ray_rendering.py:564-574 dispatch."""
     if getattr(model, "use_occ", False) and getattr(model, "occ_ready", False):
-        raise NotImplementedError("occupancy / MoE renderer (render_rays_occ) is not part of this build yet")
+        return render_rays_occ(model, rays, **kwargs)
     return render_rays_stratified(model, rays, *args, **kwargs)
 
 
