@@ -332,6 +332,30 @@ int nerf_ray_counts(const int32_t* ray_idx, int64_t M, int64_t N, int32_t* count
 int nerf_packed_points(const float* rays, const int32_t* ray_idx, const float* t0, const float* t1, int64_t M,
                        float* x_d, hipStream_t stream);
 
+/* Full-container occupancy rendering (render_rays_occ, nerfs/ray_rendering.py:384-481).
+ * nerf_rays_aabb_hit: _intersect_rays_aabb (:171-190) of rays (N,8) with box (HOST, 6 floats) -> hit (N) int32.
+ * nerf_flag_compact: idx[pos[i]] = i for flags[i] != 0 (pos = exclusive scan of flags).
+ * nerf_scatter_counts: counts[hit_idx[i]] = counts_k[i] (an expert's per-ray counts on the global rays).
+ * nerf_segments_union: _merge_segments_union (:193-258): per ray, the sorted distinct union of every expert's
+ *   t0 and t1 boundaries (t0s / t1s / offs: HOST arrays of K <= 8 device pointers; offs[k] (N+1) per-expert
+ *   offsets over the global rays) -> the segments between consecutive boundaries.  Count pass (out_off NULL)
+ *   -> counts (N); write pass -> ray_idx / t0 / t1 at out_off.
+ * nerf_moe_blend / _finish / _bwd: sigma and rgb blended BEFORE integration (:441-471): s += w_k sigma_k,
+ *   c += (w_k sigma_k) rgb_k over the rows expert k evaluated (call in expert order), then
+ *   rgb_sigma = [c / max(s, 1e-12), max(s, 1e-12)]; backward per expert -> d_y (n,4). */
+int nerf_rays_aabb_hit(const float* rays, int64_t N, const float* box, int32_t* hit, hipStream_t stream);
+int nerf_flag_compact(const int32_t* flags, const int32_t* pos, int64_t n, int32_t* idx, hipStream_t stream);
+int nerf_scatter_counts(const int32_t* hit_idx, const int32_t* counts_k, int64_t n, int32_t* counts, hipStream_t stream);
+int nerf_segments_union(const float* const* t0s, const float* const* t1s, const int32_t* const* offs, int K, int64_t N,
+                        int32_t* counts, const int32_t* out_off, int32_t* ray_idx, float* t0, float* t1,
+                        hipStream_t stream);
+int nerf_moe_blend(const float* y, int64_t n, const int32_t* idx, const float* weights, int K, int k, float* s_acc,
+                   float* c_acc, hipStream_t stream);
+int nerf_moe_blend_finish(const float* s_acc, const float* c_acc, int64_t M, float* rgb_sigma, hipStream_t stream);
+int nerf_moe_blend_bwd(const float* y, int64_t n, const int32_t* idx, const float* weights, int K, int k,
+                       const float* s_acc, const float* rgb_sigma, const float* d_rgb_sigma, float* d_y,
+                       hipStream_t stream);
+
 /* Library build identification (string, static). */
 const char* nerf_version(void);
 

@@ -361,3 +361,206 @@ extern "C" int nerf_bg_mlp_bwd(const float* d, int64_t d_stride, int64_t N, cons
   bg_reduce_kernel<<<(unsigned)nerf_cdiv(P, 256), 256, 0, st>>>(slab, (int)nblk, P, d_w);
   return nerf_launch_status();
 }
+
+// ==================================================================================== occupancy MoE path
+// render_rays_occ for a full container (nerfs/ray_rendering.py:384-481): per-expert AABB prefilter
+// (_intersect_rays_aabb :171-190), union of the experts' marched segments per ray (_merge_segments_union
+// :193-258, a per-ray Python loop in the reference), and the soft blend of sigma / rgb BEFORE integration.
+
+namespace {
+
+__global__ void rays_aabb_hit_kernel(const float* __restrict__ rays, int64_t N, float x0, float y0, float z0, float x1,
+                                     float y1, float z1, int32_t* __restrict__ hit) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= N) return;
+  const float* ry = rays + r * 8;
+  const float mn[3] = {x0, y0, z0}, mx[3] = {x1, y1, z1};
+  float tmin = -INFINITY, tmax = INFINITY;
+  for (int a = 0; a < 3; ++a) {
+    const float d = ry[3 + a];
+    const float inv = fabsf(d) > 1e-9f ? 1.0f / d : 1.0f / 1e-9f;
+    const float t0 = (mn[a] - ry[a]) * inv, t1 = (mx[a] - ry[a]) * inv;
+    tmin = fmaxf(tmin, fminf(t0, t1));
+    tmax = fminf(tmax, fmaxf(t0, t1));
+  }
+  hit[r] = fminf(tmax, ry[7]) > fmaxf(tmin, ry[6]) ? 1 : 0;
+}
+
+// idx of the set flags (order preserving): pos = exclusive scan of flags
+__global__ void flag_compact_kernel(const int32_t* __restrict__ flag, const int32_t* __restrict__ pos, int64_t n,
+                                    int32_t* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && flag[i]) idx[pos[i]] = (int32_t)i;
+}
+
+// Per ray: K-way merge of the experts' sorted boundary lists (t0 list and t1 list of every expert), unique,
+// -> segments between consecutive distinct boundaries.  seg (K*2 lists): for expert k the ray's samples are
+// [s0k, s1k) of its packed arrays.  Count pass (out_off == nullptr) or write pass.
+struct ExpertLists {
+  const float* t0[8];
+  const float* t1[8];
+  const int32_t* off[8];   // per-expert offsets over the GLOBAL rays (N+1)
+};
+
+__global__ void union_kernel(ExpertLists E, int K, int64_t N, int32_t* __restrict__ counts,
+                             const int32_t* __restrict__ out_off, int32_t* __restrict__ ri_o, float* __restrict__ t0_o,
+                             float* __restrict__ t1_o) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= N) return;
+  int pa[8], pb[8], end[8];
+  for (int k = 0; k < K; ++k) {
+    pa[k] = E.off[k][r];
+    pb[k] = pa[k];
+    end[k] = E.off[k][r + 1];
+  }
+  float prev = 0.f;
+  bool have = false;
+  int nb = 0;
+  int64_t w = out_off ? out_off[r] : 0;
+  while (true) {
+    // smallest head among the 2K sorted lists
+    float best = INFINITY;
+    int bk = -1, which = 0;
+    for (int k = 0; k < K; ++k) {
+      if (pa[k] < end[k] && E.t0[k][pa[k]] < best) { best = E.t0[k][pa[k]]; bk = k; which = 0; }
+      if (pb[k] < end[k] && E.t1[k][pb[k]] < best) { best = E.t1[k][pb[k]]; bk = k; which = 1; }
+    }
+    if (bk < 0) break;
+    if (which == 0) ++pa[bk]; else ++pb[bk];
+    if (have && best == prev) continue;  // unique
+    if (have) {
+      if (out_off) {
+        ri_o[w] = (int32_t)r;
+        t0_o[w] = prev;
+        t1_o[w] = best;
+        ++w;
+      }
+      ++nb;
+    }
+    prev = best;
+    have = true;
+  }
+  if (!out_off) counts[r] = nb;
+}
+
+// per-expert ray counts on the global ray index: cnt[hit_idx[i]] = counts_k[i]
+__global__ void scatter_counts_kernel(const int32_t* __restrict__ hit_idx, const int32_t* __restrict__ cnt_k,
+                                      int64_t n, int32_t* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) cnt[hit_idx[i]] = cnt_k[i];
+}
+
+// blend of expert k's (rgb, sigma) rows into the mix accumulators (expert order, as the reference's sums):
+// s[m] += W[m,k] * sigma ; c[m] += (W[m,k] * sigma) * rgb
+__global__ void blend_kernel(const float* __restrict__ y, int64_t n, const int32_t* __restrict__ idx,
+                             const float* __restrict__ W, int K, int k, float* __restrict__ s, float* __restrict__ c) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t m = idx[i];
+  const float4 v = reinterpret_cast<const float4*>(y)[i];
+  const float ws = W[m * K + k] * v.w;
+  s[m] = s[m] + ws;
+  c[m * 3] = c[m * 3] + ws * v.x;
+  c[m * 3 + 1] = c[m * 3 + 1] + ws * v.y;
+  c[m * 3 + 2] = c[m * 3 + 2] + ws * v.z;
+}
+
+// rs_mix[m] = [c / max(s, 1e-12), max(s, 1e-12)]
+__global__ void blend_finish_kernel(const float* __restrict__ s, const float* __restrict__ c, int64_t M,
+                                    float* __restrict__ rs) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  const float sn = fmaxf(s[m], 1e-12f);
+  reinterpret_cast<float4*>(rs)[m] = make_float4(c[m * 3] / sn, c[m * 3 + 1] / sn, c[m * 3 + 2] / sn, sn);
+}
+
+// backward of the blend for expert k: given d rs_mix (M,4) and the raw sums, d y_k (n,4)
+__global__ void blend_bwd_kernel(const float* __restrict__ y, int64_t n, const int32_t* __restrict__ idx,
+                                 const float* __restrict__ W, int K, int k, const float* __restrict__ s,
+                                 const float* __restrict__ rs, const float* __restrict__ drs, float* __restrict__ dy) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t m = idx[i];
+  const float4 v = reinterpret_cast<const float4*>(y)[i];
+  const float4 mix = reinterpret_cast<const float4*>(rs)[m];
+  const float4 g = reinterpret_cast<const float4*>(drs)[m];
+  const float w = W[m * K + k];
+  const bool live = s[m] >= 1e-12f;  // clamp_min(1e-12) passes the gradient only above the bound
+  const float sn = fmaxf(s[m], 1e-12f);
+  // rgb_mix = sum_k w_k sig_k c_k / sn ; sigma_mix = sn
+  const float dc = w * v.w / sn;
+  float dsig = (live ? g.w : 0.f) * w;
+  const float gdot = g.x * (v.x - (live ? mix.x : 0.f)) + g.y * (v.y - (live ? mix.y : 0.f)) +
+                     g.z * (v.z - (live ? mix.z : 0.f));
+  dsig += w * gdot / sn;
+  reinterpret_cast<float4*>(dy)[i] = make_float4(dc * g.x, dc * g.y, dc * g.z, dsig);
+}
+
+}  // namespace
+
+extern "C" int nerf_rays_aabb_hit(const float* rays, int64_t N, const float* box, int32_t* hit, hipStream_t st) {
+  if (N < 0 || !box) return NERF_E_ARG;
+  if (N == 0) return NERF_OK;
+  if (!rays || !hit) return NERF_E_ARG;
+  rays_aabb_hit_kernel<<<(unsigned)nerf_cdiv(N, 256), 256, 0, st>>>(rays, N, box[0], box[1], box[2], box[3], box[4],
+                                                                    box[5], hit);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_flag_compact(const int32_t* flags, const int32_t* pos, int64_t n, int32_t* idx, hipStream_t st) {
+  if (n < 0) return NERF_E_ARG;
+  if (n == 0) return NERF_OK;
+  if (!flags || !pos || !idx) return NERF_E_ARG;
+  flag_compact_kernel<<<(unsigned)nerf_cdiv(n, 256), 256, 0, st>>>(flags, pos, n, idx);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_scatter_counts(const int32_t* hit_idx, const int32_t* counts_k, int64_t n, int32_t* counts,
+                                   hipStream_t st) {
+  if (n < 0) return NERF_E_ARG;
+  if (n == 0) return NERF_OK;
+  if (!hit_idx || !counts_k || !counts) return NERF_E_ARG;
+  scatter_counts_kernel<<<(unsigned)nerf_cdiv(n, 256), 256, 0, st>>>(hit_idx, counts_k, n, counts);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_segments_union(const float* const* t0s, const float* const* t1s, const int32_t* const* offs, int K,
+                                   int64_t N, int32_t* counts, const int32_t* out_off, int32_t* ray_idx, float* t0,
+                                   float* t1, hipStream_t st) {
+  if (K < 1 || K > 8 || N < 0 || !t0s || !t1s || !offs) return NERF_E_ARG;
+  if (N == 0) return NERF_OK;
+  if (!out_off && !counts) return NERF_E_ARG;
+  ExpertLists E{};
+  for (int k = 0; k < K; ++k) { E.t0[k] = t0s[k]; E.t1[k] = t1s[k]; E.off[k] = offs[k]; }
+  union_kernel<<<(unsigned)nerf_cdiv(N, 128), 128, 0, st>>>(E, K, N, counts, out_off, ray_idx, t0, t1);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_moe_blend(const float* y, int64_t n, const int32_t* idx, const float* weights, int K, int k,
+                              float* s_acc, float* c_acc, hipStream_t st) {
+  if (n < 0 || K < 1 || k < 0 || k >= K) return NERF_E_ARG;
+  if (n == 0) return NERF_OK;
+  if (!y || !idx || !weights || !s_acc || !c_acc) return NERF_E_ARG;
+  blend_kernel<<<(unsigned)nerf_cdiv(n, 256), 256, 0, st>>>(y, n, idx, weights, K, k, s_acc, c_acc);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_moe_blend_finish(const float* s_acc, const float* c_acc, int64_t M, float* rgb_sigma,
+                                     hipStream_t st) {
+  if (M < 0) return NERF_E_ARG;
+  if (M == 0) return NERF_OK;
+  if (!s_acc || !c_acc || !rgb_sigma) return NERF_E_ARG;
+  blend_finish_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(s_acc, c_acc, M, rgb_sigma);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_moe_blend_bwd(const float* y, int64_t n, const int32_t* idx, const float* weights, int K, int k,
+                                  const float* s_acc, const float* rgb_sigma, const float* d_rgb_sigma, float* d_y,
+                                  hipStream_t st) {
+  if (n < 0 || K < 1 || k < 0 || k >= K) return NERF_E_ARG;
+  if (n == 0) return NERF_OK;
+  if (!y || !idx || !weights || !s_acc || !rgb_sigma || !d_rgb_sigma || !d_y) return NERF_E_ARG;
+  blend_bwd_kernel<<<(unsigned)nerf_cdiv(n, 256), 256, 0, st>>>(y, n, idx, weights, K, k, s_acc, rgb_sigma,
+                                                                d_rgb_sigma, d_y);
+  return nerf_launch_status();
+}

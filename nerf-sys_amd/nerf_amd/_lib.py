@@ -79,6 +79,13 @@ def lib():
             "nerf_occ_mark_invisible": [P, P, P, I, I, I, F, P, P],
             "nerf_ray_counts": [P, I64, I64, P, P],
             "nerf_packed_points": [P, P, P, P, I64, P, P],
+            "nerf_rays_aabb_hit": [P, I64, P, P, P],
+            "nerf_flag_compact": [P, P, I64, P, P],
+            "nerf_scatter_counts": [P, P, I64, P, P],
+            "nerf_segments_union": [P, P, P, I, I64, P, P, P, P, P, P],
+            "nerf_moe_blend": [P, I64, P, P, I, I, P, P, P],
+            "nerf_moe_blend_finish": [P, P, I64, P, P],
+            "nerf_moe_blend_bwd": [P, I64, P, P, I, I, P, P, P, P, P],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -109,7 +116,8 @@ EXPORTS = ("nerf_rays_gen", "nerf_pick_pixels", "nerf_clamp_near_far", "nerf_ray
            "nerf_occ_march", "nerf_scan_workspace_bytes", "nerf_exclusive_scan_i32", "nerf_packed_composite_fwd",
            "nerf_packed_composite_bwd", "nerf_packed_visibility", "nerf_packed_compact", "nerf_occ_cell_points",
            "nerf_occ_update", "nerf_occ_threshold", "nerf_occ_binarize", "nerf_occ_mark_invisible", "nerf_ray_counts",
-           "nerf_packed_points")
+           "nerf_packed_points", "nerf_rays_aabb_hit", "nerf_flag_compact", "nerf_scatter_counts", "nerf_segments_union",
+           "nerf_moe_blend", "nerf_moe_blend_finish", "nerf_moe_blend_bwd")
 
 
 def check(status: int, what: str) -> None:

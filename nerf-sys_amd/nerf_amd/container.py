@@ -11,8 +11,9 @@ fast-weights surface.  Compute per call:
   backward: nerf_moe_combine_bwd per expert (routing is no-grad in the reference too).
   background_color: nerf_bg_mlp_fwd / nerf_bg_mlp_bwd (SH + 2-layer MLP fused, one thread per ray).
 
-Not mirrored: the occupancy-grid methods (premark / update / occ_ready) and the
-``density`` / ``color`` split queries used only by the occupancy renderer; ``bg_encoding="fourier"``
+Occupancy rendering of the whole container (``render_container_occ``, SURVEY §8f rows 2+3) runs on the HIP
+kernels: per-expert AABB prefilter + marching, per-ray segment union on the GPU, soft sigma/rgb blend, one
+packed integration.  Not mirrored: the ``density`` / ``color`` split queries; ``bg_encoding="fourier"``
 fails in the reference's constructor (FrequencyEncoder without in_dim) and raises here.
 """
 from __future__ import annotations
@@ -127,6 +128,122 @@ class _BgFn(torch.autograd.Function):
         return None, dw, None
 
 
+class _BlendFn(torch.autograd.Function):
+    """sigma / rgb of the routed experts blended BEFORE integration (ray_rendering.py:441-471)."""
+
+    @staticmethod
+    def forward(ctx, W, M, sels, ks, *ys):
+        s = torch.zeros(M, dtype=torch.float32, device=W.device)
+        c = torch.zeros((M, 3), dtype=torch.float32, device=W.device)
+        K = W.shape[1]
+        ys = [y.contiguous().float() for y in ys]
+        for k, sel, y in zip(ks, sels, ys):
+            check(lib().nerf_moe_blend(ptr(y), y.shape[0], ptr(sel), ptr(W), K, k, ptr(s), ptr(c), stream()),
+                  "nerf_moe_blend")
+        rs = torch.empty((M, 4), dtype=torch.float32, device=W.device)
+        check(lib().nerf_moe_blend_finish(ptr(s), ptr(c), M, ptr(rs), stream()), "nerf_moe_blend_finish")
+        ctx.save_for_backward(W, s, rs, *sels, *ys)
+        ctx.ks, ctx.n = ks, len(ks)
+        return rs
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g):
+        W, s, rs, *rest = ctx.saved_tensors
+        sels, ys = rest[:ctx.n], rest[ctx.n:]
+        g = g.contiguous().float()
+        K = W.shape[1]
+        grads = []
+        for k, sel, y in zip(ctx.ks, sels, ys):
+            dy = torch.empty_like(y)
+            check(lib().nerf_moe_blend_bwd(ptr(y), y.shape[0], ptr(sel), ptr(W), K, k, ptr(s), ptr(rs), ptr(g), ptr(dy),
+                                           stream()), "nerf_moe_blend_bwd")
+            grads.append(dy)
+        return (None, None, None, None, *grads)
+
+
+def render_container_occ(model, rays, *, params=None, bg_color_default="white", chunk=1_000_000,
+                         render_step_size=None, alpha_thre=None, cone_angle=None):
+    """render_rays_occ for the full container (nerfs/ray_rendering.py:384-481): per-expert AABB prefilter and
+    occupancy marching, per-ray union of the experts' segments (GPU; a per-ray Python loop in the reference),
+    routing at the segment midpoints, experts evaluated only where their weight > 1e-8, sigma / rgb blended
+    before ONE packed integration.  Returns rgb (N,3), depth (N,), weights (M,1), acc (N,)."""
+    from . import kernels as K_
+    from .occupancy import exclusive_scan, render_packed
+    from .ray_rendering import _get_bg_rgb
+    rays = rays.contiguous().float()
+    N = rays.shape[0]
+    dev = rays.device
+    d = rays[:, 3:6]
+    K = len(model.submodules)
+    sub_params = ([model.get_subdict(params, f"submodules.{k}") for k in range(K)] if params is not None
+                  else [None] * K)
+    keep = []  # (t0_k, t1_k, global offsets)
+    for k, ex in enumerate(model.submodules):
+        box = (ctypes.c_float * 6)(*[float(v) for v in ex._aabb_host])
+        hit = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
+        check(lib().nerf_rays_aabb_hit(ptr(rays), N, box, ptr(hit), stream()), "nerf_rays_aabb_hit")
+        pos = exclusive_scan(hit[:N])
+        nh = int(pos[-1].item())
+        if nh == 0:
+            continue
+        hit_idx = torch.empty(nh, dtype=torch.int32, device=dev)
+        check(lib().nerf_flag_compact(ptr(hit), ptr(pos), N, ptr(hit_idx), stream()), "nerf_flag_compact")
+        rays_k = gather_rows(rays, hit_idx, 8)
+        _, t0_k, t1_k, offs_k = ex.occupancy_marching_packed(rays_k, params=sub_params[k],
+                                                             render_step_size=render_step_size,
+                                                             alpha_thre=alpha_thre, cone_angle=cone_angle)
+        if t0_k.numel() == 0:
+            continue
+        cnt_k = (offs_k[1:] - offs_k[:-1]).contiguous()
+        cnt = torch.zeros(max(N, 1), dtype=torch.int32, device=dev)
+        check(lib().nerf_scatter_counts(ptr(hit_idx), ptr(cnt_k), nh, ptr(cnt), stream()), "nerf_scatter_counts")
+        keep.append((t0_k, t1_k, exclusive_scan(cnt[:N])))
+    if not keep:
+        acc = rays.new_zeros(N)
+        bg_rgb = _get_bg_rgb(model, d, params, rays, N, bg_color_default)
+        return bg_rgb, acc.clone(), torch.zeros(1, 1, device=dev, dtype=rays.dtype), acc
+    if len(keep) > 8:
+        raise ValueError("segment union supports at most 8 experts")
+    t0s = (ctypes.c_void_p * len(keep))(*[t[0].data_ptr() for t in keep])
+    t1s = (ctypes.c_void_p * len(keep))(*[t[1].data_ptr() for t in keep])
+    ofs = (ctypes.c_void_p * len(keep))(*[t[2].data_ptr() for t in keep])
+    L = lib()
+    cnt = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
+    check(L.nerf_segments_union(t0s, t1s, ofs, len(keep), N, ptr(cnt), None, None, None, None, stream()),
+          "nerf_segments_union(count)")
+    moff = exclusive_scan(cnt[:N])
+    M = int(moff[-1].item())
+    if M == 0:
+        acc = rays.new_zeros(N)
+        bg_rgb = _get_bg_rgb(model, d, params, rays, N, bg_color_default)
+        return bg_rgb, acc.clone(), torch.zeros(1, 1, device=dev, dtype=rays.dtype), acc
+    ri = torch.empty(M, dtype=torch.int32, device=dev)
+    t0 = torch.empty(M, dtype=torch.float32, device=dev)
+    t1 = torch.empty(M, dtype=torch.float32, device=dev)
+    check(L.nerf_segments_union(t0s, t1s, ofs, len(keep), N, None, ptr(moff), ptr(ri), ptr(t0), ptr(t1), stream()),
+          "nerf_segments_union(write)")
+    xm = K_.packed_points(rays, ri, t0, t1)
+    with torch.no_grad():
+        W = moe_route(xm, model._cent_host, model.boundary_margin, model.cluster_2d)
+        offs, idx = moe_dispatch(W, 1e-8)
+    ks, sels, ys = [], [], []
+    for k, sub in enumerate(model.submodules):
+        n_k = offs[k + 1] - offs[k]
+        if n_k == 0:
+            continue
+        sel = idx[offs[k]:offs[k + 1]]
+        xk = gather_rows(xm, sel, 6)
+        yk = torch.cat([sub(xk[s:s + chunk], params=sub_params[k]) for s in range(0, n_k, chunk)], 0)
+        ks.append(k)
+        sels.append(sel)
+        ys.append(yk)
+    rs = _BlendFn.apply(W, M, sels, ks, *ys)
+    bg = _get_bg_rgb(model, d, params, rays, N, bg_color_default)
+    rgb, depth, w, acc = render_packed(rs, t0, t1, moff, bg)
+    return rgb, depth, w[:, None], acc
+
+
 # ------------------------------------------------------------------ the container
 
 
@@ -227,8 +344,14 @@ class MetaContainer(nn.Module):
         return all(getattr(sub, "occ_ready", False) for sub in self.submodules)
 
     def maybe_update_expert_occupancies(self, step: int, params=None) -> None:
-        if self.use_occ:
-            raise NotImplementedError("occupancy grids are SURVEY §8f row 2 (not built)")
+        """meta_container.py:368-372."""
+        for k, sub in enumerate(self.submodules):
+            sub.maybe_update_occ_grid(step, self.get_subdict(params, f"submodules.{k}") if params is not None
+                                      else None)
+
+    def freeze_expert_occupancies(self, flag: bool) -> None:
+        for sub in self.submodules:
+            sub.occ_frozen = flag
 
     # ---- MetaModule surface
     def meta_named_parameters(self, prefix: str = "", recurse: bool = True):

@@ -191,13 +191,15 @@ def render_expert_occ(model, rays: Tensor, *, params=None, bg_color_default: str
 
 def render_rays_occ(model, rays: Tensor, *, params=None, active_module: Optional[int] = None, **kwargs):
     """ray_rendering.py:349-481.  Single experts (and a container with active_module) render through
-    render_expert_occ; the full-container soft-MoE union path is not built yet."""
+    render_expert_occ; a full container through render_container_occ (segment union + soft blend)."""
     if active_module is not None:
         return render_expert_occ(model.submodules[active_module], rays, params=params, **kwargs)
     if getattr(model, "occ_grid", None) is not None:
         return render_expert_occ(model, rays, params=params, **kwargs)
-    raise NotImplementedError("occupancy rendering of a full MoE container (segment union + soft mix) is not "
-                              "built yet; pass active_module=k or use_occ=False")
+    from .container import render_container_occ
+    return render_container_occ(model, rays, params=params, **{k: v for k, v in kwargs.items()
+                                                               if k in ("bg_color_default", "chunk", "render_step_size",
+                                                                        "alpha_thre", "cone_angle")})
 
 
 def render_rays(model, rays, *args, **kwargs):

@@ -124,3 +124,139 @@ def test_container_render_rays(z):
                         training=False, bg=bg)
     for a, b, what in ((rgb, ref[0], "rgb"), (depth, ref[1], "depth"), (w, ref[2], "weights"), (acc, ref[3], "acc")):
         assert _err(a, b) <= 1e-4 * max(1.0, b.abs().max().item()), what
+
+
+def _occ_container(z, seed=0):
+    from nerf_amd.container import MetaContainer
+    from nerf_amd.ray_sampling import SceneBox
+    torch.manual_seed(seed)
+    occ = {"use_occ": True, "resolution": 16, "levels": 2, "occ_ready": True, "near_plane": 0.05}
+    mc = MetaContainer(num_submodules=K, centroids=z["centroids"], aabb=torch.tensor([[-1.5] * 3, [1.5] * 3]),
+                       nerf_variant="instant", boundary_margin=1.05, cluster_2d=True, use_bg_nerf=True, bg_hidden=32,
+                       occ_conf=occ, expert_box_list=[SceneBox(aabb=z[f"box{k}"]) for k in range(K)], **KW)
+    state = {k[len("soft_w/"):]: v for k, v in z.items() if k.startswith("soft_w/")}
+    mc.load_reference_state(state).to(DEV).eval()
+    g = torch.Generator().manual_seed(seed + 1)
+    for sub in mc.submodules:
+        sub.occ_grid.binaries.copy_((torch.rand(sub.occ_grid.binaries.shape, generator=g) < 0.5).to(torch.uint8).to(DEV))
+    return mc
+
+
+def _capture_packed(fn):
+    """Run fn() capturing the inputs of occupancy.render_packed (the merged packed segments)."""
+    import nerf_amd.occupancy as occmod
+    cap = {}
+    orig = occmod.render_packed
+
+    def spy(rs, t0, t1, offs, bg=None):
+        cap.update(rs=rs.detach().cpu(), t0=t0.cpu(), t1=t1.cpu(), offs=offs.cpu(), bg=bg.detach().cpu())
+        return orig(rs, t0, t1, offs, bg)
+
+    occmod.render_packed = spy
+    try:
+        out = fn()
+    finally:
+        occmod.render_packed = orig
+    return out, cap
+
+
+def _occ_rays(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    o = torch.tensor([0.1, -3.0, 0.3]).expand(n, 3)
+    d = torch.nn.functional.normalize(torch.randn(n, 3, generator=g) * 0.4 + torch.tensor([0.0, 1.0, 0.0]), dim=-1)
+    return torch.cat([o, d, torch.full((n, 1), 0.5), torch.full((n, 1), 6.0)], -1).to(DEV)
+
+
+def test_segments_union_vs_torch_unique(z):
+    """The GPU per-ray union of the experts' segments equals _merge_segments_union (torch.unique per ray,
+    nerfs/ray_rendering.py:193-258) applied to the same per-expert segments — exactly."""
+    from nerf_amd import container as C
+    mc = _occ_container(z)
+    n = 96
+    rays = _occ_rays(n, 3)
+    (rgb, depth, w, acc), cap = _capture_packed(lambda: C.render_container_occ(mc, rays))
+    per_ri, per_t0, per_t1 = [], [], []
+    r = rays.cpu()
+    for ex in mc.submodules:
+        lo, hi = torch.tensor(ex._aabb_host[:3]), torch.tensor(ex._aabb_host[3:])
+        inv = torch.where(r[:, 3:6].abs() > 1e-9, 1.0 / r[:, 3:6], torch.full_like(r[:, 3:6], 1e9))
+        ta, tb = (lo - r[:, :3]) * inv, (hi - r[:, :3]) * inv
+        hit = torch.minimum(torch.maximum(ta, tb).amin(-1), r[:, 7]) > torch.maximum(torch.minimum(ta, tb).amax(-1),
+                                                                                     r[:, 6])
+        hidx = hit.nonzero().squeeze(1)
+        if hidx.numel() == 0:
+            continue
+        ri, t0, t1, _ = ex.occupancy_marching_packed(rays[hidx.to(DEV)])
+        per_ri.append(hidx[ri.cpu().long()])
+        per_t0.append(t0.cpu())
+        per_t1.append(t1.cpu())
+    ri, t0, t1 = torch.cat(per_ri), torch.cat(per_t0), torch.cat(per_t1)
+    ref0, ref1 = [], []
+    for ray in range(n):
+        sel = ri == ray
+        if sel.any():
+            b = torch.unique(torch.cat([t0[sel], t1[sel]]), sorted=True)
+            ref0.append(b[:-1])
+            ref1.append(b[1:])
+    assert torch.equal(cap["t0"], torch.cat(ref0)) and torch.equal(cap["t1"], torch.cat(ref1))
+    assert torch.isfinite(rgb).all() and float(acc.max()) <= 1.0 + 1e-5
+
+
+def test_container_occ_render_vs_oracle(z):
+    """Full-container occupancy rendering (eval: no jitter / filtering) vs the oracle chain on the SAME merged
+    segments: route at midpoints, evaluate the routed experts, blend sigma/rgb before the packed integration
+    (ray_rendering.py:441-481)."""
+    from nerf_amd.ray_rendering import render_rays
+    from oracle import occ_oracle as OO
+    mc = _occ_container(z, 5)
+    n = 64
+    rays = _occ_rays(n, 6)
+    (rgb, depth, w, acc), cap = _capture_packed(lambda: render_rays(mc, rays, ray_samples=64))
+    p = {k[len("soft_w/"):]: v for k, v in z.items() if k.startswith("soft_w/")}
+    res, _ = NO.hash_resolutions(4, 8, 128)
+    exps = []
+    for k in range(K):
+        pre = f"submodules.{k}."
+        pk = OrderedDict((nm[len(pre):], v) for nm, v in p.items() if nm.startswith(pre))
+        tb = pk.pop("xyz_encoder.hash_table")
+        exps.append(lambda x_d, pk=pk, tb=tb, box=z[f"box{k}"]: NO.ngp_forward(pk, tb, x_d, box, res, 10, 2,
+                                                                               sigma_depth=1, color_depth=1))
+    offs = cap["offs"].long()
+    ri = torch.repeat_interleave(torch.arange(n), offs[1:] - offs[:-1])
+    t0, t1 = cap["t0"], cap["t1"]
+    r = rays.cpu()
+    tm = 0.5 * (t0 + t1)
+    xm = torch.cat([r[ri, :3] + r[ri, 3:6] * tm[:, None], r[ri, 3:6]], -1)
+    Wt, _ = MO.routing(xm[:, :3], z["centroids"], 1.05, True)
+    SIG = torch.zeros(xm.shape[0], K)
+    RGB = torch.zeros(xm.shape[0], K, 3)
+    for k in range(K):
+        sel = (Wt[:, k] > 1e-8).nonzero().squeeze(1)
+        if sel.numel():
+            y = exps[k](xm[sel])
+            SIG[sel, k] = y[:, 3]
+            RGB[sel, k] = y[:, :3]
+    s_num = (Wt * SIG).sum(1, keepdim=True).clamp_min(1e-12)
+    rgb_mix = (Wt[..., None] * SIG[..., None] * RGB).sum(1) / s_num
+    rs_ref = torch.cat([rgb_mix, s_num], -1)
+    assert _err(cap["rs"], rs_ref) <= 1e-4 * max(1.0, rs_ref.abs().max().item())
+    ref = OO.render_packed(rs_ref, t0, t1, ri, n, cap["bg"])
+    for a, b, what in ((rgb, ref[0], "rgb"), (depth, ref[1], "depth"), (acc, ref[3], "acc")):
+        assert _err(a, b) <= 1e-4 * max(1.0, b.abs().max().item()), what
+
+
+def test_container_occ_training_gradients(z):
+    """Training-mode container occupancy rendering: finite, non-zero gradients for every expert's MLP and
+    hash table and the background MLP."""
+    mc = _occ_container(z, 7).train()
+    from nerf_amd.ray_rendering import render_rays
+    rays = _occ_rays(128, 8)
+    rgb, depth, w, acc = render_rays(mc, rays, ray_samples=64)
+    ((rgb - 0.3) ** 2).mean().backward()
+    for n_, p in mc.named_parameters():
+        if p.grad is None:
+            continue
+        assert torch.isfinite(p.grad).all(), n_
+    assert float(mc.bg_mlp[0].weight.grad.abs().sum()) > 0
+    assert sum(float(s.xyz_encoder.hash_table.grad.abs().sum()) > 0 for s in mc.submodules
+               if s.xyz_encoder.hash_table.grad is not None) >= 1
