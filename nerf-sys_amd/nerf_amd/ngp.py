@@ -53,6 +53,38 @@ def _addr(s):
     return ctypes.c_void_p(ctypes.addressof(s))
 
 
+class _Timing:
+    """Optional HIP-event timing of the expert's launches on the current stream (benches): no host sync."""
+
+    def __init__(self):
+        self.enabled = False
+        self.records = []
+
+    def start(self, name, rows=0):
+        if not self.enabled:
+            return None
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return (name, e0, e1, rows)
+
+    def stop(self, h):
+        if h is not None:
+            h[2].record()
+            self.records.append(h)
+
+    def collect(self):
+        """-> {name: [(ms, rows) per launch]}"""
+        torch.cuda.synchronize()
+        out = {}
+        for name, e0, e1, rows in self.records:
+            out.setdefault(name, []).append((e0.elapsed_time(e1), rows))
+        self.records = []
+        return out
+
+
+TIMING = _Timing()
+
+
 # ------------------------------------------------------------------------------------------ kernel wrappers
 
 def hash_encode(grid: NerfHashGrid, table, x, aabb=None, enc_eps=1e-6, out_stride=None):
@@ -282,8 +314,12 @@ class _NgpFn(torch.autograd.Function):
     def forward(ctx, x_d, table, w_packed, model):
         x_d = x_d.contiguous().float()
         M = x_d.shape[0]
+        h = TIMING.start("hash_fwd", M)
         enc = hash_encode(model.xyz_encoder.grid, table.detach(), x_d, model._aabb_host, model._eps)
+        TIMING.stop(h)
+        h = TIMING.start("mlp_fwd", M)
         out = ngp_fwd(model.net_struct, w_packed, enc, x_d) if M else x_d.new_empty((0, 4))
+        TIMING.stop(h)
         ctx.model = model
         ctx.rows = table.shape[0]
         ctx.save_for_backward(x_d, enc, w_packed)
@@ -299,10 +335,14 @@ class _NgpFn(torch.autograd.Function):
         g = g.contiguous().float()
         if x_d.shape[0] == 0:
             return None, torch.zeros_like(model.xyz_encoder.hash_table), torch.zeros_like(w_packed), None
+        h = TIMING.start("mlp_bwd", x_d.shape[0])
         d_enc, d_w = ngp_bwd(model.net_struct, w_packed, enc, x_d, g)
+        TIMING.stop(h)
         d_table = None
         if ctx.needs_input_grad[1]:
+            h = TIMING.start("hash_bwd", x_d.shape[0])
             d_table = hash_encode_bwd(model.xyz_encoder.grid, x_d, d_enc, ctx.rows, model._aabb_host, model._eps)
+            TIMING.stop(h)
         return None, d_table, d_w, None
 
 

@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Bench of the reference's PRODUCTION train step (SURVEY.md §8f rows 1-3 together — not the headline metric
+of bench.py): a MetaContainer of 4 Instant-NGP experts (nerf_runner.py:103-170 defaults: 16 levels x F=2,
+2^20 entries/level, max_res 4096, sigma 2x64, colour 2x64, SH dirs; soft routing, boundary margin 1.05 on
+(y,z); background MLP 32 wide) with occupancy-grid rendering (128^3 x 4 levels per expert, cone 0.004,
+alpha_thre 1e-2, updates every 16 steps), through the reference's online train loop
+(pipelines/online_stage/runtime_adapt.py:286-310): render_rays -> MSE (linear) -> backward ->
+clip_grad_norm_(1.0) -> Adam with the encoding / sigma / color / background groups (common/args.py:115-119).
+Every op is a HIP kernel reached through autograd; the optimiser is FlatAdam (nerf_adam on flat buffers).
+
+Prints one JSON line: rays/s, ms/step, per-kernel-class times (HIP events), the dominant kernel's HBM
+roofline and a CPU baseline (the oracle's stratified NGP container step on a bounded sample).
+
+  python tools/bench_container.py [--steps 20] [--warmup 40] [--batch 4096]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from types import SimpleNamespace
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "nerf-sys_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+KW = dict(hidden=64, sigma_depth=2, color_hidden=64, color_depth=2, dir_encoding="spherical",
+          hash_enc_conf=dict(levels=16, features_per_level=2, log2_hashmap_size=20, min_res=16, max_res=4096,
+                             interpolation="Linear"))
+
+
+def boxes_and_centroids():
+    # 4 experts: the (y, z) quadrants of the [-1.5, 1.5]^3 scene box, overlapping by 0.1 (cluster_2d)
+    b, c = [], []
+    for sy in (-1, 1):
+        for sz in (-1, 1):
+            lo = torch.tensor([-1.5, -1.5 if sy < 0 else -0.1, -1.5 if sz < 0 else -0.1])
+            hi = torch.tensor([1.5, 0.1 if sy < 0 else 1.5, 0.1 if sz < 0 else 1.5])
+            b.append(torch.stack([lo, hi]))
+            c.append([0.0, 0.75 * sy, 0.75 * sz])
+    return b, torch.tensor(c)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=40, help="untimed steps; the occupancy warm-up is half of them")
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--train-views", type=int, default=100)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds):
+    """The oracle's container step (stratified, 96 samples; the occupancy marcher has no CPU reference) on
+    16-ray batches: routing + 4 NGP experts + background MLP + volume render + MSE + clip + Adam."""
+    from collections import OrderedDict
+    from oracle import moe_oracle as MO
+    from oracle import nerf_oracle as O
+    from oracle import ngp_oracle as NO
+    torch.manual_seed(0)
+    hc = KW["hash_enc_conf"]
+    L, F, log2T = hc["levels"], hc["features_per_level"], hc["log2_hashmap_size"]
+    res, _ = NO.hash_resolutions(L, hc["min_res"], hc["max_res"])
+    boxes, cents = boxes_and_centroids()
+    experts, leaves = [], []
+    for b in boxes:
+        p = OrderedDict((k, (torch.randn(s) * 0.1).requires_grad_(True))
+                        for k, s in NO.ngp_param_shapes(L * F, 64, 2, 15, 64, 2, 16).items())
+        t = ((torch.rand(L * 2 ** log2T, F) * 2 - 1) * 1e-3).requires_grad_(True)
+        experts.append(lambda x_d, p=p, t=t, b=b: NO.ngp_forward(p, t, x_d, b, res, log2T, F, sigma_depth=2,
+                                                                 color_depth=2))
+        leaves += [t] + list(p.values())
+    bgw = [(torch.randn(32, 16) * 0.1).requires_grad_(True), torch.zeros(32, requires_grad=True),
+           (torch.randn(3, 32) * 0.1).requires_grad_(True), torch.zeros(3, requires_grad=True)]
+    opt = torch.optim.Adam(leaves + bgw, lr=2e-3)
+    n = 16
+    g = torch.Generator().manual_seed(0)
+    o = torch.tensor([0.0, -4.0311, 0.5]).expand(n, 3)
+    d = torch.nn.functional.normalize(torch.randn(n, 3, generator=g) * 0.15 + torch.tensor([0.0, 1.0, -0.12]), dim=-1)
+    rays = torch.cat([o, d, torch.full((n, 1), 2.0), torch.full((n, 1), 6.0)], -1)
+    gt = torch.rand(n, 3, generator=g)
+
+    def step():
+        bg = MO.background_color(d, *bgw)
+        rgb = O.render_rays(lambda x_d: MO.container_forward(experts, x_d, cents, 1.05, True), rays, 96,
+                            training=True, bg=bg)[0]
+        loss = O.mse_loss(rgb, gt, "linear")
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(leaves + bgw, 1.0)
+        opt.step()
+
+    step()
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        step()
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or (steps >= 2 and el / steps * (steps + 1) > seconds * 1.5):
+            break
+    return {"value": round(n * steps / el, 2), "unit": "rays/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{steps} oracle container steps x {n} rays (stratified 96 samples, 4 NGP experts, fp32) "
+                      f"in {el:.1f}s"}
+
+
+def main():
+    a = parse()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    from nerf_amd import ngp as G
+    from nerf_amd.container import MetaContainer
+    from nerf_amd.losses import compute_mse_loss
+    from nerf_amd.optim import FlatAdam
+    from nerf_amd.ray_sampling import SceneBox
+    from nerf_amd.scene import make_blender_scene
+    from nerf_amd.trainer import RayBatcher
+
+    torch.manual_seed(0)
+    scene = make_blender_scene(n_train=a.train_views, n_test=1, H=800, W=800, seed=0, device=dev)
+    boxes, cents = boxes_and_centroids()
+    occ = {"use_occ": True, "resolution": 128, "levels": 4, "render_step_size": None, "occ_thre": 1e-2,
+           "alpha_thre": 1e-2, "alpha_thre_start": 0.0, "alpha_thre_end": 1e-2, "cosine_anneal": True,
+           "warmup_steps": a.warmup // 2, "update_interval": 16, "ema_decay": 0.95, "cone_angle": 0.004,
+           "near_plane": 2.0, "far_plane": 6.0}
+    model = MetaContainer(num_submodules=4, centroids=cents, aabb=torch.tensor([[-1.5] * 3, [1.5] * 3]),
+                          nerf_variant="instant", boundary_margin=1.05, cluster_2d=True, use_bg_nerf=True,
+                          bg_hidden=32, occ_conf=occ, expert_box_list=[SceneBox(aabb=b) for b in boxes], **KW)
+    model = model.to(dev).train()
+    lr = {"encoding": 1e-2, "sigma": 2e-3, "color": 2e-3, "background": 1e-3}
+    groups = [{"params": g["params"], "lr": lr[k]} for k, g in model.get_param_groups().items()]
+    opt = FlatAdam(groups, grad_clip=1.0)
+    rb = RayBatcher(scene, dev)
+    P = SimpleNamespace(ray_samples=96, chunk_points=262_144 * 17, color_space="linear")
+
+    def one(step):
+        model.maybe_update_expert_occupancies(step)
+        rays, gt = rb.batch(a.batch, seed=step)
+        opt.zero_grad()
+        loss = compute_mse_loss(P, model, {"rays": rays, "rgbs": gt})
+        loss.backward()
+        opt.step()
+        return loss
+
+    for s in range(a.warmup):
+        loss = one(s)
+    assert model.occ_ready, "occupancy warm-up did not finish"
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(a.warmup, a.warmup + a.steps):
+        loss = one(s)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    # per-kernel-class times from HIP events in separate steps
+    G.TIMING.enabled = True
+    for s in range(a.steps):
+        one(a.warmup + a.steps + s)
+    per = G.TIMING.collect()
+    G.TIMING.enabled = False
+    ms = {k: sum(t for t, _ in v) / a.steps for k, v in per.items()}          # per step (all experts)
+    launch = {k: sum(t for t, _ in v) / len(v) for k, v in per.items()}      # per launch
+    n_launch = {k: len(v) / a.steps for k, v in per.items()}
+    rows = {k: sum(r for _, r in v) for k, v in per.items()}
+    dom = max(ms, key=ms.get)
+    # algorithmic bytes of the hash-grid kernels per sample (L=16, F=2): fwd 12 + 8*L*F*4 + L*F*4;
+    # bwd 12 + L*F*4 + 2*8*L*F*4 (atomic read-modify-write)
+    L, F = 16, 2
+    bps = {"hash_fwd": 12 + 8 * L * F * 4 + L * F * 4, "hash_bwd": 12 + L * F * 4 + 2 * 8 * L * F * 4}
+    hk = max(bps, key=lambda k: ms.get(k, 0.0))
+    tot_ms = sum(t for t, _ in per[hk])
+    ach = bps[hk] * rows[hk] / (tot_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "kernel": hk, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "bytes_per_launch": round(bps[hk] * rows[hk] / len(per[hk])), "mean_launch_ms": round(launch[hk], 4)}
+    out = {
+        "metric": "rays/sec (train step), production MoE container: 4 Instant-NGP experts + occupancy rendering "
+                  "+ background MLP (SURVEY §8f rows 1-3), 800x800 Lego-style",
+        "value": round(a.batch * a.steps / el, 1), "unit": "rays/s", "n_gpus": 1, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True, "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": "MetaContainer(4 x MetaNGP 16x2^20, 2x64 / 2x64, SH), soft routing bm 1.05, "
+                               "occupancy 128^3 x 4 levels, bg MLP 32, autograd train step + FlatAdam",
+                   "rays_per_step": a.batch},
+        "kernels_ms_per_step": {k: round(v, 4) for k, v in ms.items()},
+        "launches_per_step": {k: round(v, 2) for k, v in n_launch.items()},
+        "mean_launch_ms": {k: round(v, 4) for k, v in launch.items()},
+        "dominant": dom,
+        "roofline": roof,
+        "samples_per_step": round(rows.get("mlp_fwd", 0) / a.steps),
+        "final_loss": round(float(loss.item()), 6),
+    }
+    out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(a.cpu_seconds)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
