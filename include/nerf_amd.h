@@ -319,6 +319,8 @@ int nerf_occ_cell_points(const NerfOccGrid* grid, const int32_t* cells, int64_t 
 int nerf_occ_update(float* occs, const int32_t* cells, const float* values, int64_t n, float ema_decay,
                     hipStream_t stream);
 int nerf_occ_threshold(const float* occs, int64_t n, float occ_thre, float* thre_out, hipStream_t stream);
+/* thre_out must hold nerf_occ_threshold_floats() floats (2 results + 16-B pad + fp64 block partials). */
+int64_t nerf_occ_threshold_floats(void);
 int nerf_occ_binarize(const float* occs, int64_t n, const float* thre, uint8_t* binaries, hipStream_t stream);
 
 /* OccGridEstimator.mark_invisible_cells: cells whose centre no camera sees (K (n_cam,3,3), c2w (n_cam,3,4) RDF,

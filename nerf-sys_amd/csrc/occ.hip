@@ -317,27 +317,44 @@ __global__ void occ_update_kernel(float* __restrict__ occs, const int32_t* __res
 }
 
 // mean of the visible occupancies (occs >= 0), clamped to occ_thre -> thre[0]; also the mean over all cells ->
-// thre[1] (nerfacc caps alpha_thre at occs.mean()).  Single workgroup, fixed order: deterministic.
-__global__ void occ_thre_kernel(const float* __restrict__ occs, int64_t n, float occ_thre, float* __restrict__ thre) {
-  __shared__ double s1[256], s2[256];
-  __shared__ int64_t c1[256];
-  double a = 0.0, b = 0.0;
-  int64_t c = 0;
-  for (int64_t i = threadIdx.x; i < n; i += 256) {
+// thre[1] (nerfacc caps alpha_thre at occs.mean()).  256 blocks write fp64 partials, one block sums them in a
+// fixed order: deterministic.  (A single-workgroup version took 9 ms on 4 x 128^3 cells.)
+constexpr int THR_BLOCKS = 256;
+
+__global__ __launch_bounds__(256) void occ_thre_part_kernel(const float* __restrict__ occs, int64_t n,
+                                                            double* __restrict__ part) {
+  __shared__ double s1[256], s2[256], c1[256];
+  double a = 0.0, b = 0.0, c = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const float o = occs[i];
     b += o;
-    if (o >= 0.f) { a += o; ++c; }
+    if (o >= 0.f) { a += o; c += 1.0; }
   }
   s1[threadIdx.x] = a; s2[threadIdx.x] = b; c1[threadIdx.x] = c;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double A = 0.0, B = 0.0;
-    int64_t C = 0;
-    for (int k = 0; k < 256; ++k) { A += s1[k]; B += s2[k]; C += c1[k]; }
-    const float mean = C ? (float)(A / (double)C) : 0.f;
-    thre[0] = fminf(mean, occ_thre);
-    thre[1] = n ? (float)(B / (double)n) : 0.f;
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      s1[threadIdx.x] += s1[threadIdx.x + w];
+      s2[threadIdx.x] += s2[threadIdx.x + w];
+      c1[threadIdx.x] += c1[threadIdx.x + w];
+    }
+    __syncthreads();
   }
+  if (threadIdx.x == 0) {
+    part[3 * blockIdx.x] = s1[0];
+    part[3 * blockIdx.x + 1] = s2[0];
+    part[3 * blockIdx.x + 2] = c1[0];
+  }
+}
+
+__global__ void occ_thre_final_kernel(const double* __restrict__ part, int64_t n, float occ_thre,
+                                      float* __restrict__ thre) {
+  if (threadIdx.x != 0) return;
+  double A = 0.0, B = 0.0, C = 0.0;
+  for (int k = 0; k < THR_BLOCKS; ++k) { A += part[3 * k]; B += part[3 * k + 1]; C += part[3 * k + 2]; }
+  const float mean = C > 0.0 ? (float)(A / C) : 0.f;
+  thre[0] = fminf(mean, occ_thre);
+  thre[1] = n ? (float)(B / (double)n) : 0.f;
 }
 
 __global__ void binarize_kernel(const float* __restrict__ occs, int64_t n, const float* __restrict__ thre,
@@ -512,9 +529,15 @@ extern "C" int nerf_occ_update(float* occs, const int32_t* cells, const float* v
 
 extern "C" int nerf_occ_threshold(const float* occs, int64_t n, float occ_thre, float* thre_out, hipStream_t st) {
   if (n < 0 || !occs || !thre_out) return NERF_E_ARG;
-  occ_thre_kernel<<<1, 256, 0, st>>>(occs, n, occ_thre, thre_out);
+  // thre_out holds 2 floats followed by the caller-provided scratch of nerf_occ_threshold_scratch_floats()
+  double* part = reinterpret_cast<double*>(thre_out + 4);
+  if ((reinterpret_cast<uintptr_t>(part) & 7u) != 0) return NERF_E_ALIGN;
+  occ_thre_part_kernel<<<THR_BLOCKS, 256, 0, st>>>(occs, n, part);
+  occ_thre_final_kernel<<<1, 64, 0, st>>>(part, n, occ_thre, thre_out);
   return nerf_launch_status();
 }
+
+extern "C" int64_t nerf_occ_threshold_floats(void) { return 4 + 2 * 3 * THR_BLOCKS; }
 
 extern "C" int nerf_occ_binarize(const float* occs, int64_t n, const float* thre, uint8_t* binaries, hipStream_t st) {
   if (n < 0) return NERF_E_ARG;

@@ -127,7 +127,7 @@ class OccGridEstimator(nn.Module):
         self.register_buffer("occs", torch.zeros(self.levels * self.cells_per_lvl))
         self.register_buffer("binaries", torch.zeros(self.levels, self.resolution, self.resolution, self.resolution,
                                                      dtype=torch.uint8))
-        self.register_buffer("_thre", torch.zeros(2))
+        self.register_buffer("_thre", torch.zeros(int(lib().nerf_occ_threshold_floats())), persistent=False)
         g = NerfOccGrid()
         g.levels, g.resolution = self.levels, self.resolution
         for i, v in enumerate(roi.tolist()):

@@ -161,8 +161,10 @@ def test_ngp_production_config_render(N):
 def test_ngp_unsupported_config_raises(N):
     with pytest.raises(ValueError):
         N.InstantNGP(occ_conf={}, scene_box=torch.tensor([[0.0, 0, 0], [1, 1, 1]]), hidden=128)
-    with pytest.raises(NotImplementedError):
-        N.InstantNGP(occ_conf={"use_occ": True}, scene_box=torch.tensor([[0.0, 0, 0], [1, 1, 1]]))
+    with pytest.raises(ValueError):
+        N.InstantNGP(occ_conf={}, scene_box=torch.tensor([[0.0, 0, 0], [1, 1, -1]]))  # min >= max
+    m = N.InstantNGP(occ_conf={"use_occ": True}, scene_box=torch.tensor([[0.0, 0, 0], [1, 1, 1]]))
+    assert m.use_occ and not m.occ_ready and m.occ_grid.levels == 4 and m.occ_grid.resolution == 128
 
 
 def test_ngp_trainer_step_vs_oracle(z, N):
