@@ -178,7 +178,8 @@ int main(int argc, char** argv) {
   const double flop = 2.0 * M * N * K;
   struct V { const char* name; std::vector<float> ms; };
   std::vector<V> vs = {{"fwd relu+bits (lib)", {}}, {"dgrad bits (lib)", {}}, {"wgrad (lib)", {}},
-                       };
+                       {"fwd abl: no gload", {}}, {"fwd abl: no lds-store+bar", {}}, {"fwd abl: no C store", {}},
+                       {"fwd abl: mfma+lds-read only", {}}};
   auto run = [&](int v) {
     const int ntn = N / 128; const unsigned nb = (unsigned)((M / 128) * ntn);
     switch (v) {
@@ -186,6 +187,10 @@ int main(int argc, char** argv) {
       case 1: gemm_nt_kernel<128, 128, 2, EPI_MASK, 4><<<nb, 256>>>(A, K, B, K, bias, C, N, mb, 8, nullptr, K, ntn); break;
       case 2: { const int nt = 4; const int64_t rps = M / S;
         gemm_wgrad_kernel<128, 128, 2><<<nt * S, 256>>>(A, K, C, N, P, 256, P + 65536, slab, rps, M, 2, nt); break; }
+      case 3: gemm_abl<128, 128, 2, EPI_BIAS_RELU, 4, 16, 2, 1><<<nb, 256>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, K, ntn); break;
+      case 4: gemm_abl<128, 128, 2, EPI_BIAS_RELU, 4, 16, 2, 2><<<nb, 256>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, K, ntn); break;
+      case 5: gemm_abl<128, 128, 2, EPI_BIAS_RELU, 4, 16, 2, 4><<<nb, 256>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, K, ntn); break;
+      case 6: gemm_abl<128, 128, 2, EPI_BIAS_RELU, 4, 16, 2, 7><<<nb, 256>>>(A, K, B, K, bias, C, N, nullptr, 8, mb, K, ntn); break;
     }
   };
   for (int v = 0; v < (int)vs.size(); ++v) run(v);
