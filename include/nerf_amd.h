@@ -358,6 +358,32 @@ int nerf_moe_blend_bwd(const float* y, int64_t n, const int32_t* idx, const floa
                        const float* s_acc, const float* rgb_sigma, const float* d_rgb_sigma, float* d_y,
                        hipStream_t stream);
 
+/* ------------------------------------------------------------------ meta-learning updates (§8f row 4) */
+
+/* task_adapt's inner update (adaptive_nerf/pipelines/offline_stage/meta_core.py:61-64):
+ * out_i = w_i - lr * g_i (two rounded fp32 ops, like torch) for up to 64 fast tensors in one launch.
+ * w / g / out / numel are HOST arrays; g[i] NULL -> out_i = w_i (a parameter autograd left unused). */
+int nerf_sgd_multi(int n_tensors, const float* const* w, const float* const* g, float* const* out,
+                   const int64_t* numel, float lr, hipStream_t stream);
+
+/* reptile_meta_update (meta_core.py:145-176): per tensor t, delta = (sum_f (fast[t*n_fast+f] - theta_t)) / n_fast
+ * (summed in fast-list order) and theta_t += lr * delta, skipped when delta has a non-finite element or is all
+ * zero (the reference's per-tensor guard). theta / fast / numel are HOST arrays of device pointers / sizes;
+ * flags: device int32 workspace of nerf_reptile_workspace_bytes(n_tensors) bytes. */
+int64_t nerf_reptile_workspace_bytes(int n_tensors);
+int nerf_reptile_update(int n_tensors, float* const* theta, const float* const* fast, int n_fast,
+                        const int64_t* numel, float lr, int32_t* flags, int64_t ws_bytes, hipStream_t stream);
+
+/* ------------------------------------------------------------------ ray dataset build (§8f row 4) */
+
+/* _process_single_image (adaptive_nerf/data/ram_rays_dataset.py:46-121) after nerf_rays_gen + nerf_clamp_near_far:
+ * flags[i] = valid[i] && (mask == NULL || mask[i])  (the keep mask of :97-104 and the valid filter of :114). */
+int nerf_ray_keep_flags(const uint8_t* valid, const uint8_t* mask, int64_t n, int32_t* flags, hipStream_t stream);
+/* kept row i -> row pos[i] (pos = exclusive scan of flags) of out_rays (8 floats), out_rgb (3), out_idx
+ * (= image_index, :117). rays / out_rays 16-byte aligned. */
+int nerf_rays_compact(const float* rays, const float* rgb, const int32_t* flags, const int32_t* pos, int64_t n,
+                      int32_t image_index, float* out_rays, float* out_rgb, int32_t* out_idx, hipStream_t stream);
+
 /* Library build identification (string, static). */
 const char* nerf_version(void);
 

@@ -115,3 +115,4 @@ extern "C" int nerf_adam(float* p, const float* g, float* m, float* v, int64_t n
                                                       max_norm);
   return nerf_launch_status();
 }
+

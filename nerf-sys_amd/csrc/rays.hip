@@ -66,9 +66,9 @@ __global__ void rays_gen_kernel(const float* __restrict__ c2w, const int32_t* __
   out[1] = make_float4(d[1], d[2], tn, tf);
   if (img && rgb) {
     const uint8_t* px = img + (((int64_t)im * H + row) * W + col) * 3;
-    rgb[3 * p + 0] = px[0] * (1.0f / 255.0f);
-    rgb[3 * p + 1] = px[1] * (1.0f / 255.0f);
-    rgb[3 * p + 2] = px[2] * (1.0f / 255.0f);
+    rgb[3 * p + 0] = px[0] / 255.0f;
+    rgb[3 * p + 1] = px[1] / 255.0f;
+    rgb[3 * p + 2] = px[2] / 255.0f;
   }
 }
 

@@ -12,8 +12,9 @@ renderer), ``jaxtyping`` (scene_box.py:3, a type annotation), ``viser.transforms
 MetaNeRF's (x,d,params)->dict forward is wrapped in a 6-line adapter to the container
 contract expert(x_d (M,6), params) -> (M,4) (SURVEY.md §0 defect 2).
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--only-ngp | --only-moe]
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--only-ngp | --only-moe | --only-data | --only-meta]
 """
+import math
 import os
 import sys
 import types
@@ -203,6 +204,7 @@ def main():
                         gnorm=np.float32(gnorm.item()), lr=np.float32(2e-3), **after)
     gen_ngp()
     gen_moe()
+    gen_data()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 
@@ -340,8 +342,118 @@ def gen_moe():
     np.savez_compressed(os.path.join(OUT, "moe.npz"), **arr)
 
 
+def gen_data():
+    """Data-path fixtures: RamRaysDataset's per-image ray generation
+    (_process_single_image, data/ram_rays_dataset.py:46-121) on in-memory images: AABB near/far with misses,
+    a pixel mask, a near/far override; and one first-order task_adapt inner loop
+    (pipelines/offline_stage/meta_core.py:14-68) of MetaNeRF(frequency) on support rays."""
+    from data.ram_rays_dataset import _process_single_image     # noqa: E402
+    from nerfs.scene_box import SceneBox                        # noqa: E402
+    g = torch.Generator().manual_seed(99)
+    arr = {}
+
+    class MD:  # ImageMetadata surface used by _process_single_image (load_image / load_mask / fields)
+        def __init__(self, i, H, W, c2w, K, img, mask):
+            self.H, self.W, self.c2w, self.intrinsics, self.image_index, self.is_val = H, W, c2w, K, i, False
+            self._img, self._mask = img, mask
+
+        def load_image(self):
+            return self._img
+
+        def load_mask(self):
+            return self._mask
+
+    H, W = 24, 32
+    box = SceneBox(aabb=torch.tensor([[-1.5, -1.5, -1.5], [1.5, 1.5, 1.5]]))
+    cases = []
+    for i in range(2):
+        ang = 0.4 + 0.9 * i
+        c2w = torch.tensor([[math.cos(ang), 0.0, math.sin(ang), 4.0 * math.sin(ang)],
+                            [0.0, 1.0, 0.0, 0.3],
+                            [-math.sin(ang), 0.0, math.cos(ang), 4.0 * math.cos(ang)]])
+        K = torch.tensor([40.0, 38.0, 15.7, 12.2]) if i == 1 else torch.tensor([9.0, 8.5, 15.7, 12.2])  # d0: wide, some rays miss
+        img = torch.randint(0, 256, (H, W, 3), generator=g, dtype=torch.uint8)
+        mask = (torch.rand(H, W, generator=g) > 0.3) if i == 1 else None
+        md = MD(7 + i, H, W, c2w, K, img, mask)
+        ovr = (0.5, 4.0) if i == 1 else None
+        rgbs, rays, idx = _process_single_image(md, True, False, {"scene_box": box, "near_far_override": ovr})
+        arr[f"d{i}_c2w"], arr[f"d{i}_K"], arr[f"d{i}_img"] = c2w.numpy(), K.numpy(), img.numpy()
+        if mask is not None:
+            arr[f"d{i}_mask"] = mask.numpy()
+        arr[f"d{i}_rgbs"], arr[f"d{i}_rays"], arr[f"d{i}_idx"] = rgbs.numpy(), rays.numpy(), idx.numpy()
+    np.savez_compressed(os.path.join(OUT, "data.npz"), **arr)
+    gen_meta()
+
+
+def gen_meta():
+    """task_adapt (first-order, pipelines/offline_stage/meta_core.py:14-68) of MetaNeRF(frequency) with the
+    mlp.npz weights on 64 support rays (eval-mode t, linear colour space, white bg), then reptile_meta_update
+    (:145-176) with two fast lists, one NaN tensor and one zero-delta tensor (the per-tensor guard)."""
+    from models.inr.meta_vanilla import MetaNeRF                      # noqa: E402
+    from pipelines.offline_stage.meta_core import task_adapt, reptile_meta_update  # noqa: E402
+    z = np.load(os.path.join(OUT, "mlp.npz"))
+    zr = np.load(os.path.join(OUT, "rays.npz"))
+    net = MetaNeRF(encoding_dir="frequency")
+    with torch.no_grad():
+        for n, p in net.meta_named_parameters():
+            p.copy_(torch.from_numpy(z[f"w/{n}"]))
+
+    class Expert(torch.nn.Module):  # expert(x_d (M,6), params) -> (M,4) over MetaNeRF's own fast-weight names
+        def __init__(self, n):
+            super().__init__(); self.net = n
+
+        def forward(self, x_d, params=None):
+            o = self.net(x_d[:, :3], x_d[:, 3:6], params=params)
+            return torch.cat([o["rgb"], o["sigma"]], -1)
+
+        def meta_named_parameters(self):
+            return self.net.meta_named_parameters()
+
+    class Model(torch.nn.Module):
+        def __init__(self, e):
+            super().__init__(); self.submodules = torch.nn.ModuleList([e]); self.use_occ = False
+
+        def meta_named_parameters(self):
+            return self.submodules[0].meta_named_parameters()
+
+    model = Model(Expert(net)).eval()
+    g = torch.Generator().manual_seed(4321)
+    rays = torch.from_numpy(zr["rays_const"])[torch.randperm(10000, generator=g)[:64]].contiguous()
+    gt = torch.rand(64, 3, generator=g)
+    P = SimpleNamespace(algo="fomaml", fim=False, use_amp=False, ray_samples=32, chunk_points=1 << 20,
+                        color_space="linear", lr=0.5)
+    fast, losses = task_adapt(P, model, {"rays": rays, "rgbs": gt}, inner_lr=0.05, iterations=3, active_module=0)
+    arr = {"rays": rays.numpy(), "gt": gt.numpy(), "losses": torch.stack(losses).numpy()}
+    arr.update({f"fast/{n}": v.detach().numpy() for n, v in fast.items()})
+    # reptile: theta = the mlp.npz weights, fast_list = [task_adapt result, a second perturbed copy]
+    fast1 = OrderedDict((n, v.detach().clone()) for n, v in fast.items())
+    fast2 = OrderedDict((n, v.detach() + 0.01 * torch.randn(v.shape, generator=g)) for n, v in fast.items())
+    fast2["trunk.3.linear.bias"][5] = float("nan")                 # non-finite delta -> tensor skipped
+    theta = OrderedDict((n, p.detach().clone()) for n, p in net.meta_named_parameters())
+    fast1["geo_head.bias"] = theta["geo_head.bias"].clone()         # zero delta -> tensor skipped
+    fast2["geo_head.bias"] = theta["geo_head.bias"].clone()
+    reptile_meta_update(P, model, [fast1, fast2])
+    # stored for a subset of tensors (the fixture stays small); the guard cases are among them
+    keep = ("trunk.0.linear.weight", "trunk.3.linear.bias", "trunk.7.linear.bias", "sigma_head.weight",
+            "geo_head.bias", "color_mlp.color_out.weight", "color_mlp.color_out.bias")
+    new = dict(net.meta_named_parameters())
+    for n in keep:
+        arr[f"fast2/{n}"], arr[f"reptile/{n}"] = fast2[n].numpy(), new[n].detach().numpy()
+    np.savez_compressed(os.path.join(OUT, "meta.npz"), **arr)
+
+
 if __name__ == "__main__":
-    if "--only-ngp" in sys.argv or "--only-moe" in sys.argv:
+    if "--only-meta" in sys.argv:
+        sys.dont_write_bytecode = True
+        _install_stubs()
+        sys.path.insert(0, REF)
+        gen_meta()
+    elif "--only-data" in sys.argv:
+        sys.dont_write_bytecode = True
+        _install_stubs()
+        sys.path.insert(0, REF)
+        gen_data()
+    elif "--only-ngp" in sys.argv or "--only-moe" in sys.argv:
         sys.dont_write_bytecode = True
         _install_stubs()
         sys.path.insert(0, REF)
