@@ -287,7 +287,8 @@ int nerf_occ_march(const NerfOccGrid* grid, const uint8_t* binaries, const float
                    int max_steps, int32_t* counts, const int32_t* offsets, int32_t* ray_idx, float* t0, float* t1,
                    hipStream_t stream);
 
-/* Exclusive scan of n int32 into out[n+1] (out[n] = total). */
+/* Exclusive scan of n int32 into out[n+1] (out[n] = total); in / out 16-byte aligned. Reduce-then-scan over
+ * 2048-element tiles: 3 launches, 12 B of HBM traffic per element. */
 int64_t nerf_scan_workspace_bytes(int64_t n);
 int nerf_exclusive_scan_i32(const int32_t* in, int64_t n, int32_t* out, void* ws, int64_t ws_bytes,
                             hipStream_t stream);
@@ -376,13 +377,18 @@ int nerf_reptile_update(int n_tensors, float* const* theta, const float* const* 
 
 /* ------------------------------------------------------------------ ray dataset build (§8f row 4) */
 
-/* _process_single_image (adaptive_nerf/data/ram_rays_dataset.py:46-121) after nerf_rays_gen + nerf_clamp_near_far:
- * flags[i] = valid[i] && (mask == NULL || mask[i])  (the keep mask of :97-104 and the valid filter of :114). */
-int nerf_ray_keep_flags(const uint8_t* valid, const uint8_t* mask, int64_t n, int32_t* flags, hipStream_t stream);
-/* kept row i -> row pos[i] (pos = exclusive scan of flags) of out_rays (8 floats), out_rgb (3), out_idx
- * (= image_index, :117). rays / out_rays 16-byte aligned. */
-int nerf_rays_compact(const float* rays, const float* rgb, const int32_t* flags, const int32_t* pos, int64_t n,
-                      int32_t image_index, float* out_rays, float* out_rgb, int32_t* out_idx, hipStream_t stream);
+/* _process_single_image (adaptive_nerf/data/ram_rays_dataset.py:46-121) for n_images same-size (H x W) images in
+ * two passes around nerf_exclusive_scan_i32 (n = n_images*H*W pixels, image-major, row-major):
+ *   count pass (pos == NULL): flags[n] = keep-mask (:97-104; masks NULL = keep all) && valid after
+ *     get_rays with the AABB near/far (:88-92, max_bound = invalid = 1e10) and clamp_rays_near_far (:104-106,
+ *     has_near / has_far = the override; eps 1e-6, invalid -> inf);
+ *   write pass (pos = exclusive scan of flags, n+1 entries): kept pixel g -> row pos[g] of out_rays (8 floats,
+ *     16-byte aligned), out_rgb (3 floats, pixel / 255, :112) and out_idx (image_index[image of g], :117).
+ * c2w (n_images x 12), intrinsics (n_images x 4: fx fy cx cy), image_index (n_images), aabb (6): device. */
+int nerf_dataset_rays(const float* c2w, const float* intrinsics, const int32_t* image_index, int n_images, int H,
+                      int W, int center_pixels, const float* aabb, int has_near, float near_v, int has_far,
+                      float far_v, const uint8_t* images, const uint8_t* masks, int32_t* flags, const int32_t* pos,
+                      float* out_rays, float* out_rgb, int32_t* out_idx, hipStream_t stream);
 
 /* Library build identification (string, static). */
 const char* nerf_version(void);

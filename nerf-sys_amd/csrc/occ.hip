@@ -117,41 +117,104 @@ __global__ void march_kernel(Grid G, const uint8_t* __restrict__ bin, const floa
   if (!offsets) counts[r] = n;
 }
 
-// ---- exclusive scan of int32 (n+1 outputs): block sums -> one-thread scan of the sums -> add
-__global__ void scan_block_kernel(const int32_t* __restrict__ in, int64_t n, int32_t* __restrict__ out,
-                                  int32_t* __restrict__ bsum) {
-  __shared__ int32_t ws[4];
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int v = i < n ? in[i] : 0;
+// ---- exclusive scan of int32 (n+1 outputs): reduce-then-scan over 2048-element tiles (256 threads x 8
+// consecutive elements, 32-byte vector loads). Pass 1 writes one sum per tile, pass 2 (one 1024-thread block)
+// scans the tile sums in place and writes out[n], pass 3 re-reads each tile, scans it and adds the tile's offset.
+// HBM: 12 B per element (read twice, write once).
+constexpr int SCAN_V = 8;
+constexpr int SCAN_TILE = 256 * SCAN_V;
+
+__device__ __forceinline__ void scan_load8(const int32_t* __restrict__ in, int64_t i0, int64_t n, int v[SCAN_V]) {
+  if (i0 + SCAN_V <= n) {
+    const int4 a = *reinterpret_cast<const int4*>(in + i0);
+    const int4 b = *reinterpret_cast<const int4*>(in + i0 + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < SCAN_V; ++k) v[k] = i0 + k < n ? in[i0 + k] : 0;
+  }
+}
+
+// exclusive scan of one int per thread over a block of NW waves; *total = block sum
+template <int NW>
+__device__ __forceinline__ int block_excl_scan(int x, int* lds, int* total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int x = v;
+  int inc = x;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
+    const int y = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += y;
   }
-  if (lane == 63) ws[wave] = x;
+  if (lane == 63) lds[wave] = inc;
   __syncthreads();
-  int base = 0;
-  for (int k = 0; k < wave; ++k) base += ws[k];
-  if (i < n) out[i] = base + x - v;  // exclusive within the block
-  if (threadIdx.x == 255) bsum[blockIdx.x] = base + x;
-}
-
-__global__ void scan_sums_kernel(int32_t* __restrict__ bsum, int64_t nb, int32_t* __restrict__ out, int64_t n) {
-  if (threadIdx.x != 0) return;
-  int s = 0;
-  for (int64_t b = 0; b < nb; ++b) {
-    const int c = bsum[b];
-    bsum[b] = s;
-    s += c;
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const int w = lds[k];
+    base += k < wave ? w : 0;
+    tot += w;
   }
-  out[n] = s;
+  __syncthreads();
+  *total = tot;
+  return base + inc - x;
 }
 
-__global__ void scan_add_kernel(int32_t* __restrict__ out, int64_t n, const int32_t* __restrict__ bsum) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) out[i] += bsum[blockIdx.x];
+__global__ __launch_bounds__(256) void scan_reduce_kernel(const int32_t* __restrict__ in, int64_t n,
+                                                          int32_t* __restrict__ tile_sums) {
+  __shared__ int lds[4];
+  int v[SCAN_V];
+  scan_load8(in, (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_V, n, v);
+  int s = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_V; ++k) s += v[k];
+  int tot;
+  block_excl_scan<4>(s, lds, &tot);
+  if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(1024) void scan_tiles_kernel(int32_t* __restrict__ tile_sums, int64_t nb,
+                                                          int32_t* __restrict__ out, int64_t n) {
+  __shared__ int lds[16];
+  const int64_t per = (nb + 1023) / 1024;
+  const int64_t b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
+  int s = 0;
+  for (int64_t b = b0; b < b1; ++b) s += tile_sums[b];
+  int tot;
+  int run = block_excl_scan<16>(s, lds, &tot);
+  for (int64_t b = b0; b < b1; ++b) {
+    const int c = tile_sums[b];
+    tile_sums[b] = run;
+    run += c;
+  }
+  if (threadIdx.x == 0) out[n] = tot;
+}
+
+__global__ __launch_bounds__(256) void scan_down_kernel(const int32_t* __restrict__ in, int64_t n,
+                                                        const int32_t* __restrict__ tile_off,
+                                                        int32_t* __restrict__ out) {
+  __shared__ int lds[4];
+  const int64_t i0 = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_V;
+  int v[SCAN_V];
+  scan_load8(in, i0, n, v);
+  int s = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_V; ++k) s += v[k];
+  int tot;
+  int run = tile_off[blockIdx.x] + block_excl_scan<4>(s, lds, &tot);
+  int o[SCAN_V];
+#pragma unroll
+  for (int k = 0; k < SCAN_V; ++k) {
+    o[k] = run;
+    run += v[k];
+  }
+  if (i0 + SCAN_V <= n) {
+    *reinterpret_cast<int4*>(out + i0) = make_int4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<int4*>(out + i0 + 4) = make_int4(o[4], o[5], o[6], o[7]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < SCAN_V; ++k)
+      if (i0 + k < n) out[i0 + k] = o[k];
+  }
 }
 
 // ---- packed compositing: one wave per ray, 64-sample chunks with a carried exclusive sum of sigma*dt
@@ -442,7 +505,7 @@ extern "C" int nerf_occ_march(const NerfOccGrid* grid, const uint8_t* binaries, 
 
 extern "C" int64_t nerf_scan_workspace_bytes(int64_t n) {
   if (n < 0) return NERF_E_ARG;
-  return nerf_cdiv(n < 1 ? 1 : n, 256) * 4 + 256;
+  return nerf_cdiv(n < 1 ? 1 : n, SCAN_TILE) * 4 + 256;
 }
 
 extern "C" int nerf_exclusive_scan_i32(const int32_t* in, int64_t n, int32_t* out, void* ws, int64_t ws_bytes,
@@ -453,12 +516,13 @@ extern "C" int nerf_exclusive_scan_i32(const int32_t* in, int64_t n, int32_t* ou
     return nerf_launch_status();
   }
   if (!in || !ws) return NERF_E_ARG;
-  const int64_t nb = nerf_cdiv(n, 256);
+  if (((uintptr_t)in | (uintptr_t)out) & 15) return NERF_E_ALIGN;  // 16-byte vector loads / stores
+  const int64_t nb = nerf_cdiv(n, SCAN_TILE);
   if (ws_bytes < nb * 4) return NERF_E_WORKSPACE;
-  int32_t* bs = reinterpret_cast<int32_t*>(ws);
-  scan_block_kernel<<<(unsigned)nb, 256, 0, st>>>(in, n, out, bs);
-  scan_sums_kernel<<<1, 64, 0, st>>>(bs, nb, out, n);
-  scan_add_kernel<<<(unsigned)nb, 256, 0, st>>>(out, n, bs);
+  int32_t* ts = reinterpret_cast<int32_t*>(ws);
+  scan_reduce_kernel<<<(unsigned)nb, 256, 0, st>>>(in, n, ts);
+  scan_tiles_kernel<<<1, 1024, 0, st>>>(ts, nb, out, n);
+  scan_down_kernel<<<(unsigned)nb, 256, 0, st>>>(in, n, ts, out);
   return nerf_launch_status();
 }
 

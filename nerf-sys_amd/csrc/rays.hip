@@ -31,6 +31,38 @@ __device__ __forceinline__ void aabb_slab(const float o[3], const float d[3], co
   tf = tmax;
 }
 
+// One ray of get_ray_directions + get_rays (+ the AABB slab test): pixel (row, col) of the camera c2w M (3x4)
+// -> o[3], d[3], near, far. Shared by the batch / dense generator and the dataset build so both give the same bits.
+__device__ __forceinline__ void make_ray(const float* M, int row, int col, float fx, float fy, float cx, float cy,
+                                         int center, float near_v, float far_v, const float* aabb, float max_bound,
+                                         float invalid, float o[3], float d[3], float& tn, float& tf) {
+  float i = (float)col, j = (float)row;
+  if (center) { i += 0.5f; j += 0.5f; }
+  float x = (i - cx) / fx, y = -((j - cy) / fy), z = -1.0f;
+  float nrm = sqrtf(x * x + y * y + z * z);
+  nrm = fmaxf(nrm, 1e-12f);
+  x = x / nrm; y = y / nrm; z = z / nrm;
+  o[0] = M[3]; o[1] = M[7]; o[2] = M[11];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) d[r] = x * M[4 * r + 0] + y * M[4 * r + 1] + z * M[4 * r + 2];
+  tn = near_v;
+  tf = far_v;
+  if (aabb) aabb_slab(o, d, aabb, max_bound, invalid, tn, tf);
+}
+
+// clamp_rays_near_far (nerfs/ray_sampling.py:139-176) of one ray; returns valid
+__device__ __forceinline__ bool clamp_ray(float& a, float& b, int has_near, float nv, int has_far, float fv, float eps,
+                                          float invalid) {
+  if (has_near) a = fmaxf(a, nv);
+  if (has_far) b = fminf(b, fv);
+  const bool ok = isfinite(a) && isfinite(b) && (b > a + eps);
+  if (has_near || has_far) {
+    a = ok ? a : invalid;
+    b = ok ? b : invalid;
+  }
+  return ok;
+}
+
 __global__ void rays_gen_kernel(const float* __restrict__ c2w, const int32_t* __restrict__ pix, int64_t n, int H,
                                 int W, float fx, float fy, float cx, float cy, int center, float near_v,
                                 float far_v, const float* __restrict__ aabb, float max_bound, float invalid,
@@ -48,19 +80,9 @@ __global__ void rays_gen_kernel(const float* __restrict__ c2w, const int32_t* __
     row = (int)(p / W);
     col = (int)(p % W);
   }
-  float i = (float)col, j = (float)row;
-  if (center) { i += 0.5f; j += 0.5f; }
-  float x = (i - cx) / fx, y = -((j - cy) / fy), z = -1.0f;
-  float nrm = sqrtf(x * x + y * y + z * z);
-  nrm = fmaxf(nrm, 1e-12f);
-  x = x / nrm; y = y / nrm; z = z / nrm;
-  const float* M = c2w + 12 * (int64_t)im;
-  float o[3] = {M[3], M[7], M[11]};
-  float d[3];
-#pragma unroll
-  for (int r = 0; r < 3; ++r) d[r] = x * M[4 * r + 0] + y * M[4 * r + 1] + z * M[4 * r + 2];
-  float tn = near_v, tf = far_v;
-  if (aabb) aabb_slab(o, d, aabb, max_bound, invalid, tn, tf);
+  float o[3], d[3], tn, tf;
+  make_ray(c2w + 12 * (int64_t)im, row, col, fx, fy, cx, cy, center, near_v, far_v, aabb, max_bound, invalid, o, d,
+           tn, tf);
   float4* out = reinterpret_cast<float4*>(rays + 8 * p);
   out[0] = make_float4(o[0], o[1], o[2], d[0]);
   out[1] = make_float4(d[1], d[2], tn, tf);
@@ -70,6 +92,67 @@ __global__ void rays_gen_kernel(const float* __restrict__ c2w, const int32_t* __
     rgb[3 * p + 1] = px[1] / 255.0f;
     rgb[3 * p + 2] = px[2] / 255.0f;
   }
+}
+
+// RamRaysDataset build (data/ram_rays_dataset.py:46-121) for a run of same-size images, two passes around one
+// exclusive scan. Count pass (pos == NULL): flags[g] = mask && valid-after-clamp for every pixel g of the run.
+// Write pass: a pixel is kept iff pos[g+1] > pos[g]; its ray is recomputed (ALU is free here, the 44-byte
+// intermediate row is not) and written with its colour / 255 and image index at row pos[g]. HBM per pixel:
+// mask 1 B + flags 4 B (count), scan 8 B, pos 4 B + pixel 3 B + 48 B per kept row (write).
+struct DatasetArgs {
+  const float* c2w;         // n_images x 12
+  const float* intr;        // n_images x 4: fx fy cx cy
+  const int32_t* image_index;
+  int H, W, center;
+  const float* aabb;
+  int has_near, has_far;
+  float near_v, far_v;
+  const uint8_t* images;    // n_images x H x W x 3
+  const uint8_t* masks;     // n_images x H x W, or NULL
+};
+
+__device__ __forceinline__ bool dataset_ray(const DatasetArgs& A, int64_t g, int& im, float o[3], float d[3],
+                                            float& tn, float& tf) {
+  const int64_t hw = (int64_t)A.H * A.W;
+  im = (int)(g / hw);
+  const int64_t q = g - (int64_t)im * hw;
+  const int row = (int)(q / A.W), col = (int)(q - (int64_t)row * A.W);
+  const float* K = A.intr + 4 * (int64_t)im;
+  make_ray(A.c2w + 12 * (int64_t)im, row, col, K[0], K[1], K[2], K[3], A.center, 0.f, 0.f, A.aabb, 1e10f, 1e10f, o,
+           d, tn, tf);
+  return clamp_ray(tn, tf, A.has_near, A.near_v, A.has_far, A.far_v, 1e-6f, INFINITY);
+}
+
+__global__ void dataset_count_kernel(DatasetArgs A, int64_t n, int32_t* __restrict__ flags) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  int keep = 0;
+  if (A.masks == nullptr || A.masks[g]) {
+    int im;
+    float o[3], d[3], tn, tf;
+    keep = dataset_ray(A, g, im, o, d, tn, tf) ? 1 : 0;
+  }
+  flags[g] = keep;
+}
+
+__global__ void dataset_write_kernel(DatasetArgs A, int64_t n, const int32_t* __restrict__ pos,
+                                     float* __restrict__ out_rays, float* __restrict__ out_rgb,
+                                     int32_t* __restrict__ out_idx) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  const int32_t r = pos[g];
+  if (pos[g + 1] == r) return;
+  int im;
+  float o[3], d[3], tn, tf;
+  dataset_ray(A, g, im, o, d, tn, tf);
+  float4* w = reinterpret_cast<float4*>(out_rays + 8 * (int64_t)r);
+  w[0] = make_float4(o[0], o[1], o[2], d[0]);
+  w[1] = make_float4(d[1], d[2], tn, tf);
+  const uint8_t* px = A.images + 3 * g;
+  out_rgb[3 * (int64_t)r + 0] = px[0] / 255.0f;
+  out_rgb[3 * (int64_t)r + 1] = px[1] / 255.0f;
+  out_rgb[3 * (int64_t)r + 2] = px[2] / 255.0f;
+  out_idx[r] = A.image_index[im];
 }
 
 __global__ void pick_pixels_kernel(int64_t n, int n_images, int H, int W, uint64_t seed, int32_t* __restrict__ pix) {
@@ -89,12 +172,10 @@ __global__ void clamp_kernel(float* __restrict__ rays, int64_t n, int has_near, 
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
   float a = rays[8 * p + 6], b = rays[8 * p + 7];
-  if (has_near) a = fmaxf(a, nv);
-  if (has_far) b = fminf(b, fv);
-  const bool ok = isfinite(a) && isfinite(b) && (b > a + eps);
+  const bool ok = clamp_ray(a, b, has_near, nv, has_far, fv, eps, invalid);
   if (has_near || has_far) {
-    rays[8 * p + 6] = ok ? a : invalid;
-    rays[8 * p + 7] = ok ? b : invalid;
+    rays[8 * p + 6] = a;
+    rays[8 * p + 7] = b;
   }
   if (valid) valid[p] = ok ? 1 : 0;
 }
@@ -256,6 +337,28 @@ extern "C" int nerf_freq_encode(const float* x, int64_t n, int D, int L, int inc
   NERF_CHECK_ARG(ld_out >= D * (2 * L + (include_input ? 1 : 0)));
   if (n == 0) return NERF_OK;
   freq_encode_kernel<<<blocks_for(n * D, 256), 256, 0, stream>>>(x, n, D, L, include_input, out, ld_out);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_dataset_rays(const float* c2w, const float* intrinsics, const int32_t* image_index,
+                                 int n_images, int H, int W, int center_pixels, const float* aabb, int has_near,
+                                 float near_v, int has_far, float far_v, const uint8_t* images, const uint8_t* masks,
+                                 int32_t* flags, const int32_t* pos, float* out_rays, float* out_rgb,
+                                 int32_t* out_idx, hipStream_t stream) {
+  NERF_CHECK_ARG(n_images >= 0 && H > 0 && W > 0);
+  if (n_images == 0) return NERF_OK;
+  NERF_CHECK_ARG(c2w && intrinsics && image_index && aabb);
+  const int64_t n = (int64_t)n_images * H * W;
+  DatasetArgs A{c2w, intrinsics, image_index, H, W, center_pixels, aabb, has_near, has_far, near_v, far_v, images,
+                masks};
+  if (pos == nullptr) {
+    NERF_CHECK_ARG(flags);
+    dataset_count_kernel<<<blocks_for(n, 256), 256, 0, stream>>>(A, n, flags);
+  } else {
+    NERF_CHECK_ARG(images && out_rays && out_rgb && out_idx);
+    if (!nerf_aligned16(out_rays)) return NERF_E_ALIGN;
+    dataset_write_kernel<<<blocks_for(n, 256), 256, 0, stream>>>(A, n, pos, out_rays, out_rgb, out_idx);
+  }
   return nerf_launch_status();
 }
 

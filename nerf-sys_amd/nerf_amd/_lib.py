@@ -84,8 +84,7 @@ def lib():
             "nerf_sgd_multi": [I, P, P, P, P, F, P],
             "nerf_reptile_workspace_bytes": [I],
             "nerf_reptile_update": [I, P, P, I, P, F, P, I64, P],
-            "nerf_ray_keep_flags": [P, P, I64, P, P],
-            "nerf_rays_compact": [P, P, P, P, I64, I, P, P, P, P],
+            "nerf_dataset_rays": [P, P, P, I, I, I, I, P, I, F, I, F, P, P, P, P, P, P, P, P],
             "nerf_flag_compact": [P, P, I64, P, P],
             "nerf_scatter_counts": [P, P, I64, P, P],
             "nerf_segments_union": [P, P, P, I, I64, P, P, P, P, P, P],
@@ -126,8 +125,7 @@ EXPORTS = ("nerf_rays_gen", "nerf_pick_pixels", "nerf_clamp_near_far", "nerf_ray
            "nerf_occ_update", "nerf_occ_threshold", "nerf_occ_binarize", "nerf_occ_mark_invisible", "nerf_ray_counts",
            "nerf_packed_points", "nerf_rays_aabb_hit", "nerf_flag_compact", "nerf_scatter_counts", "nerf_segments_union",
            "nerf_moe_blend", "nerf_moe_blend_finish", "nerf_moe_blend_bwd", "nerf_occ_threshold_floats",
-           "nerf_sgd_multi", "nerf_reptile_workspace_bytes", "nerf_reptile_update", "nerf_ray_keep_flags",
-           "nerf_rays_compact")
+           "nerf_sgd_multi", "nerf_reptile_workspace_bytes", "nerf_reptile_update", "nerf_dataset_rays")
 
 
 def check(status: int, what: str) -> None:

@@ -3,10 +3,11 @@
 
 The reference decodes each image on the CPU, builds (H*W, 8) rays with torch, masks, clamps and filters them
 there (a process pool of up to 8 workers, ram_rays_dataset.py:151-204) and keeps the dataset in host RAM.
-Here the host only decodes the file (PIL, as the reference) and uploads the uint8 pixels; one fused kernel
-(nerf_rays_gen) makes every pixel's ray with the AABB near/far and gathers its colour / 255, nerf_clamp_near_far
-applies the override in place, and a keep-flag / exclusive-scan / compaction pass writes the kept rows straight
-into the dataset's concatenated device arrays. The dataset lives in HBM (32 + 12 + 4 B per ray), which is where
+Here the host only decodes the file (PIL, as the reference) and uploads the uint8 pixels of a run of same-size
+images in one copy; nerf_dataset_rays then makes every pixel's ray (directions, cam->world, AABB near/far, the
+near/far override) in a count pass that writes only a keep flag, one exclusive scan places the kept rows, and
+a write pass recomputes the kept rays and writes them with their colour / 255 and image index straight into the
+dataset's device arrays — one host read per run. The dataset lives in HBM (32 + 12 + 4 B per ray), which is where
 the training loop consumes it.
 
 Mirrors: ImageMetadata (image_metadata.py:41-121), get_image_metadata / get_metadata_item / cap_metadata /
@@ -139,33 +140,47 @@ def get_meta_lookups(train_md, val_md):
 
 # ---------------------------------------------------------------- GPU ray build
 
-def _image_rays(md, img_u8_dev, mask_dev, aabb_dev, center_pixels, override):
-    """Per image: fused rays + colours (HBM), clamp in place, keep flags -> (rays, rgb, flags, pos, n_kept)."""
-    H, W = int(md.H), int(md.W)
-    n = H * W
-    dev = img_u8_dev.device
-    c2w = md.c2w[:3, :4].to(dev, torch.float32).contiguous()
-    fx, fy, cx, cy = [float(v) for v in md.intrinsics]
-    rays = torch.empty((n, 8), dtype=torch.float32, device=dev)
-    rgb = torch.empty((n, 3), dtype=torch.float32, device=dev)
-    L = lib()
-    check(L.nerf_rays_gen(ptr(c2w), 1, None, n, H, W, fx, fy, cx, cy, int(center_pixels), 0.0, 0.0, ptr(aabb_dev),
-                          1e10, 1e10, ptr(img_u8_dev), ptr(rays), ptr(rgb), stream()), "nerf_rays_gen")
-    valid = torch.empty(n, dtype=torch.uint8, device=dev)
+def _override_args(override):
     if override is None:
-        has_n, nv, has_f, fv = 0, 0.0, 0, 0.0
-    else:
-        no, fo = override
-        # an override tuple always rewrites invalid rays to inf (ray_sampling.py:169-176), even (None, None):
-        # max(near, -inf) is the identity
-        has_n, nv = 1, (float("-inf") if no is None else float(no))
-        has_f, fv = (0, 0.0) if fo is None else (1, float(fo))
-    check(L.nerf_clamp_near_far(ptr(rays), n, has_n, nv, has_f, fv, 1e-6, float("inf"), ptr(valid), stream()),
-          "nerf_clamp_near_far")
+        return 0, 0.0, 0, 0.0
+    no, fo = override
+    # an override tuple always rewrites invalid rays to inf (ray_sampling.py:169-176), even (None, None):
+    # max(near, -inf) is the identity
+    return 1, (float("-inf") if no is None else float(no)), (0 if fo is None else 1), (0.0 if fo is None else float(fo))
+
+
+def build_run(run, aabb_dev, center_pixels, override, dev):
+    """One run of same-size images -> (rays (n,8), rgbs (n,3), img_indices (n,), kept image ids): nerf_dataset_rays
+    count pass, exclusive scan, ONE host read (per-image kept counts), write pass."""
+    H, W = int(run[0][0].H), int(run[0][0].W)
+    n_img = len(run)
+    imgs = torch.from_numpy(np.stack([np.asarray(img, dtype=np.uint8).reshape(H, W, 3) for _, img, _ in run]))
+    masks = None
+    if any(k is not None for _, _, k in run):
+        masks = torch.stack([torch.ones(H * W, dtype=torch.bool) if k is None else k.reshape(-1).bool()
+                             for _, _, k in run]).to(torch.uint8).to(dev)
+    imgs = imgs.to(dev)
+    c2w = torch.stack([md.c2w[:3, :4].float().reshape(12) for md, _, _ in run]).to(dev)
+    intr = torch.stack([torch.as_tensor(md.intrinsics, dtype=torch.float32).reshape(4) for md, _, _ in run]).to(dev)
+    ids = torch.tensor([int(md.image_index) for md, _, _ in run], dtype=torch.int32).to(dev)
+    hn, nv, hf, fv = _override_args(override)
+    n = n_img * H * W
     flags = torch.empty(n, dtype=torch.int32, device=dev)
-    check(L.nerf_ray_keep_flags(ptr(valid), ptr(mask_dev), n, ptr(flags), stream()), "nerf_ray_keep_flags")
+    L = lib()
+    args = (ptr(c2w), ptr(intr), ptr(ids), n_img, H, W, int(center_pixels), ptr(aabb_dev), hn, nv, hf, fv, ptr(imgs),
+            ptr(masks))
+    check(L.nerf_dataset_rays(*args, ptr(flags), None, None, None, None, stream()), "nerf_dataset_rays(count)")
     pos = exclusive_scan(flags)
-    return rays, rgb, flags, pos
+    bounds = pos[:: H * W].cpu().tolist()           # n_img + 1 image boundaries (the last one = total)
+    total = bounds[-1]
+    rays = torch.empty((total, 8), dtype=torch.float32, device=dev)
+    rgbs = torch.empty((total, 3), dtype=torch.float32, device=dev)
+    idx = torch.empty((total,), dtype=torch.int32, device=dev)
+    if total:
+        check(L.nerf_dataset_rays(*args, None, ptr(pos), ptr(rays), ptr(rgbs), ptr(idx), stream()),
+              "nerf_dataset_rays(write)")
+    kept = [int(md.image_index) for (md, _, _), a, b in zip(run, bounds[:-1], bounds[1:]) if b > a]
+    return rays, rgbs, idx, kept
 
 
 class RamRaysDataset(torch.utils.data.Dataset):
@@ -186,7 +201,16 @@ class RamRaysDataset(torch.utils.data.Dataset):
         override = ray_gen_kwargs.get("near_far_override", None)
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         aabb = box.aabb.reshape(6).to(dev, torch.float32).contiguous()
-        chunks, kept_ids, pending, pending_px = [], [], [], 0
+        chunks, kept_ids, run, run_px = [], [], [], 0
+
+        def flush():
+            nonlocal run, run_px
+            if run:
+                r, c, i, k = build_run(run, aabb, center_pixels, override, dev)
+                chunks.append((r, c, i))
+                kept_ids.extend(k)
+            run, run_px = [], 0
+
         with torch.no_grad():
             for md in metadata_items:
                 if md is None:
@@ -209,47 +233,26 @@ class RamRaysDataset(torch.utils.data.Dataset):
                     keep = self._apply_meganerf_val_balancing_static(keep, md.H, md.W)
                 if keep is not None and int(keep.sum()) == 0:
                     continue
-                img_d = img.contiguous().to(dev)
-                mask_d = None if keep is None else keep.reshape(-1).to(torch.uint8).to(dev)
-                rays, rgb, flags, pos = _image_rays(md, img_d, mask_d, aabb, center_pixels, override)
-                pending.append((md.image_index, rays, rgb, flags, pos))
-                pending_px += rays.shape[0]
-                if pending_px >= self.FLUSH_PIXELS:
-                    chunks.append(self._compact(pending, dev, kept_ids))
-                    pending, pending_px = [], 0
-            if pending or not chunks:
-                chunks.append(self._compact(pending, dev, kept_ids))
-        if len(chunks) == 1:
+                if run and ((run[0][0].H, run[0][0].W) != (md.H, md.W) or run_px >= self.FLUSH_PIXELS):
+                    flush()
+                run.append((md, img.contiguous().numpy() if isinstance(img, torch.Tensor) else img, keep))
+                run_px += md.H * md.W
+            flush()
+        if not chunks:
+            self._rays = torch.zeros((0, 8), dtype=torch.float32, device=dev)
+            self._rgbs = torch.zeros((0, 3), dtype=torch.float32, device=dev)
+            self._img_indices = torch.zeros((0,), dtype=torch.int32, device=dev)
+        elif len(chunks) == 1:
             self._rays, self._rgbs, self._img_indices = chunks[0]
         else:
             self._rays, self._rgbs, self._img_indices = (torch.cat([c[i] for c in chunks]) for i in range(3))
-        total = self._rays.shape[0]
         self._num_images = len(kept_ids)
         self._img_unique_ids = sorted(set(kept_ids))
-        if total == 0:
+        if len(self) == 0:
             print("Warning: MemoryDataset ended up empty. Check masks/val logic.")
 
-    # per-image full-resolution ray buffers (44 B / pixel) are compacted once this many pixels are pending
+    # images of one size are built together, up to this many pixels per run (HBM scratch: 12 B / pixel)
     FLUSH_PIXELS = 1 << 26
-
-    @staticmethod
-    def _compact(pending, dev, kept_ids):
-        """One host read of the pending images' kept counts, then compaction into one set of arrays."""
-        counts = torch.stack([p[4][-1] for p in pending]).cpu().tolist() if pending else []
-        total = int(sum(counts))
-        rays_o = torch.empty((total, 8), dtype=torch.float32, device=dev)
-        rgbs_o = torch.empty((total, 3), dtype=torch.float32, device=dev)
-        idx_o = torch.empty((total,), dtype=torch.int32, device=dev)
-        o = 0
-        for (iid, rays, rgb, flags, pos), c in zip(pending, counts):
-            if c == 0:  # no valid ray: the image is dropped (ram_rays_dataset.py:107-108)
-                continue
-            check(lib().nerf_rays_compact(ptr(rays), ptr(rgb), ptr(flags), ptr(pos), rays.shape[0], int(iid),
-                                          ptr(rays_o[o:]), ptr(rgbs_o[o:]), ptr(idx_o[o:]), stream()),
-                  "nerf_rays_compact")
-            o += c
-            kept_ids.append(int(iid))
-        return rays_o, rgbs_o, idx_o
 
     def __len__(self) -> int:
         return self._rgbs.shape[0]

@@ -228,3 +228,14 @@ def test_occ_training_step_gradients(occ):
     g2 = net.xyz_encoder.hash_table.grad
     assert torch.isfinite(g1).all() and float(g1.abs().sum()) > 0
     assert torch.isfinite(g2).all() and float(g2.abs().sum()) > 0
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 2047, 2048, 2049, 100_003, 5_000_001])
+def test_exclusive_scan_sizes(occ, n):
+    """nerf_exclusive_scan_i32 (reduce-then-scan over 2048-element tiles) vs an int64 cumsum: ragged tails,
+    tile boundaries, > 1024 tiles (several tile sums per thread of the middle pass)."""
+    g = torch.Generator().manual_seed(n)
+    x = torch.randint(0, 5, (n,), generator=g, dtype=torch.int32)
+    out = occ.exclusive_scan(x.to(DEV)).cpu()
+    ref = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(x.long(), 0)])
+    assert torch.equal(out.long(), ref)
