@@ -287,6 +287,16 @@ int nerf_occ_march(const NerfOccGrid* grid, const uint8_t* binaries, const float
                    int max_steps, int32_t* counts, const int32_t* offsets, int32_t* ray_idx, float* t0, float* t1,
                    hipStream_t stream);
 
+/* nerf_occ_march for every expert of a container in one launch (render_rays_occ, nerfs/ray_rendering.py:397-422):
+ * ray r is marched through expert k's grid only when it hits boxes[6k..6k+5] (_intersect_rays_aabb, :171-190).
+ * grids (K), binaries (K device pointers), boxes (K x 6), steps (K): HOST arrays; K <= 8.  Count pass:
+ * counts[k*N + r]; write pass: offsets (K*N+1, exclusive scan of counts) -> ray_idx (= r) / t0 / t1, so expert
+ * k's samples are the contiguous range [offsets[k*N], offsets[(k+1)*N]).  Jitter: counter RNG (seed, k, r). */
+int nerf_occ_march_multi(const NerfOccGrid* grids, const uint8_t* const* binaries, const float* boxes,
+                         const float* steps, int K, const float* rays, int64_t N, float near_plane, float far_plane,
+                         float cone_angle, int stratified, uint64_t seed, int max_steps, int32_t* counts,
+                         const int32_t* offsets, int32_t* ray_idx, float* t0, float* t1, hipStream_t stream);
+
 /* Exclusive scan of n int32 into out[n+1] (out[n] = total); in / out 16-byte aligned. Reduce-then-scan over
  * 2048-element tiles: 3 launches, 12 B of HBM traffic per element. */
 int64_t nerf_scan_workspace_bytes(int64_t n);
@@ -304,9 +314,14 @@ int nerf_packed_composite_bwd(const float* rgb_sigma, const float* t0, const flo
                               const float* g_weights, float* d_rgb_sigma, hipStream_t stream);
 
 /* render_visibility_from_density: keep[j] = T_j >= early_stop_eps && (alpha_thre <= 0 || alpha_j >= alpha_thre). */
+/* nerf_packed_visibility over n_seg segments in groups of `group` consecutive segments (one group per expert of
+ * a multi-expert march): segment s uses min(alpha_thre, alpha_groups[s / group]) (alpha_groups: device). */
+int nerf_packed_visibility_groups(const float* t0, const float* t1, const float* sigmas, const int32_t* offsets,
+                                  int64_t n_seg, int64_t group, float early_stop_eps, float alpha_thre,
+                                  const float* alpha_groups, int32_t* keep, hipStream_t stream);
 int nerf_packed_visibility(const float* t0, const float* t1, const float* sigmas, const int32_t* offsets, int64_t N,
                            float early_stop_eps, float alpha_thre, int32_t* keep, hipStream_t stream);
-/* Compaction of the kept samples (pos = exclusive scan of keep); counts_out (N, zeroed by the caller)
+/* Compaction of the kept samples (pos = exclusive scan of keep); counts_out (N, zeroed by the caller, or NULL)
  * receives the per-ray kept counts. */
 int nerf_packed_compact(const int32_t* keep, const int32_t* pos, int64_t M, const int32_t* ray_idx, const float* t0,
                         const float* t1, int32_t* ray_idx_out, float* t0_out, float* t1_out, int32_t* counts_out,

@@ -60,20 +60,13 @@ __device__ __forceinline__ int64_t cell_of(const Grid& G, float px, float py, fl
   return id;
 }
 
-// One thread per ray.  count pass (offsets == nullptr): counts[r] = #samples; write pass: fills the packed
-// arrays from offsets[r].
-__global__ void march_kernel(Grid G, const uint8_t* __restrict__ bin, const float* __restrict__ rays, int64_t N,
-                             float near_plane, float far_plane, float step, float cone, int stratified,
-                             const float* __restrict__ u, uint64_t seed, int max_steps, int32_t* __restrict__ counts,
-                             const int32_t* __restrict__ offsets, int32_t* __restrict__ ray_idx,
-                             float* __restrict__ t0, float* __restrict__ t1) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= N) return;
-  const float* ry = rays + r * 8;
-  const float o[3] = {ry[0], ry[1], ry[2]}, d[3] = {ry[3], ry[4], ry[5]};
-  float t = fmaxf(near_plane, ry[6]);
-  float tf = fminf(far_plane, ry[7]);
-  if (stratified) t += (u ? u[r] : nerf_uniform(seed, 0x0CC, (uint64_t)r)) * step;
+// March one ray through one grid from t (already jittered) to tf: emits [t, t+dt) when the cell of the midpoint
+// is occupied and skips empty cells on the dt lattice past the cell exit.  Count only when t0 == nullptr,
+// else writes from position w.  Returns the sample count.
+__device__ __forceinline__ int march_ray(const Grid& G, const uint8_t* __restrict__ bin, const float o[3],
+                                         const float d[3], float t, float tf, float step, float cone, int max_steps,
+                                         int64_t w, int32_t rid, int32_t* __restrict__ ray_idx,
+                                         float* __restrict__ t0, float* __restrict__ t1) {
   // clip to the outermost level box
   const float big = (float)(1 << (G.L - 1));
   for (int a = 0; a < 3; ++a) {
@@ -87,7 +80,6 @@ __global__ void march_kernel(Grid G, const uint8_t* __restrict__ bin, const floa
     tf = fminf(tf, fmaxf(ta, tb));
   }
   int n = 0, it = 0;
-  int64_t w = offsets ? offsets[r] : 0;
   while (t < tf && it < max_steps) {
     ++it;
     const float dt = fminf(fmaxf(t * cone, step), 1e10f);
@@ -98,8 +90,8 @@ __global__ void march_kernel(Grid G, const uint8_t* __restrict__ bin, const floa
     const int64_t id = cell_of(G, o[0] + d[0] * mid, o[1] + d[1] * mid, o[2] + d[2] * mid, &lvl, cmin, csz);
     if (id < 0) break;
     if (bin[id]) {
-      if (offsets) {
-        ray_idx[w] = (int32_t)r;
+      if (t0) {
+        ray_idx[w] = rid;
         t0[w] = t;
         t1[w] = t + dt;
         ++w;
@@ -114,7 +106,66 @@ __global__ void march_kernel(Grid G, const uint8_t* __restrict__ bin, const floa
       t = t + k * dt;
     }
   }
+  return n;
+}
+
+// One thread per ray.  count pass (offsets == nullptr): counts[r] = #samples; write pass: fills the packed
+// arrays from offsets[r].
+__global__ void march_kernel(Grid G, const uint8_t* __restrict__ bin, const float* __restrict__ rays, int64_t N,
+                             float near_plane, float far_plane, float step, float cone, int stratified,
+                             const float* __restrict__ u, uint64_t seed, int max_steps, int32_t* __restrict__ counts,
+                             const int32_t* __restrict__ offsets, int32_t* __restrict__ ray_idx,
+                             float* __restrict__ t0, float* __restrict__ t1) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= N) return;
+  const float* ry = rays + r * 8;
+  const float o[3] = {ry[0], ry[1], ry[2]}, d[3] = {ry[3], ry[4], ry[5]};
+  float t = fmaxf(near_plane, ry[6]);
+  const float tf = fminf(far_plane, ry[7]);
+  if (stratified) t += (u ? u[r] : nerf_uniform(seed, 0x0CC, (uint64_t)r)) * step;
+  const int n = march_ray(G, bin, o, d, t, tf, step, cone, max_steps, offsets ? offsets[r] : 0, (int32_t)r, ray_idx,
+                          offsets ? t0 : nullptr, t1);
   if (!offsets) counts[r] = n;
+}
+
+// All experts of a container in one launch (render_rays_occ, nerfs/ray_rendering.py:397-422): blockIdx.y =
+// expert k.  A ray is marched through expert k only when it hits k's scene box (_intersect_rays_aabb, :171-190,
+// the same arithmetic as nerf_rays_aabb_hit); counts / offsets are indexed k*N + r, ray_idx holds r.
+constexpr int MARCH_MAX_EXPERTS = 8;
+struct MarchExperts {
+  Grid G[MARCH_MAX_EXPERTS];
+  const uint8_t* bin[MARCH_MAX_EXPERTS];
+  float box[MARCH_MAX_EXPERTS][6];
+  float step[MARCH_MAX_EXPERTS];
+};
+
+__global__ void march_multi_kernel(MarchExperts E, const float* __restrict__ rays, int64_t N, float near_plane,
+                                   float far_plane, float cone, int stratified, uint64_t seed, int max_steps,
+                                   int32_t* __restrict__ counts, const int32_t* __restrict__ offsets,
+                                   int32_t* __restrict__ ray_idx, float* __restrict__ t0, float* __restrict__ t1) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  if (r >= N) return;
+  const float* ry = rays + r * 8;
+  float tmin = -INFINITY, tmax = INFINITY;
+  for (int a = 0; a < 3; ++a) {
+    const float dd = ry[3 + a];
+    const float inv = fabsf(dd) > 1e-9f ? 1.0f / dd : 1.0f / 1e-9f;
+    const float ta = (E.box[k][a] - ry[a]) * inv, tb = (E.box[k][3 + a] - ry[a]) * inv;
+    tmin = fmaxf(tmin, fminf(ta, tb));
+    tmax = fminf(tmax, fmaxf(ta, tb));
+  }
+  int n = 0;
+  if (fminf(tmax, ry[7]) > fmaxf(tmin, ry[6])) {
+    const float o[3] = {ry[0], ry[1], ry[2]}, d[3] = {ry[3], ry[4], ry[5]};
+    float t = fmaxf(near_plane, ry[6]);
+    const float tf = fminf(far_plane, ry[7]);
+    if (stratified) t += nerf_uniform(seed, 0x0CC00 + (uint64_t)k, (uint64_t)r) * E.step[k];
+    const int64_t j = (int64_t)k * N + r;
+    n = march_ray(E.G[k], E.bin[k], o, d, t, tf, E.step[k], cone, max_steps, offsets ? offsets[j] : 0, (int32_t)r,
+                  ray_idx, offsets ? t0 : nullptr, t1);
+  }
+  if (!offsets) counts[(int64_t)k * N + r] = n;
 }
 
 // ---- exclusive scan of int32 (n+1 outputs): reduce-then-scan over 2048-element tiles (256 threads x 8
@@ -321,9 +372,11 @@ __global__ void packed_bwd_kernel(const float* __restrict__ rs, const float* __r
 // keep[j] = T_j >= eps && alpha_j >= alpha_thre  (one wave per ray)
 __global__ void packed_vis_kernel(const float* __restrict__ t0, const float* __restrict__ t1,
                                   const float* __restrict__ sig, const int32_t* __restrict__ off, int64_t N,
-                                  float eps, float athr, int32_t* __restrict__ keep) {
+                                  float eps, float athr, const float* __restrict__ athr_group, int64_t group,
+                                  int32_t* __restrict__ keep) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= N) return;
+  if (athr_group) athr = fminf(athr, athr_group[r / group]);
   const int lane = threadIdx.x & 63;
   const int s0 = off[r], s1 = off[r + 1];
   float S = 0.f;
@@ -349,7 +402,7 @@ __global__ void compact_kernel(const int32_t* __restrict__ keep, const int32_t* 
   ri_o[p] = ri[j];
   t0_o[p] = t0[j];
   t1_o[p] = t1[j];
-  atomicAdd(&cnt_ray[ri[j]], 1);
+  if (cnt_ray) atomicAdd(&cnt_ray[ri[j]], 1);
 }
 
 // ---- occupancy update
@@ -503,6 +556,30 @@ extern "C" int nerf_occ_march(const NerfOccGrid* grid, const uint8_t* binaries, 
   return nerf_launch_status();
 }
 
+extern "C" int nerf_occ_march_multi(const NerfOccGrid* grids, const uint8_t* const* binaries, const float* boxes,
+                                    const float* steps, int K, const float* rays, int64_t N, float near_plane,
+                                    float far_plane, float cone_angle, int stratified, uint64_t seed, int max_steps,
+                                    int32_t* counts, const int32_t* offsets, int32_t* ray_idx, float* t0, float* t1,
+                                    hipStream_t st) {
+  if (K < 1 || K > MARCH_MAX_EXPERTS || N < 0 || max_steps < 1 || !grids || !binaries || !boxes || !steps)
+    return NERF_E_ARG;
+  if (N == 0) return NERF_OK;
+  if (!rays || (!offsets && !counts) || (offsets && (!ray_idx || !t0 || !t1))) return NERF_E_ARG;
+  if ((int64_t)K * N > INT32_MAX) return NERF_E_ARG;
+  MarchExperts E{};
+  for (int k = 0; k < K; ++k) {
+    if (!grid_ok(&grids[k]) || !binaries[k] || !(steps[k] > 0.f)) return NERF_E_ARG;
+    E.G[k] = make_grid(&grids[k]);
+    E.bin[k] = binaries[k];
+    for (int a = 0; a < 6; ++a) E.box[k][a] = boxes[6 * k + a];
+    E.step[k] = steps[k];
+  }
+  march_multi_kernel<<<dim3((unsigned)nerf_cdiv(N, 64), K), 64, 0, st>>>(E, rays, N, near_plane, far_plane, cone_angle,
+                                                                         stratified, seed, max_steps, counts, offsets,
+                                                                         ray_idx, t0, t1);
+  return nerf_launch_status();
+}
+
 extern "C" int64_t nerf_scan_workspace_bytes(int64_t n) {
   if (n < 0) return NERF_E_ARG;
   return nerf_cdiv(n < 1 ? 1 : n, SCAN_TILE) * 4 + 256;
@@ -558,7 +635,19 @@ extern "C" int nerf_packed_visibility(const float* t0, const float* t1, const fl
   if (N == 0) return NERF_OK;
   if (!t0 || !t1 || !sigmas || !offsets || !keep) return NERF_E_ARG;
   packed_vis_kernel<<<(unsigned)nerf_cdiv(N, 4), 256, 0, st>>>(t0, t1, sigmas, offsets, N, early_stop_eps, alpha_thre,
-                                                               keep);
+                                                               nullptr, 1, keep);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_packed_visibility_groups(const float* t0, const float* t1, const float* sigmas,
+                                             const int32_t* offsets, int64_t n_seg, int64_t group, float early_stop_eps,
+                                             float alpha_thre, const float* alpha_groups, int32_t* keep,
+                                             hipStream_t st) {
+  if (n_seg < 0 || group < 1) return NERF_E_ARG;
+  if (n_seg == 0) return NERF_OK;
+  if (!t0 || !t1 || !sigmas || !offsets || !keep || !alpha_groups) return NERF_E_ARG;
+  packed_vis_kernel<<<(unsigned)nerf_cdiv(n_seg, 4), 256, 0, st>>>(t0, t1, sigmas, offsets, n_seg, early_stop_eps,
+                                                                   alpha_thre, alpha_groups, group, keep);
   return nerf_launch_status();
 }
 
@@ -567,7 +656,7 @@ extern "C" int nerf_packed_compact(const int32_t* keep, const int32_t* pos, int6
                                    float* t1_out, int32_t* counts_out, hipStream_t st) {
   if (M < 0) return NERF_E_ARG;
   if (M == 0) return NERF_OK;
-  if (!keep || !pos || !ray_idx || !t0 || !t1 || !ray_idx_out || !t0_out || !t1_out || !counts_out) return NERF_E_ARG;
+  if (!keep || !pos || !ray_idx || !t0 || !t1 || !ray_idx_out || !t0_out || !t1_out) return NERF_E_ARG;
   compact_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(keep, pos, M, ray_idx, t0, t1, ray_idx_out, t0_out, t1_out,
                                                               counts_out);
   return nerf_launch_status();

@@ -162,6 +162,73 @@ class _BlendFn(torch.autograd.Function):
         return (None, None, None, None, *grads)
 
 
+def _march_experts(model, rays, sub_params, render_step_size, alpha_thre, cone_angle):
+    """Every expert's occupancy marching (MetaNGP.occupancy_marching, meta_ngp.py:384-443, on the rays that hit its
+    box, ray_rendering.py:397-422) in ONE launch pair: count -> scan -> ONE host read of the K+1 expert boundaries
+    -> write.  In training, the visibility filter (nerfacc render_visibility_from_density with alpha_thre =
+    min(alpha_thre, mean occupancy) per expert) runs over all experts' segments at once and compacts in place of
+    the per-expert host reads: the compacted offsets are pos[offsets], sizes stay on the device.
+    Returns (ray_idx, t0, t1, offsets (K*N+1)) or (None,)*4 when no expert produced a sample."""
+    from . import kernels as K_
+    from .occupancy import exclusive_scan
+    subs = list(model.submodules)
+    K, N, dev = len(subs), rays.shape[0], rays.device
+    ex0 = subs[0]
+    for ex in subs[1:]:
+        if (ex.near_plane, ex.far_plane) != (ex0.near_plane, ex0.far_plane):
+            raise ValueError("experts with different near/far planes")
+    cone = [ex.cone_angle if cone_angle is None else cone_angle for ex in subs]
+    if len(set(cone)) != 1:
+        raise ValueError("experts with different cone angles")
+    grids = (type(ex0.occ_grid.grid) * K)(*[ex.occ_grid.grid for ex in subs])
+    bins = (ctypes.c_void_p * K)(*[ex.occ_grid.binaries.data_ptr() for ex in subs])
+    boxes = (ctypes.c_float * (6 * K))(*[float(v) for ex in subs for v in ex._aabb_host])
+    steps = (ctypes.c_float * K)(*[float(ex.render_step_size if render_step_size is None else render_step_size)
+                                   for ex in subs])
+    training = bool(ex0.training)
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    L = lib()
+    counts = torch.empty(K * N, dtype=torch.int32, device=dev)
+    args = (grids, bins, boxes, steps, K, ptr(rays), N, float(ex0.near_plane), float(ex0.far_plane), float(cone[0]),
+            int(training), ctypes.c_uint64(seed), 8192)
+    check(L.nerf_occ_march_multi(*args, ptr(counts), None, None, None, None, stream()), "nerf_occ_march_multi(count)")
+    offs = exclusive_scan(counts)
+    bounds = offs[::N].cpu().tolist()                  # the one host read: K+1 expert boundaries
+    M = bounds[-1]
+    if M == 0:
+        return None, None, None, None
+    ri = torch.empty(M, dtype=torch.int32, device=dev)
+    t0 = torch.empty(M, dtype=torch.float32, device=dev)
+    t1 = torch.empty(M, dtype=torch.float32, device=dev)
+    check(L.nerf_occ_march_multi(*args, None, ptr(offs), ptr(ri), ptr(t0), ptr(t1), stream()),
+          "nerf_occ_march_multi(write)")
+    athr = [ex.alpha_thre if alpha_thre is None else alpha_thre for ex in subs]
+    if training:
+        # visibility (nerfacc sampling with sigma_fn, early_stop_eps 1e-4): sigma of every sample from its expert
+        with torch.no_grad():
+            xd = K_.packed_points(rays, ri, t0, t1)
+            sig = torch.empty(M, dtype=torch.float32, device=dev)
+            for k, ex in enumerate(subs):
+                a, b = bounds[k], bounds[k + 1]
+                if b > a:
+                    sig[a:b] = ex.forward(xd[a:b], params=sub_params[k])[:, 3]
+            occ_mean = torch.stack([ex.occ_grid.occs.mean() for ex in subs]).float()
+            thr = torch.minimum(occ_mean, torch.tensor(athr, dtype=torch.float32, device=dev)).contiguous()
+            keep = torch.empty(M, dtype=torch.int32, device=dev)
+            check(L.nerf_packed_visibility_groups(ptr(t0), ptr(t1), ptr(sig), ptr(offs), K * N, N, 1e-4,
+                                                  float(max(athr)), ptr(thr), ptr(keep), stream()),
+                  "nerf_packed_visibility_groups")
+            pos = exclusive_scan(keep)
+            ri2 = torch.empty(M, dtype=torch.int32, device=dev)
+            t02 = torch.empty(M, dtype=torch.float32, device=dev)
+            t12 = torch.empty(M, dtype=torch.float32, device=dev)
+            check(L.nerf_packed_compact(ptr(keep), ptr(pos), M, ptr(ri), ptr(t0), ptr(t1), ptr(ri2), ptr(t02),
+                                        ptr(t12), None, stream()), "nerf_packed_compact")
+            offs = pos[offs.long()].contiguous()          # segment j now starts at pos[offsets[j]]
+            ri, t0, t1 = ri2, t02, t12
+    return ri, t0, t1, offs
+
+
 def render_container_occ(model, rays, *, params=None, bg_color_default="white", chunk=1_000_000,
                          render_step_size=None, alpha_thre=None, cone_angle=None):
     """render_rays_occ for the full container (nerfs/ray_rendering.py:384-481): per-expert AABB prefilter and
@@ -178,39 +245,21 @@ def render_container_occ(model, rays, *, params=None, bg_color_default="white", 
     K = len(model.submodules)
     sub_params = ([model.get_subdict(params, f"submodules.{k}") for k in range(K)] if params is not None
                   else [None] * K)
-    keep = []  # (t0_k, t1_k, global offsets)
-    for k, ex in enumerate(model.submodules):
-        box = (ctypes.c_float * 6)(*[float(v) for v in ex._aabb_host])
-        hit = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
-        check(lib().nerf_rays_aabb_hit(ptr(rays), N, box, ptr(hit), stream()), "nerf_rays_aabb_hit")
-        pos = exclusive_scan(hit[:N])
-        nh = int(pos[-1].item())
-        if nh == 0:
-            continue
-        hit_idx = torch.empty(nh, dtype=torch.int32, device=dev)
-        check(lib().nerf_flag_compact(ptr(hit), ptr(pos), N, ptr(hit_idx), stream()), "nerf_flag_compact")
-        rays_k = gather_rows(rays, hit_idx, 8)
-        _, t0_k, t1_k, offs_k = ex.occupancy_marching_packed(rays_k, params=sub_params[k],
-                                                             render_step_size=render_step_size,
-                                                             alpha_thre=alpha_thre, cone_angle=cone_angle)
-        if t0_k.numel() == 0:
-            continue
-        cnt_k = (offs_k[1:] - offs_k[:-1]).contiguous()
-        cnt = torch.zeros(max(N, 1), dtype=torch.int32, device=dev)
-        check(lib().nerf_scatter_counts(ptr(hit_idx), ptr(cnt_k), nh, ptr(cnt), stream()), "nerf_scatter_counts")
-        keep.append((t0_k, t1_k, exclusive_scan(cnt[:N])))
-    if not keep:
+    if K > 8:
+        raise ValueError("occupancy marching / segment union support at most 8 experts")
+    ri_all, t0_all, t1_all, offs_all = _march_experts(model, rays, sub_params, render_step_size, alpha_thre,
+                                                      cone_angle)
+    if offs_all is None:
         acc = rays.new_zeros(N)
         bg_rgb = _get_bg_rgb(model, d, params, rays, N, bg_color_default)
         return bg_rgb, acc.clone(), torch.zeros(1, 1, device=dev, dtype=rays.dtype), acc
-    if len(keep) > 8:
-        raise ValueError("segment union supports at most 8 experts")
-    t0s = (ctypes.c_void_p * len(keep))(*[t[0].data_ptr() for t in keep])
-    t1s = (ctypes.c_void_p * len(keep))(*[t[1].data_ptr() for t in keep])
-    ofs = (ctypes.c_void_p * len(keep))(*[t[2].data_ptr() for t in keep])
+    # expert k's segments: offsets[k*N : (k+1)*N + 1] index the shared t0 / t1 arrays
+    t0s = (ctypes.c_void_p * K)(*([t0_all.data_ptr()] * K))
+    t1s = (ctypes.c_void_p * K)(*([t1_all.data_ptr()] * K))
+    ofs = (ctypes.c_void_p * K)(*[offs_all[k * N:].data_ptr() for k in range(K)])
     L = lib()
     cnt = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
-    check(L.nerf_segments_union(t0s, t1s, ofs, len(keep), N, ptr(cnt), None, None, None, None, stream()),
+    check(L.nerf_segments_union(t0s, t1s, ofs, K, N, ptr(cnt), None, None, None, None, stream()),
           "nerf_segments_union(count)")
     moff = exclusive_scan(cnt[:N])
     M = int(moff[-1].item())
@@ -221,7 +270,7 @@ def render_container_occ(model, rays, *, params=None, bg_color_default="white", 
     ri = torch.empty(M, dtype=torch.int32, device=dev)
     t0 = torch.empty(M, dtype=torch.float32, device=dev)
     t1 = torch.empty(M, dtype=torch.float32, device=dev)
-    check(L.nerf_segments_union(t0s, t1s, ofs, len(keep), N, None, ptr(moff), ptr(ri), ptr(t0), ptr(t1), stream()),
+    check(L.nerf_segments_union(t0s, t1s, ofs, K, N, None, ptr(moff), ptr(ri), ptr(t0), ptr(t1), stream()),
           "nerf_segments_union(write)")
     xm = K_.packed_points(rays, ri, t0, t1)
     with torch.no_grad():
