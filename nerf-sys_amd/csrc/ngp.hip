@@ -20,6 +20,7 @@
 // persistent workgroup visits (one 32x32 accumulator block per (layer, n-block, k-block), dealt to the 4
 // waves), input gradients go tile-to-tile in LDS, d_enc leaves to HBM for the hash-grid scatter.  Each
 // workgroup writes ONE slab of the packed gradient; a deterministic reduce sums the slabs.
+#include <cstdlib>
 #include <mutex>
 
 #include "mlp_common.hpp"
@@ -333,6 +334,64 @@ __global__ void hash_bwd_f2_kernel(HashArgs a, const float* __restrict__ x, int6
     const int dy = yz >> 1, dz = yz & 1;
     const float v = __fmul_rn(__fmul_rn(__fmul_rn(gg, dz ? w[2] : u[2]), dy ? w[1] : u[1]), wx);
     unsafeAtomicAdd(tb + (int64_t)ngp_hash(i0[0] + dx, i0[1] + dy, i0[2] + dz, mask) * 2 + f, v);
+  }
+}
+
+// F = 2 with run aggregation.  Lanes: q = lane & 3 (feature q & 1, x-corner q >> 1), sample m = global lane / 4,
+// so a wave holds 16 consecutive samples — consecutive samples of one ray in the packed (ray-major, t-sorted)
+// order.  Each thread walks the L levels; at coarse levels neighbouring samples share cells, so before every
+// atomic the lanes of one (feature, x-corner) sub-sequence holding the same table entry are summed with a
+// segmented suffix scan (runs of equal index) and only the run head issues the atomic: the atomic count drops
+// where samples per cell > 1 (levels with res * step < 1), the result is the same sum in another order.
+__global__ __launch_bounds__(256) void hash_bwd_f2_agg_kernel(HashArgs a, const float* __restrict__ x, int64_t xs,
+                                                              int64_t M, const float* __restrict__ g, int gs,
+                                                              float* __restrict__ dtab) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int q = lane & 3, grp = lane >> 2;
+  const int64_t m = gid >> 2;
+  const bool valid = m < M;
+  if (__ballot(valid) == 0) return;
+  float p[3] = {0.f, 0.f, 0.f};
+  if (valid) load_x01(a, x, xs, m, p);
+  const uint32_t mask = (1u << a.log2T) - 1u;
+  const int dx = q >> 1, f = q & 1;
+  const unsigned long long qmask = 0x1111111111111111ull << q;
+  const unsigned long long after = lane == 63 ? 0ull : ~((2ull << lane) - 1ull);
+  for (int l = 0; l < a.L; ++l) {
+    const float r = (float)a.res[l];
+    float w[3];
+    int i0[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float sc = __fmul_rn(p[c], r);
+      const float fl = floorf(sc);
+      w[c] = __fsub_rn(sc, fl);
+      i0[c] = (int)fl;
+      if (a.interp == 2) w[c] = __fmul_rn(__fmul_rn(w[c], w[c]), __fsub_rn(3.0f, __fmul_rn(2.0f, w[c])));
+    }
+    const float u[3] = {__fsub_rn(1.0f, w[0]), __fsub_rn(1.0f, w[1]), __fsub_rn(1.0f, w[2])};
+    const float wx = dx ? w[0] : u[0];
+    const float gg = valid ? g[m * gs + l * 2 + f] : 0.f;
+    float* tb = dtab + ((int64_t)l << a.log2T) * 2;
+#pragma unroll
+    for (int yz = 0; yz < 4; ++yz) {
+      const int dy = yz >> 1, dz = yz & 1;
+      const float v = __fmul_rn(__fmul_rn(__fmul_rn(gg, dz ? w[2] : u[2]), dy ? w[1] : u[1]), wx);
+      const uint32_t idx = valid ? ngp_hash(i0[0] + dx, i0[1] + dy, i0[2] + dz, mask) * 2u + (uint32_t)f
+                                 : 0xFFFFFFFFu;
+      const uint32_t prev = __shfl_up(idx, 4, 64);
+      const bool head = grp == 0 || prev != idx;
+      const unsigned long long nxt = __ballot(head) & qmask & after;  // heads after me in my sub-sequence
+      const int run_end = nxt ? (int)__builtin_ctzll(nxt) - 4 : 60 + q;
+      float sum = v;
+#pragma unroll
+      for (int off = 4; off < 64; off <<= 1) {
+        const float o = __shfl_down(sum, off, 64);
+        if (lane + off <= run_end) sum += o;
+      }
+      if (head && valid) unsafeAtomicAdd(tb + idx, sum);
+    }
   }
 }
 
@@ -782,6 +841,15 @@ extern "C" int nerf_hash_encode(const NerfHashGrid* grid, const float* table, co
   return nerf_launch_status();
 }
 
+// NERF_HASH_BWD_AGG=0 selects the per-(sample, level) kernel without run aggregation (A/B measurements)
+static bool hash_bwd_aggregate() {
+  static const bool on = [] {
+    const char* e = getenv("NERF_HASH_BWD_AGG");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 extern "C" int nerf_hash_encode_bwd(const NerfHashGrid* grid, const float* x, int64_t x_stride, int64_t M,
                                     const float* aabb, float enc_eps, const float* d_out, int d_stride,
                                     float* d_table, hipStream_t st) {
@@ -800,7 +868,12 @@ extern "C" int nerf_hash_encode_bwd(const NerfHashGrid* grid, const float* x, in
   switch (a.F) {
     case 1: hash_bwd_kernel<1><<<blocks, 256, 0, st>>>(a, x, x_stride, M, d_out, d_stride, d_table); break;
     case 2:
-      hash_bwd_f2_kernel<<<(unsigned)nerf_cdiv(4 * n, 256), 256, 0, st>>>(a, x, x_stride, M, d_out, d_stride, d_table);
+      if (a.interp != 0 && hash_bwd_aggregate())
+        hash_bwd_f2_agg_kernel<<<(unsigned)nerf_cdiv(4 * M, 256), 256, 0, st>>>(a, x, x_stride, M, d_out, d_stride,
+                                                                                d_table);
+      else
+        hash_bwd_f2_kernel<<<(unsigned)nerf_cdiv(4 * n, 256), 256, 0, st>>>(a, x, x_stride, M, d_out, d_stride,
+                                                                            d_table);
       break;
     case 4: hash_bwd_kernel<4><<<blocks, 256, 0, st>>>(a, x, x_stride, M, d_out, d_stride, d_table); break;
     default: hash_bwd_kernel<8><<<blocks, 256, 0, st>>>(a, x, x_stride, M, d_out, d_stride, d_table); break;
