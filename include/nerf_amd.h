@@ -221,6 +221,10 @@ int64_t nerf_ngp_workspace_bytes(const NerfNgpNet* net, int64_t M);
  * run on fp32 MFMA with the activations in LDS. */
 int nerf_ngp_fwd(const NerfNgpNet* net, const float* w, const float* enc, int enc_stride, const float* x_d,
                  int64_t M, float* rgb_sigma, hipStream_t stream);
+/* MetaNGP.density (models/inr/meta_ngp.py:192-224): sigma (M) = trunc_exp of the sigma head after the trunk;
+ * the colour branch is not evaluated. */
+int nerf_ngp_density(const NerfNgpNet* net, const float* w, const float* enc, int enc_stride, int64_t M,
+                     float* sigma, hipStream_t stream);
 
 /* Backward of nerf_ngp_fwd (recomputes the forward on chip): d_enc (M rows, pitch enc_stride; cols
  * >= in_dim untouched) and d_w (packed layout; overwritten, or accumulated into if accumulate != 0). */

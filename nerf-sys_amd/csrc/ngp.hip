@@ -587,6 +587,30 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpPlan P, const float* __
   }
 }
 
+// MetaNGP.density (meta_ngp.py:192-224): the sigma trunk and head only — sigma = trunc_exp(raw) per row; the
+// colour branch (direction encoding + colour MLP, about half the network) is skipped.  Used by the visibility
+// filter of the occupancy marcher and the occupancy-grid update, which need sigma only.
+__global__ __launch_bounds__(256) void ngp_density_kernel(NgpPlan P, const float* __restrict__ w,
+                                                          const float* __restrict__ enc, int es, int64_t M,
+                                                          float* __restrict__ sigma) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 31, lh = lane >> 5;
+  const int64_t m0 = (int64_t)blockIdx.x * NGP_ROWS;
+  load_enc(P, smem, enc, es, m0, M);
+  __syncthreads();
+  for (int l = 0; l <= P.head; ++l) {
+    layer_fwd(P.ly[l], smem, w, wave, li, lh);
+    __syncthreads();
+  }
+  if (threadIdx.x < NGP_ROWS) {
+    const int64_t m = m0 + threadIdx.x;
+    if (m < M) {
+      const float sr = smem[P.ly[P.head].out_buf + threadIdx.x * P.ly[P.head].out_ld];
+      sigma[m] = expf(fminf(fmaxf(sr, -nerf_mlp::EXP_MAX), nerf_mlp::EXP_MAX));
+    }
+  }
+}
+
 // Gnext[r][k] = sum_n G[r][n] W[n][k]  (masked by X > 0 when the input is a ReLU output).  If dst_global the
 // result goes to d_enc rows m < M, columns < ncols instead of LDS.
 __device__ __forceinline__ void layer_dgrad(const NgpLayer& L, float* smem, const float* __restrict__ w, int G,
@@ -926,6 +950,19 @@ extern "C" int nerf_ngp_fwd(const NerfNgpNet* net, const float* w, const float* 
   const size_t sm = (size_t)P.smem_floats * 4;
   allow_lds(ngp_fwd_kernel);
   ngp_fwd_kernel<<<(unsigned)nerf_cdiv(M, NGP_ROWS), 256, sm, st>>>(P, w, enc, enc_stride, x_d, M, rgb_sigma);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_ngp_density(const NerfNgpNet* net, const float* w, const float* enc, int enc_stride, int64_t M,
+                                float* sigma, hipStream_t st) {
+  NgpPlan P;
+  if (!net || M < 0 || !make_plan(*net, false, P) || enc_stride < net->in_dim) return NERF_E_ARG;
+  if (M == 0) return NERF_OK;
+  if (!w || !enc || !sigma) return NERF_E_ARG;
+  if (!nerf_aligned16(w)) return NERF_E_ALIGN;
+  const size_t sm = (size_t)P.smem_floats * 4;
+  allow_lds(ngp_density_kernel);
+  ngp_density_kernel<<<(unsigned)nerf_cdiv(M, NGP_ROWS), 256, sm, st>>>(P, w, enc, enc_stride, M, sigma);
   return nerf_launch_status();
 }
 

@@ -211,7 +211,7 @@ def _march_experts(model, rays, sub_params, render_step_size, alpha_thre, cone_a
             for k, ex in enumerate(subs):
                 a, b = bounds[k], bounds[k + 1]
                 if b > a:
-                    sig[a:b] = ex.forward(xd[a:b], params=sub_params[k])[:, 3]
+                    sig[a:b] = ex.density(xd[a:b, :3], params=sub_params[k]).view(-1)
             occ_mean = torch.stack([ex.occ_grid.occs.mean() for ex in subs]).float()
             thr = torch.minimum(occ_mean, torch.tensor(athr, dtype=torch.float32, device=dev)).contiguous()
             keep = torch.empty(M, dtype=torch.int32, device=dev)

@@ -134,6 +134,15 @@ def ngp_fwd(net: NerfNgpNet, w_packed, enc, x_d, out=None):
     return out
 
 
+def ngp_density(net: NerfNgpNet, w_packed, enc):
+    """nerf_ngp_density: enc (M, >=in_dim) -> sigma (M,) (trunk + sigma head only)."""
+    M = enc.shape[0]
+    out = torch.empty(M, dtype=torch.float32, device=enc.device)
+    check(lib().nerf_ngp_density(_addr(net), ptr(w_packed), ptr(enc), enc.stride(0), M, ptr(out), stream()),
+          "nerf_ngp_density")
+    return out
+
+
 _WS = {}
 
 
@@ -450,7 +459,20 @@ class InstantNGP(nn.Module):
         if return_feats:
             raise NotImplementedError("density(return_feats=True): geo features are not materialised")
         shp = x.shape[:-1]
-        xd = torch.cat([x.reshape(-1, 3).float(), torch.zeros_like(x.reshape(-1, 3).float())], -1)
+        xf = x.reshape(-1, 3).float()
+        w = self.packed(params)
+        if not (torch.is_grad_enabled() and (w.requires_grad or self.xyz_encoder.hash_table.requires_grad)):
+            # no graph needed (visibility filter, occupancy update): sigma branch only
+            with torch.no_grad():
+                h = TIMING.start("hash_fwd", xf.shape[0])
+                enc = hash_encode(self.xyz_encoder.grid, self.xyz_encoder.hash_table.detach(), xf, self._aabb_host,
+                                  self._eps)
+                TIMING.stop(h)
+                h = TIMING.start("mlp_density", xf.shape[0])
+                sig = ngp_density(self.net_struct, w.detach(), enc)
+                TIMING.stop(h)
+                return sig.view(*shp, 1)
+        xd = torch.cat([xf, torch.zeros_like(xf)], -1)
         xd[:, 5] = 1.0
         return self.forward(xd, params=params)[:, 3:4].view(*shp, 1)
 

@@ -227,3 +227,25 @@ def test_ngp_trainer_step_vs_oracle(z, N):
         opt.step()
         losses.append(float(loss))
     assert abs(l2 - losses[1]) <= 1e-3 * max(1e-3, losses[1]), (l2, losses[1])
+
+
+def test_density_only_kernel_matches_forward():
+    """nerf_ngp_density (trunk + sigma head only) == the sigma column of the full fused forward, bit for bit
+    (the same trunk code path), on ragged M; density() under no_grad takes it, with grad it keeps the graph."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from nerf_amd.ngp import InstantNGP
+    torch.manual_seed(0)
+    m = InstantNGP(scene_box=torch.tensor([[-1.5] * 3, [1.5] * 3]), hidden=64, sigma_depth=2, color_hidden=64, color_depth=2, dir_encoding="spherical",
+                   hash_enc_conf=dict(levels=8, features_per_level=2, log2_hashmap_size=14, min_res=8, max_res=256,
+                                      interpolation="Linear")).to("cuda")
+    for M in (1, 63, 64, 1000):
+        x = (torch.rand(M, 3, device="cuda") * 3 - 1.5)
+        d = torch.nn.functional.normalize(torch.randn(M, 3, device="cuda"), dim=-1)
+        full = m(torch.cat([x, d], -1))[:, 3]
+        with torch.no_grad():
+            s = m.density(x).view(-1)
+        assert torch.equal(s, full.detach()), M
+    xg = torch.rand(50, 3, device="cuda") * 3 - 1.5
+    s = m.density(xg)
+    assert s.requires_grad
