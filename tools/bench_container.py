@@ -108,18 +108,14 @@ def cpu_baseline(seconds):
                       f"in {el:.1f}s"}
 
 
-def main():
-    a = parse()
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
-    from nerf_amd import ngp as G
+def build_step(a, dev):
+    """The container, FlatAdam and one train step closure (step -> loss)."""
     from nerf_amd.container import MetaContainer
     from nerf_amd.losses import compute_mse_loss
     from nerf_amd.optim import FlatAdam
     from nerf_amd.ray_sampling import SceneBox
     from nerf_amd.scene import make_blender_scene
     from nerf_amd.trainer import RayBatcher
-
     torch.manual_seed(0)
     scene = make_blender_scene(n_train=a.train_views, n_test=1, H=800, W=800, seed=0, device=dev)
     boxes, cents = boxes_and_centroids()
@@ -146,6 +142,16 @@ def main():
         opt.step()
         return loss
 
+    return one, model
+
+
+def main():
+    a = parse()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    from nerf_amd import ngp as G
+
+    one, model = build_step(a, dev)
     for s in range(a.warmup):
         loss = one(s)
     assert model.occ_ready, "occupancy warm-up did not finish"
