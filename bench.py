@@ -48,7 +48,8 @@ def parse():
                     help="blender = Lego-style 800x800 (configs[1]/[2]); llff = Fern-style 1008x756 NDC (configs[3])")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--psnr", action="store_true", help="render one held-out 800x800 view after the timed steps")
+    ap.add_argument("--no-psnr", action="store_true",
+                    help="skip the full-image PSNR of one held-out view rendered after the timed steps")
     ap.add_argument("--no-overlap", action="store_true", help="run the coarse-net backward on the main stream")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
                     help="MLP GEMM precision: fp32 = BASELINE configs[1] (default, the headline), bf16 = configs[2]")
@@ -193,7 +194,7 @@ def main():
         "step_mfma_frac": round(value * FLOP_PER_RAY / world / 1e12 / peak_step, 4),
         "final_loss": round(final_loss, 6),
     }
-    if a.psnr and rank == 0:
+    if not a.no_psnr and rank == 0:
         from nerf_amd.ray_rendering import render_image
         tr.sync_to_modules()
         coarse.eval()
@@ -203,6 +204,9 @@ def main():
                                  fine_model=fine.eval(), ndc=(scene.focal, 1.0) if scene.ndc else None)
         from nerf_amd.losses import image_psnr
         out["psnr_after_steps"] = round(image_psnr(img, scene.test_images[0], "linear"), 3)
+        out["psnr_note"] = ("held-out view after warmup+steps train steps (outside the timed region); "
+                            "convergence: tools/train_psnr.py, profiles/r01/psnr_*.jsonl (fp32 28.1 dB / bf16 "
+                            "28.1 dB after 3000 steps)")
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.samples, a.importance)
     elif rank == 0:

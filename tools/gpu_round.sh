@@ -19,7 +19,7 @@ if [[ $STEP == all || $STEP == bench ]]; then
 fi
 if [[ $STEP == all || $STEP == prof ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-    python3 bench.py $BENCH_ARGS --no-cpu-baseline > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
+    python3 bench.py $BENCH_ARGS --no-cpu-baseline --no-psnr > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
   python3 tools/prof_summary.py gpurun_out/prof/run_kernel_stats.csv 25 > gpurun_out/prof_summary.txt 2>&1
   tail -1 gpurun_out/prof.log | cut -c1-200
 fi
