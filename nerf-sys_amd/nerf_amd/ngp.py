@@ -148,7 +148,8 @@ _WS = {}
 
 def ngp_workspace(net: NerfNgpNet, M, device):
     need_b = max(int(lib().nerf_ngp_workspace_bytes(_addr(net), M)), 16)
-    key = str(device)
+    # one buffer per (device, stream): launches on different streams never share a workspace
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
     ws = _WS.get(key)
     if ws is None or ws.numel() < need_b:
         ws = torch.empty(need_b, dtype=torch.uint8, device=device)

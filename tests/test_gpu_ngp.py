@@ -249,3 +249,39 @@ def test_density_only_kernel_matches_forward():
     xg = torch.rand(50, 3, device="cuda") * 3 - 1.5
     s = m.density(xg)
     assert s.requires_grad
+
+
+def test_two_streams_do_not_share_workspaces():
+    """SURVEY §8b threading: forward + backward of one expert issued on two streams at once equal the same work
+    run one after the other (the backward workspace is per stream)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from nerf_amd.ngp import InstantNGP
+    torch.manual_seed(1)
+    m = InstantNGP(scene_box=torch.tensor([[-1.5] * 3, [1.5] * 3]), hidden=64, sigma_depth=2, color_hidden=64,
+                   color_depth=2, dir_encoding="spherical",
+                   hash_enc_conf=dict(levels=8, features_per_level=2, log2_hashmap_size=14, min_res=8, max_res=256,
+                                      interpolation="Linear")).to("cuda")
+    ws = [p for n, p in m.named_parameters() if "hash_table" not in n]
+    xs = []
+    for s in range(2):
+        g = torch.Generator().manual_seed(10 + s)
+        x = torch.rand(20000, 3, generator=g) * 3 - 1.5
+        d = torch.nn.functional.normalize(torch.randn(20000, 3, generator=g), dim=-1)
+        xs.append(torch.cat([x, d], -1).to("cuda"))
+
+    def run(x):
+        return torch.autograd.grad(m(x).square().sum(), ws)
+
+    ref = [run(x) for x in xs]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    out = [None, None]
+    for i in range(2):
+        streams[i].wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(streams[i]):
+            out[i] = run(xs[i])
+    torch.cuda.synchronize()
+    for i in range(2):
+        for a, b in zip(out[i], ref[i]):
+            assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
