@@ -214,6 +214,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()  # the other ranks wait for rank 0's PSNR render / report before tearing down
         dist.destroy_process_group()
 
 
