@@ -338,6 +338,12 @@ int nerf_occ_cell_points(const NerfOccGrid* grid, const int32_t* cells, int64_t 
                          hipStream_t stream);
 int nerf_occ_update(float* occs, const int32_t* cells, const float* values, int64_t n, float ema_decay,
                     hipStream_t stream);
+/* The cell draw of OccGridEstimator._update after warm-up (nerfacc _sample_uniform_and_occupied_cells) with no
+ * host read: occ_list / pos = nerf_flag_compact / exclusive scan of the binaries (levels x cells_per_level) as
+ * int32 flags.  Per level: n uniform cells, then every occupied cell if there are <= n of them (other slots
+ * -1), else n draws with replacement.  cells: levels x 2n global ids; cell_points / update skip ids < 0. */
+int nerf_occ_sample_cells(const int32_t* occ_list, const int32_t* pos, int levels, int64_t cells_per_level,
+                          int64_t n, uint64_t seed, int32_t* cells, hipStream_t stream);
 int nerf_occ_threshold(const float* occs, int64_t n, float occ_thre, float* thre_out, hipStream_t stream);
 /* thre_out must hold nerf_occ_threshold_floats() floats (2 results + 16-B pad + fp64 block partials). */
 int64_t nerf_occ_threshold_floats(void);

@@ -412,6 +412,10 @@ __global__ void cell_points_kernel(Grid G, const int32_t* __restrict__ cells, in
   if (i >= n) return;
   const int64_t cpl = (int64_t)G.R * G.R * G.R;
   const int64_t id = cells[i];
+  if (id < 0) {  // empty sample slot (nerf_occ_sample_cells): a harmless point, its value is never used
+    for (int a = 0; a < 3; ++a) x[i * 3 + a] = G.c[a];
+    return;
+  }
   const int l = (int)(id / cpl);
   const int64_t q = id - l * cpl;
   const int ci[3] = {(int)(q / ((int64_t)G.R * G.R)), (int)((q / G.R) % G.R), (int)(q % G.R)};
@@ -428,8 +432,33 @@ __global__ void occ_update_kernel(float* __restrict__ occs, const int32_t* __res
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t id = cells[i];
+  if (id < 0) return;
   const float o = occs[id];
   if (o >= 0.f) occs[id] = fmaxf(o * decay, val[i]);
+}
+
+// _sample_uniform_and_occupied_cells without a host read: per level l, n uniform cells, then n slots over the
+// level's occupied cells occ_list[pos[l*cpl] .. pos[(l+1)*cpl]) (count c on the device): every occupied cell
+// when c <= n (remaining slots -1 = empty), else n draws with replacement.  cells: L x 2n global cell ids.
+__global__ void sample_cells_kernel(const int32_t* __restrict__ occ_list, const int32_t* __restrict__ pos, int L,
+                                    int64_t cpl, int64_t n, uint64_t seed, int32_t* __restrict__ cells) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)L * 2 * n) return;
+  const int l = (int)(i / (2 * n));
+  const int64_t j = i - (int64_t)l * 2 * n;
+  if (j < n) {
+    const uint64_t r = (uint64_t)(nerf_uniform(seed, 0x51u + (uint64_t)l, (uint64_t)j) * (float)cpl);
+    cells[i] = (int32_t)((int64_t)l * cpl + (int64_t)(r < (uint64_t)cpl ? r : cpl - 1));
+    return;
+  }
+  const int64_t k = j - n;
+  const int64_t base = pos[(int64_t)l * cpl], c = (int64_t)pos[(int64_t)(l + 1) * cpl] - base;
+  if (c <= n) {
+    cells[i] = k < c ? occ_list[base + k] : -1;
+  } else {
+    const uint64_t r = (uint64_t)(nerf_uniform(seed, 0xA3u + (uint64_t)l, (uint64_t)k) * (float)c);
+    cells[i] = occ_list[base + (int64_t)(r < (uint64_t)c ? r : c - 1)];
+  }
 }
 
 // mean of the visible occupancies (occs >= 0), clamped to occ_thre -> thre[0]; also the mean over all cells ->
@@ -668,6 +697,17 @@ extern "C" int nerf_occ_cell_points(const NerfOccGrid* grid, const int32_t* cell
   if (n == 0) return NERF_OK;
   if (!cells || !x) return NERF_E_ARG;
   cell_points_kernel<<<(unsigned)nerf_cdiv(n, 256), 256, 0, st>>>(make_grid(grid), cells, n, seed, x);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_occ_sample_cells(const int32_t* occ_list, const int32_t* pos, int levels, int64_t cells_per_level,
+                                     int64_t n, uint64_t seed, int32_t* cells, hipStream_t st) {
+  if (levels < 1 || cells_per_level < 1 || n < 0) return NERF_E_ARG;
+  if (n == 0) return NERF_OK;
+  if (!occ_list || !pos || !cells) return NERF_E_ARG;
+  const int64_t tot = (int64_t)levels * 2 * n;
+  sample_cells_kernel<<<(unsigned)nerf_cdiv(tot, 256), 256, 0, st>>>(occ_list, pos, levels, cells_per_level, n, seed,
+                                                                     cells);
   return nerf_launch_status();
 }
 

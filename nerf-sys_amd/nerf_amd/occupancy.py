@@ -200,19 +200,20 @@ class OccGridEstimator(nn.Module):
     def _update(self, step, occ_eval_fn, occ_thre=0.01, ema_decay=0.95, warmup_steps=256):
         dev = self.occs.device
         cpl = self.cells_per_lvl
-        ids = []
-        for lvl in range(self.levels):
-            if step < warmup_steps:
-                idx = torch.arange(cpl, device=dev)
-            else:
-                n = cpl // 4
-                uni = torch.randint(cpl, (n,), device=dev)
-                occ = torch.nonzero(self.binaries[lvl].reshape(-1)).squeeze(1)
-                if occ.numel() > n:
-                    occ = occ[torch.randint(occ.numel(), (n,), device=dev)]
-                idx = torch.cat([uni, occ])
-            ids.append((lvl * cpl + idx).to(torch.int32))
-        cells = torch.cat(ids).contiguous()
+        L = lib()
+        if step < warmup_steps:
+            cells = torch.arange(self.levels * cpl, dtype=torch.int32, device=dev)
+        else:
+            # uniform + occupied cells per level, drawn on the device (no nonzero / host read)
+            n = cpl // 4
+            flags = self.binaries.reshape(-1).to(torch.int32)
+            pos = exclusive_scan(flags)
+            occ_list = torch.empty(flags.numel(), dtype=torch.int32, device=dev)
+            check(L.nerf_flag_compact(ptr(flags), ptr(pos), flags.numel(), ptr(occ_list), stream()),
+                  "nerf_flag_compact")
+            cells = torch.empty(self.levels * 2 * n, dtype=torch.int32, device=dev)
+            check(L.nerf_occ_sample_cells(ptr(occ_list), ptr(pos), self.levels, cpl, n, ctypes.c_uint64(self._seed()),
+                                          ptr(cells), stream()), "nerf_occ_sample_cells")
         n = cells.numel()
         x = torch.empty((n, 3), dtype=torch.float32, device=dev)
         check(lib().nerf_occ_cell_points(_addr(self.grid), ptr(cells), n, ctypes.c_uint64(self._seed()), ptr(x),

@@ -239,3 +239,49 @@ def test_exclusive_scan_sizes(occ, n):
     out = occ.exclusive_scan(x.to(DEV)).cpu()
     ref = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(x.long(), 0)])
     assert torch.equal(out.long(), ref)
+
+
+def test_occupancy_cell_sampling_after_warmup(occ):
+    """nerfacc _sample_uniform_and_occupied_cells on the device (nerf_occ_sample_cells): per level n uniform
+    cells + every occupied cell when there are <= n of them (other slots empty), else n draws among them."""
+    import ctypes
+    from nerf_amd._lib import check, lib, ptr, stream
+    L, R = 2, 16
+    cpl = R ** 3
+    n = cpl // 4
+    g = torch.Generator().manual_seed(3)
+    b = torch.zeros(L, cpl, dtype=torch.uint8)
+    few = torch.randperm(cpl, generator=g)[: n // 3].sort().values      # level 0: fewer than n occupied
+    many = torch.randperm(cpl, generator=g)[: 3 * n].sort().values      # level 1: more than n occupied
+    b[0, few] = 1
+    b[1, many] = 1
+    flags = b.reshape(-1).to(torch.int32).to(DEV)
+    pos = occ.exclusive_scan(flags)
+    occ_list = torch.empty(flags.numel(), dtype=torch.int32, device=DEV)
+    check(lib().nerf_flag_compact(ptr(flags), ptr(pos), flags.numel(), ptr(occ_list), stream()), "compact")
+    cells = torch.empty(L * 2 * n, dtype=torch.int32, device=DEV)
+    check(lib().nerf_occ_sample_cells(ptr(occ_list), ptr(pos), L, cpl, n, ctypes.c_uint64(7), ptr(cells), stream()),
+          "sample")
+    c = cells.cpu().long().view(L, 2 * n)
+    for lvl in range(L):
+        uni = c[lvl, :n]
+        assert ((uni >= lvl * cpl) & (uni < (lvl + 1) * cpl)).all()
+    occ0 = c[0, n:]
+    assert torch.equal(occ0[: few.numel()], few) and (occ0[few.numel():] == -1).all()
+    occ1 = c[1, n:]
+    assert (occ1 >= 0).all() and bool(torch.isin(occ1 - cpl, many).all())
+    assert occ1.unique().numel() > n // 2                                 # draws spread over the occupied set
+
+
+def test_occupancy_update_after_warmup_touches_only_sampled(occ):
+    from nerf_amd.occupancy import OccGridEstimator
+    est = OccGridEstimator(roi_aabb=[-1, -1, -1, 1, 1, 1], resolution=16, levels=1).to(DEV)
+    est.train()
+    fn = lambda x: torch.ones(x.shape[0], device=x.device)           # every evaluated cell -> 1
+    est.update_every_n_steps(0, fn, occ_thre=0.5, warmup_steps=0, n=16)   # post-warm-up path from step 0
+    o = est.occs.cpu()
+    touched = int((o == 1.0).sum())
+    n = 16 ** 3 // 4
+    assert 0 < touched <= n                         # no occupied cells yet: only the n uniform draws
+    assert ((o == 0.0) | (o == 1.0)).all()
+    assert int(est.binaries.sum()) == touched
