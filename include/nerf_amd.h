@@ -240,6 +240,10 @@ int nerf_ngp_bwd(const NerfNgpNet* net, const float* w, const float* enc, int en
  * argmin.  weights (M, K) fp32. */
 int nerf_moe_route(const float* x, int64_t x_stride, int64_t M, const float* centroids, int K, int cluster_2d,
                    float boundary_margin, float* weights, hipStream_t stream);
+/* nerf_moe_route over `capacity` rows of which the first *m_dev (device int32) are real: rows past it get all-zero
+ * weights (no expert), so a following nerf_moe_dispatch over the capacity needs no host read of the count. */
+int nerf_moe_route_n(const float* x, int64_t x_stride, int64_t capacity, const int32_t* m_dev, const float* centroids,
+                     int K, int cluster_2d, float boundary_margin, float* weights, hipStream_t stream);
 
 /* Order-preserving per-expert dispatch (the `(w[:,k] > 0).nonzero()` of meta_container.py:288-296):
  * idx (up to M*K int32) receives the rows with weights[m][k] > eps, expert-major and ascending within an
@@ -359,6 +363,9 @@ int nerf_ray_counts(const int32_t* ray_idx, int64_t M, int64_t N, int32_t* count
 /* Sample points of packed intervals (render_expert_occ, ray_rendering.py:523-525): x_d[j] = [o + d t_mid, d]. */
 int nerf_packed_points(const float* rays, const int32_t* ray_idx, const float* t0, const float* t1, int64_t M,
                        float* x_d, hipStream_t stream);
+/* nerf_packed_points for the first *m_dev (device int32) of `capacity` rows; the rest are left untouched. */
+int nerf_packed_points_n(const float* rays, const int32_t* ray_idx, const float* t0, const float* t1,
+                         int64_t capacity, const int32_t* m_dev, float* x_d, hipStream_t stream);
 
 /* Full-container occupancy rendering (render_rays_occ, nerfs/ray_rendering.py:384-481).
  * nerf_rays_aabb_hit: _intersect_rays_aabb (:171-190) of rays (N,8) with box (HOST, 6 floats) -> hit (N) int32.

@@ -24,9 +24,13 @@ struct Cent {
 };
 
 __global__ void route_kernel(const float* __restrict__ x, int64_t xs, int64_t M, Cent cen, int K, int c2d, float bm,
-                             float* __restrict__ W) {
+                             const int32_t* __restrict__ m_dev, float* __restrict__ W) {
   const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
+  if (m_dev && m >= *m_dev) {  // capacity rows past the device-side count: no expert
+    for (int k = 0; k < K; ++k) W[m * K + k] = 0.f;
+    return;
+  }
   const float px = x[m * xs], py = x[m * xs + 1], pz = x[m * xs + 2];
   float dist[MOE_MAX_K];
   float mind = INFINITY;
@@ -287,7 +291,21 @@ extern "C" int nerf_moe_route(const float* x, int64_t x_stride, int64_t M, const
   for (int k = 0; k < K; ++k)
     for (int j = 0; j < 3; ++j) c.c[k][j] = centroids[3 * k + j];
   route_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(x, x_stride, M, c, K, cluster_2d, boundary_margin,
-                                                            weights);
+                                                            nullptr, weights);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_moe_route_n(const float* x, int64_t x_stride, int64_t capacity, const int32_t* m_dev,
+                                const float* centroids, int K, int cluster_2d, float boundary_margin, float* weights,
+                                hipStream_t st) {
+  if (capacity < 0 || K < 1 || K > MOE_MAX_K || x_stride < 3 || !centroids || !m_dev) return NERF_E_ARG;
+  if (capacity == 0) return NERF_OK;
+  if (!x || !weights) return NERF_E_ARG;
+  Cent c{};
+  for (int k = 0; k < K; ++k)
+    for (int j = 0; j < 3; ++j) c.c[k][j] = centroids[3 * k + j];
+  route_kernel<<<(unsigned)nerf_cdiv(capacity, 256), 256, 0, st>>>(x, x_stride, capacity, c, K, cluster_2d,
+                                                                   boundary_margin, m_dev, weights);
   return nerf_launch_status();
 }
 

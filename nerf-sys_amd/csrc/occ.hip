@@ -547,9 +547,9 @@ __global__ void ray_counts_kernel(const int32_t* __restrict__ ri, int64_t M, int
 
 __global__ void packed_points_kernel(const float* __restrict__ rays, const int32_t* __restrict__ ri,
                                      const float* __restrict__ t0, const float* __restrict__ t1, int64_t M,
-                                     float* __restrict__ xd) {
+                                     const int32_t* __restrict__ m_dev, float* __restrict__ xd) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= M) return;
+  if (j >= M || (m_dev && j >= *m_dev)) return;
   const float* r = rays + (int64_t)ri[j] * 8;
   const float tm = 0.5f * (t0[j] + t1[j]);
   float* o = xd + j * 6;
@@ -764,6 +764,15 @@ extern "C" int nerf_packed_points(const float* rays, const int32_t* ray_idx, con
   if (M < 0) return NERF_E_ARG;
   if (M == 0) return NERF_OK;
   if (!rays || !ray_idx || !t0 || !t1 || !x_d) return NERF_E_ARG;
-  packed_points_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(rays, ray_idx, t0, t1, M, x_d);
+  packed_points_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(rays, ray_idx, t0, t1, M, nullptr, x_d);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_packed_points_n(const float* rays, const int32_t* ray_idx, const float* t0, const float* t1,
+                                    int64_t capacity, const int32_t* m_dev, float* x_d, hipStream_t st) {
+  if (capacity < 0 || !m_dev) return NERF_E_ARG;
+  if (capacity == 0) return NERF_OK;
+  if (!rays || !ray_idx || !t0 || !t1 || !x_d) return NERF_E_ARG;
+  packed_points_kernel<<<(unsigned)nerf_cdiv(capacity, 256), 256, 0, st>>>(rays, ray_idx, t0, t1, capacity, m_dev, x_d);
   return nerf_launch_status();
 }

@@ -58,6 +58,7 @@ def lib():
             "nerf_ngp_density": [P, P, P, I, I64, P, P],
             "nerf_ngp_bwd": [P, P, P, I, P, I64, P, P, P, I, P, I64, P],
             "nerf_moe_route": [P, I64, I64, P, I, I, F, P, P],
+            "nerf_moe_route_n": [P, I64, I64, P, P, I, I, F, P, P],
             "nerf_moe_dispatch_workspace_bytes": [I64, I],
             "nerf_moe_dispatch": [P, I64, I, F, P, P, P, I64, P],
             "nerf_gather_rows": [P, I64, P, I64, I, P, I64, P],
@@ -83,6 +84,7 @@ def lib():
             "nerf_occ_mark_invisible": [P, P, P, I, I, I, F, P, P],
             "nerf_ray_counts": [P, I64, I64, P, P],
             "nerf_packed_points": [P, P, P, P, I64, P, P],
+            "nerf_packed_points_n": [P, P, P, P, I64, P, P, P],
             "nerf_rays_aabb_hit": [P, I64, P, P, P],
             "nerf_occ_threshold_floats": [],
             "nerf_sgd_multi": [I, P, P, P, P, F, P],
@@ -131,7 +133,8 @@ EXPORTS = ("nerf_rays_gen", "nerf_pick_pixels", "nerf_clamp_near_far", "nerf_ray
            "nerf_moe_blend", "nerf_moe_blend_finish", "nerf_moe_blend_bwd", "nerf_occ_threshold_floats",
            "nerf_sgd_multi", "nerf_reptile_workspace_bytes", "nerf_reptile_update", "nerf_dataset_rays",
            "nerf_occ_march_multi", "nerf_packed_visibility_groups", "nerf_ngp_density",
-           "nerf_occ_sample_cells")
+           "nerf_occ_sample_cells", "nerf_moe_route_n",
+           "nerf_packed_points_n")
 
 
 def check(status: int, what: str) -> None:
@@ -152,7 +155,8 @@ def ptr(t):
 
 
 def stream():
-    return c_void_p(torch.cuda.current_stream().cuda_stream)
+    """The current HIP stream of the current device (the raw handle torch's own kernel launchers use)."""
+    return c_void_p(torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice()))
 
 
 def need(t, name, dtype=torch.float32):

@@ -51,8 +51,9 @@ def moe_route(x, centroids_host, boundary_margin, cluster_2d):
     return W
 
 
-def moe_dispatch(W, eps=0.0):
-    """-> (offsets (K+1) host list, idx (device int32, expert-major))."""
+def moe_dispatch(W, eps=0.0, host_offsets=True):
+    """-> (offsets (K+1): host list, or the device int32 tensor when host_offsets is False; idx (device int32,
+    expert-major))."""
     M, K = W.shape
     offs = torch.empty(K + 1, dtype=torch.int32, device=W.device)
     idx = torch.empty(max(M * K, 1), dtype=torch.int32, device=W.device)
@@ -60,7 +61,7 @@ def moe_dispatch(W, eps=0.0):
     ws = torch.empty(wsb, dtype=torch.uint8, device=W.device)
     check(lib().nerf_moe_dispatch(ptr(W), M, K, float(eps), ptr(offs), ptr(idx), ptr(ws), wsb, stream()),
           "nerf_moe_dispatch")
-    return offs.cpu().tolist(), idx
+    return (offs.cpu().tolist() if host_offsets else offs), idx
 
 
 def gather_rows(src, idx, cols=None):
@@ -262,20 +263,32 @@ def render_container_occ(model, rays, *, params=None, bg_color_default="white", 
     check(L.nerf_segments_union(t0s, t1s, ofs, K, N, ptr(cnt), None, None, None, None, stream()),
           "nerf_segments_union(count)")
     moff = exclusive_scan(cnt[:N])
-    M = int(moff[-1].item())
+    # the merged count stays on the device: the union, its points, the routing and the dispatch run over a
+    # capacity (a ray's union of k sorted boundary lists has < 2x their segments), then ONE host read brings
+    # the merged count and the K+1 expert offsets together
+    cap = 2 * int(t0_all.numel())
+    ri = torch.empty(cap, dtype=torch.int32, device=dev)
+    t0 = torch.empty(cap, dtype=torch.float32, device=dev)
+    t1 = torch.empty(cap, dtype=torch.float32, device=dev)
+    check(L.nerf_segments_union(t0s, t1s, ofs, K, N, None, ptr(moff), ptr(ri), ptr(t0), ptr(t1), stream()),
+          "nerf_segments_union(write)")
+    m_dev = moff[N:]
+    xm = torch.empty((cap, 6), dtype=torch.float32, device=dev)
+    check(L.nerf_packed_points_n(ptr(rays), ptr(ri), ptr(t0), ptr(t1), cap, ptr(m_dev), ptr(xm), stream()),
+          "nerf_packed_points_n")
+    with torch.no_grad():
+        W = torch.empty((cap, K), dtype=torch.float32, device=dev)
+        c = (ctypes.c_float * len(model._cent_host))(*model._cent_host)
+        check(L.nerf_moe_route_n(ptr(xm), 6, cap, ptr(m_dev), c, K, int(model.cluster_2d),
+                                 float(model.boundary_margin), ptr(W), stream()), "nerf_moe_route_n")
+        offs_dev, idx = moe_dispatch(W, 1e-8, host_offsets=False)
+    host = torch.cat([m_dev, offs_dev]).cpu().tolist()
+    M, offs = host[0], host[1:]
     if M == 0:
         acc = rays.new_zeros(N)
         bg_rgb = _get_bg_rgb(model, d, params, rays, N, bg_color_default)
         return bg_rgb, acc.clone(), torch.zeros(1, 1, device=dev, dtype=rays.dtype), acc
-    ri = torch.empty(M, dtype=torch.int32, device=dev)
-    t0 = torch.empty(M, dtype=torch.float32, device=dev)
-    t1 = torch.empty(M, dtype=torch.float32, device=dev)
-    check(L.nerf_segments_union(t0s, t1s, ofs, K, N, None, ptr(moff), ptr(ri), ptr(t0), ptr(t1), stream()),
-          "nerf_segments_union(write)")
-    xm = K_.packed_points(rays, ri, t0, t1)
-    with torch.no_grad():
-        W = moe_route(xm, model._cent_host, model.boundary_margin, model.cluster_2d)
-        offs, idx = moe_dispatch(W, 1e-8)
+    ri, t0, t1, xm, W = ri[:M], t0[:M], t1[:M], xm[:M], W[:M]
     ks, sels, ys = [], [], []
     for k, sub in enumerate(model.submodules):
         n_k = offs[k + 1] - offs[k]
