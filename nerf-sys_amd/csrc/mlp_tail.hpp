@@ -1,0 +1,234 @@
+// Fused colour-branch backward of the vanilla MLP (fp32 path, mlp.hip).  The activations C0 / CIN may be read as
+// fp32 or bf16 (TA) and dO16 written as fp32 or bf16 (TD); all arithmetic and the weight-gradient sums are fp32.
+// Measured: fp32 path 28.2 -> 28.0 ms/step (six launches and ~1.7 GB of HBM traffic per step removed); the bf16
+// path keeps its bf16-MFMA chain, which is faster there (8.36 vs 8.74 ms/step with this kernel: one 256-thread
+// workgroup per CU walking 48 tiles is latency-bound at ~11 us per tile).
+#pragma once
+#include "gemm.hpp"
+#include "mlp_common.hpp"
+
+// ------------------------------------------------------------------ fused colour-branch backward
+// One kernel for everything between d_rgb_sigma and dO16 (the gradient of the [sigma | geo] head output):
+// sigmoid' and trunc_exp' (head_out), the colour_out and colour layer-0 weight / bias gradients and the
+// geo-feature input gradient.  Grid = the S row splits of the packed weight-gradient slabs; each
+// workgroup walks its split in 64-row tiles (the next tile's C0 / CIN rows are prefetched into registers
+// while the current one is computed), keeps its weight-gradient sums in registers across the tiles and
+// writes them into its slab once.  Per row it reads C0 / CIN / O3 / O16[0] / d_rgb_sigma (~1 KB) and writes
+// one 128-B dO16 row; the unfused chain moved ~2.7 KB per row through six launches.
+//   dO3   = g.rgb * s(1-s)                   (3 columns; VALU)
+//   dWc1 += dO3^T C0, dbc1 += sum dO3        (3 x 128: VALU, thread = output column)
+//   dC0   = (dO3 Wc1[:3]) * (C0 > 0)         (VALU, the forward ReLU mask is C0 > 0)
+//   dWc0 += dC0^T CIN, dbc0 += sum dC0       (128 x 64: MFMA, wave w -> rows 32w.., both 32-col blocks)
+//   dgeo  = dC0 Wc0[:, :15]                  (MFMA, C^T form (lane = row); wave w -> row block w&1,
+//                                             contraction half w>>1, the halves summed through LDS)
+//   dO16  = [g.sigma * exp(clamp(sigma_raw)), dgeo, 0...]
+namespace nerf_mlp {
+constexpr int CB_ROWS = 64;
+constexpr int CB_C0 = 132, CB_CIN = 68, CB_WT = 132, CB_GEO = 33;
+
+// 4 consecutive activations as fp32 (fp32 or bf16 storage) and 4 fp32 values stored as T
+__device__ __forceinline__ float4 tail_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 tail_ld4(const __bf16* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+__device__ __forceinline__ void tail_st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ void tail_st4(__bf16* p, float4 v) {
+  p[0] = (__bf16)v.x; p[1] = (__bf16)v.y; p[2] = (__bf16)v.z; p[3] = (__bf16)v.w;
+}
+
+template <typename TA, typename TD>
+__global__ __launch_bounds__(256) void color_bwd_kernel(const float* __restrict__ g, const float* __restrict__ O3,
+                                                        const float* __restrict__ O16,
+                                                        const TA* __restrict__ C0,
+                                                        const TA* __restrict__ CIN,
+                                                        const float* __restrict__ Wc0,  // [128][64]
+                                                        const float* __restrict__ Wc1,  // [32][128]
+                                                        TD* __restrict__ dO16, float* __restrict__ partial,
+                                                        int64_t slab, int64_t off_w0, int64_t off_b0,
+                                                        int64_t off_w1, int64_t off_b1, int64_t rps, int64_t M,
+                                                        int64_t Mp) {
+  __shared__ __attribute__((aligned(16))) float s_c0[CB_ROWS * CB_C0];
+  __shared__ __attribute__((aligned(16))) float s_dc0[CB_ROWS * CB_C0];
+  __shared__ __attribute__((aligned(16))) float s_cin[CB_ROWS * CB_CIN];
+  __shared__ __attribute__((aligned(16))) float s_wt[32 * CB_WT];  // Wc0^T rows c < 32: [c][j]
+  __shared__ __attribute__((aligned(16))) float s_w1[3 * 128];
+  __shared__ float s_do3[CB_ROWS * 4];
+  __shared__ float s_geo[2 * CB_ROWS * CB_GEO];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 31, lh = lane >> 5;
+  const int64_t r0 = (int64_t)blockIdx.x * rps;
+  int64_t r1 = r0 + rps;
+  if (r1 > Mp) r1 = Mp;
+
+  for (int i = tid; i < 32 * 128; i += 256) {
+    const int c = i >> 7, j = i & 127;
+    s_wt[c * CB_WT + j] = Wc0[j * 64 + c];
+  }
+  for (int i = tid; i < 3 * 128; i += 256) s_w1[i] = Wc1[i];
+
+  // register prefetch of one tile: C0 = 2048 float4 (8 / thread), CIN = 1024 float4 (4 / thread)
+  float4 pc[8], pi[4];
+  auto fetch = [&](int64_t t0) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int f = tid + 256 * u, r = f >> 5, c4 = f & 31;
+      const int64_t m = t0 + r;
+      pc[u] = m < r1 ? tail_ld4(C0 + m * 128 + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int f = tid + 256 * u, r = f >> 4, c4 = f & 15;
+      const int64_t m = t0 + r;
+      pi[u] = m < r1 ? tail_ld4(CIN + m * 64 + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+
+  // VALU accumulators: thread t -> dWc1 column j = t & 127, rows n = 0,1 (t < 128) or 2 (t >= 128)
+  const int jw = tid & 127, nw = tid < 128 ? 0 : 2;
+  float w1a = 0.f, w1b = 0.f, b1 = 0.f, b1b = 0.f;  // b1 / b1b: dbc1 sums kept by threads 0 and 128
+  nerf_f32x16 acc0[2], accg;
+  for (int r = 0; r < 16; ++r) { acc0[0][r] = 0.f; acc0[1][r] = 0.f; }
+  float bsum0 = 0.f;
+
+  if (r0 < r1) fetch(r0);
+  for (int64_t t0 = r0; t0 < r1; t0 += CB_ROWS) {
+    __syncthreads();  // previous tile's LDS readers are done
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int f = tid + 256 * u;
+      *reinterpret_cast<float4*>(s_c0 + (f >> 5) * CB_C0 + 4 * (f & 31)) = pc[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int f = tid + 256 * u;
+      *reinterpret_cast<float4*>(s_cin + (f >> 4) * CB_CIN + 4 * (f & 15)) = pi[u];
+    }
+    if (tid < CB_ROWS) {
+      const int64_t m = t0 + tid;
+      float a = 0.f, b = 0.f, c = 0.f, ds = 0.f;
+      if (m < r1 && m < M) {
+        const float4 gg = reinterpret_cast<const float4*>(g)[m];
+        const float* o = O3 + m * 32;
+        const float s0 = sigmoidf_(o[0]), s1 = sigmoidf_(o[1]), s2 = sigmoidf_(o[2]);
+        a = gg.x * (s0 * (1.0f - s0));
+        b = gg.y * (s1 * (1.0f - s1));
+        c = gg.z * (s2 * (1.0f - s2));
+        ds = gg.w * expf(fminf(fmaxf(O16[m * 32], -EXP_MAX), EXP_MAX));
+      }
+      s_do3[tid * 4 + 0] = a;
+      s_do3[tid * 4 + 1] = b;
+      s_do3[tid * 4 + 2] = c;
+      s_do3[tid * 4 + 3] = ds;
+    }
+    __syncthreads();
+    if (t0 + CB_ROWS < r1) fetch(t0 + CB_ROWS);  // in flight during this tile's compute
+    // ---- VALU: dWc1 / dbc1 columns, then dC0 (row r = tid / 4, 32 columns)
+#pragma unroll 16
+    for (int r = 0; r < CB_ROWS; ++r) {
+      const float c0 = s_c0[r * CB_C0 + jw];
+      const float d0 = s_do3[r * 4 + nw];
+      w1a += d0 * c0;
+      if (nw == 0) {
+        const float d1 = s_do3[r * 4 + 1];
+        w1b += d1 * c0;
+        if (jw == 0) b1b += d1;
+      }
+      if (jw == 0) b1 += d0;
+    }
+    {
+      const int r = tid >> 2, jb = (tid & 3) * 32;
+      const float d0 = s_do3[r * 4 + 0], d1 = s_do3[r * 4 + 1], d2 = s_do3[r * 4 + 2];
+      const float* crow = s_c0 + r * CB_C0 + jb;
+      float* drow = s_dc0 + r * CB_C0 + jb;
+#pragma unroll 8
+      for (int j = 0; j < 32; ++j) {
+        const float v = d0 * s_w1[jb + j] + d1 * s_w1[128 + jb + j] + d2 * s_w1[256 + jb + j];
+        drow[j] = crow[j] > 0.f ? v : 0.f;
+      }
+    }
+    __syncthreads();
+    // ---- MFMA: dWc0 (wave w -> rows 32w..), bias sums; dgeo partial over contraction half w >> 1
+#pragma unroll 16
+    for (int st = 0; st < CB_ROWS / 2; ++st) {
+      const int row = 2 * st + lh;
+      const float av = s_dc0[row * CB_C0 + 32 * wave + li];
+      bsum0 += av;
+      acc0[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, s_cin[row * CB_CIN + li], acc0[0], 0, 0, 0);
+      acc0[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, s_cin[row * CB_CIN + 32 + li], acc0[1], 0, 0, 0);
+    }
+    {
+      const int rb = wave & 1, kh = wave >> 1;
+      for (int r = 0; r < 16; ++r) accg[r] = 0.f;
+      const float* arow = s_dc0 + (rb * 32 + li) * CB_C0 + 64 * kh;
+      const float* brow = s_wt + li * CB_WT + 64 * kh;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // 16 k per slab: lane half lh owns k = 16q + 8lh + t
+        const float4 a0 = *reinterpret_cast<const float4*>(arow + 16 * q + 8 * lh);
+        const float4 a1 = *reinterpret_cast<const float4*>(arow + 16 * q + 8 * lh + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(brow + 16 * q + 8 * lh);
+        const float4 bb = *reinterpret_cast<const float4*>(brow + 16 * q + 8 * lh + 4);
+        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.x, a0.x, accg, 0, 0, 0);
+        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.y, a0.y, accg, 0, 0, 0);
+        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.z, a0.z, accg, 0, 0, 0);
+        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.w, a0.w, accg, 0, 0, 0);
+        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.x, a1.x, accg, 0, 0, 0);
+        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.y, a1.y, accg, 0, 0, 0);
+        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.z, a1.z, accg, 0, 0, 0);
+        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.w, a1.w, accg, 0, 0, 0);
+      }
+      // lane li holds row rb*32 + li; register 4q + e holds column 8q + 4lh + e
+      float* grow = s_geo + (kh * CB_ROWS + rb * 32 + li) * CB_GEO;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 8 * q + 4 * lh + e;
+          if (c < 15) grow[c] = accg[4 * q + e];
+        }
+    }
+    __syncthreads();
+    // ---- dO16 rows: [ds, dgeo (sum of the two halves), 0 x 16]
+    for (int f = tid; f < CB_ROWS * 8; f += 256) {
+      const int r = f >> 3, c4 = f & 7;
+      const int64_t m = t0 + r;
+      if (m >= r1) continue;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (c4 < 4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 4 * c4 + e;  // dO16 column
+          if (c == 0) v[e] = s_do3[r * 4 + 3];
+          else if (c <= 15) v[e] = s_geo[r * CB_GEO + c - 1] + s_geo[(CB_ROWS + r) * CB_GEO + c - 1];
+        }
+      }
+      tail_st4(dO16 + m * 32 + 4 * c4, make_float4(v[0], v[1], v[2], v[3]));
+    }
+  }
+  // ---- this split's slab: weight sums, bias sums (lane halves combined)
+  float* P = partial + (int64_t)blockIdx.x * slab;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int n = (r & 3) + 8 * (r >> 2) + 4 * lh;
+    P[off_w0 + (int64_t)(32 * wave + n) * 64 + li] = acc0[0][r];
+    P[off_w0 + (int64_t)(32 * wave + n) * 64 + 32 + li] = acc0[1][r];
+  }
+  const float v0 = bsum0 + __shfl_xor(bsum0, 32, 64);
+  if (lh == 0) P[off_b0 + 32 * wave + li] = v0;
+  // colour_out: rows 0..2 from the VALU sums, rows 3..31 zero; its bias likewise
+  for (int i = tid; i < 32 * 128; i += 256) {
+    const int n = i >> 7;
+    if (n >= 3) P[off_w1 + i] = 0.f;
+  }
+  P[off_w1 + (int64_t)nw * 128 + jw] = w1a;
+  if (nw == 0) P[off_w1 + 128 + jw] = w1b;
+  if (tid >= 3 && tid < 32) P[off_b1 + tid] = 0.f;
+  if (tid == 0) {
+    P[off_b1 + 0] = b1;
+    P[off_b1 + 1] = b1b;
+  }
+  if (tid == 128) P[off_b1 + 2] = b1;
+}
+}  // namespace nerf_mlp
+
