@@ -15,7 +15,6 @@ Prints ONE JSON line on rank 0 (contract in the task statement), with
 """
 import argparse
 import json
-import math
 import os
 import sys
 import time

@@ -19,8 +19,6 @@ fails in the reference's constructor (FrequencyEncoder without in_dim) and raise
 from __future__ import annotations
 
 import ctypes
-import re
-import warnings
 from collections import OrderedDict
 from typing import Dict, List, Optional
 

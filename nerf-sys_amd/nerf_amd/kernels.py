@@ -3,7 +3,7 @@ current stream, raise on a non-zero status.  No autograd here (see ray_rendering
 from __future__ import annotations
 
 import ctypes
-from typing import Optional, Sequence
+from typing import Sequence
 
 import torch
 

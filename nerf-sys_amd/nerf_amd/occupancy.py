@@ -11,7 +11,6 @@ restatement).  Kernels: ``csrc/occ.hip``.
 from __future__ import annotations
 
 import ctypes
-import math
 from typing import Callable, Optional
 
 import torch

@@ -13,7 +13,6 @@ in ``extras`` when ``return_extras=True``.  The occupancy renderer (render_rays_
 """
 from __future__ import annotations
 
-import warnings
 from typing import Optional, Tuple
 
 import torch

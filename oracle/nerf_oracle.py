@@ -21,7 +21,6 @@ from __future__ import annotations
 
 import math
 from collections import OrderedDict
-from typing import Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F

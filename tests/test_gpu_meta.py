@@ -9,12 +9,10 @@ each tensor's scale (the reference's own CPU fp32 GEMMs differ from any other su
 import types
 from collections import OrderedDict
 
-import numpy as np
 import pytest
 import torch
 
 from oracle import meta_oracle as MO
-from oracle import nerf_oracle as O
 from tests.golden_io import load, mlp_params
 
 pytestmark = pytest.mark.gpu

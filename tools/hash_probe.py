@@ -4,7 +4,6 @@ sample distribution: 4096 random pixels x 96 stratified samples through the [-1.
 production 16-level grid (2^20 entries, F=2).  Times subsets of levels by passing sub-grids."""
 import os
 import sys
-import ctypes
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "nerf-sys_amd"), ROOT]

@@ -10,7 +10,6 @@ Writes one JSON line per checkpoint to stdout (and --out): step, wall seconds of
 """
 import argparse
 import json
-import math
 import os
 import sys
 import time
