@@ -4,7 +4,9 @@ pipelines/online_stage/runtime_adapt.py:305-307) for autograd-driven models (con
 
 Every parameter of the given groups is re-pointed to a view of ONE flat fp32 buffer and its ``.grad`` to a view
 of ONE flat gradient buffer (autograd accumulates into those views in place), so a step is two launches:
-``nerf_grad_sqnorm`` (clip) and ``nerf_adam`` (per-group learning rates as segments), no host sync.
+``nerf_grad_sqnorm`` (clip) and ``nerf_adam`` (per-group learning rates as segments), no host sync.  The
+parameters are tagged ``_nerf_flat_grad``: the Instant-NGP hash-table backward then scatter-adds straight into
+the table's ``.grad`` view (gradients of FlatAdam-owned parameters come from ``loss.backward()``).
 """
 from __future__ import annotations
 
@@ -39,6 +41,9 @@ class FlatAdam:
                     self.flat[o:o + k].copy_(p.detach().reshape(-1).float())
                     p.data = self.flat[o:o + k].view_as(p)
                     p.grad = self.grad[o:o + k].view_as(p)
+                    # HIP ops may accumulate this parameter's gradient in place (e.g. the hash-table scatter);
+                    # use loss.backward(), not torch.autograd.grad, for parameters owned by FlatAdam
+                    p._nerf_flat_grad = True
                     o += k
                 self.seg_off.append(o)
                 self.seg_lr.append(float(g["lr"]))

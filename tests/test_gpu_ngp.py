@@ -285,3 +285,26 @@ def test_two_streams_do_not_share_workspaces():
     for i in range(2):
         for a, b in zip(out[i], ref[i]):
             assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_table_grad_in_place_for_flat_adam_params():
+    """A FlatAdam-owned hash table (tagged _nerf_flat_grad, .grad a preset view) receives its gradient by the
+    scatter-add straight into .grad, equal to the autograd-accumulated one; an existing gradient is added to."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from nerf_amd.ngp import InstantNGP
+    torch.manual_seed(2)
+    m = InstantNGP(scene_box=torch.tensor([[-1.5] * 3, [1.5] * 3]), hidden=64, sigma_depth=2, color_hidden=64,
+                   color_depth=2, dir_encoding="spherical",
+                   hash_enc_conf=dict(levels=8, features_per_level=2, log2_hashmap_size=14, min_res=8, max_res=256,
+                                      interpolation="Linear")).to("cuda")
+    g = torch.Generator().manual_seed(4)
+    x = torch.cat([torch.rand(5000, 3, generator=g) * 3 - 1.5,
+                   torch.nn.functional.normalize(torch.randn(5000, 3, generator=g), dim=-1)], -1).to("cuda")
+    t = m.xyz_encoder.hash_table
+    m(x).square().sum().backward()
+    ref = t.grad.detach().clone()
+    t.grad = torch.full_like(t, 0.5)
+    t._nerf_flat_grad = True
+    m(x).square().sum().backward()
+    assert torch.allclose(t.grad, ref + 0.5, rtol=1e-5, atol=1e-6)
