@@ -54,7 +54,8 @@ struct NgpPlan {
   int cin_buf, cin_ld, cin_kpad, geo, dir_mode, sh_levels, dir_dim;
   int sigmoid;
   int g0, g1;            // gradient tiles (ld 68)
-  int dsig;              // d sigma_raw per tile row (64 floats)
+  int dsig;              // d sigma_raw per tile row (64 floats; backward plan)
+  int sraw;              // sigma_raw per tile row (64 floats; forward plan, -1 in the backward plan)
   int smem_floats;
   int nsb;               // weight-gradient 32x32 blocks: layer, n-block, k-block
   int sb_layer[NGP_MAX_SB], sb_nb[NGP_MAX_SB], sb_kb[NGP_MAX_SB];
@@ -112,21 +113,31 @@ bool make_plan(const NerfNgpNet& n, bool save, NgpPlan& P) {
   P.enc_buf = take(P.enc_ld);
   P.cin_ld = P.cin_kpad + 4;
   P.cin_buf = take(P.cin_ld);
-  P.g0 = take(68);
-  P.g1 = take(68);
-  P.dsig = s; s += NGP_ROWS;
+  // backward plan: two gradient tiles (g0 also holds the raw head output, g1 the rgb logits) and d sigma_raw.
+  // forward plan: activations ping-pong through two tiles (the head output too; its sigma_raw column is copied
+  // to sraw before the colour layers overwrite it), which halves the LDS of a workgroup so two fit per CU.
   int pp[2] = {-1, -1};
-  if (!save) { pp[0] = take(68); pp[1] = take(68); }
+  if (save) {
+    P.g0 = take(68);
+    P.g1 = take(68);
+    P.dsig = s; s += NGP_ROWS;
+    P.sraw = -1;
+  } else {
+    pp[0] = take(68);
+    pp[1] = take(68);
+    P.g0 = P.g1 = P.dsig = -1;
+    P.sraw = s; s += NGP_ROWS;
+  }
   int prev_out = P.enc_buf, prev_ld = P.enc_ld;
   for (int l = 0; l < P.nl; ++l) {
     NgpLayer& L = P.ly[l];
     if (l == P.head + 1) { prev_out = P.cin_buf; prev_ld = P.cin_ld; }
     L.in_buf = prev_out;
     L.in_ld = prev_ld;
-    if (l == P.head) { L.out_buf = P.g0; L.out_ld = 68; }           // raw [sigma, geo]: aliases a grad tile
+    if (!save) { L.out_buf = pp[l & 1]; L.out_ld = 68; }
+    else if (l == P.head) { L.out_buf = P.g0; L.out_ld = 68; }           // raw [sigma, geo]: aliases a grad tile
     else if (l == P.nl - 1) { L.out_buf = P.g1; L.out_ld = 68; }    // raw rgb logits
-    else if (save) { L.out_buf = take(L.Npad + 4); L.out_ld = L.Npad + 4; }
-    else { L.out_buf = pp[l & 1]; L.out_ld = 68; }
+    else { L.out_buf = take(L.Npad + 4); L.out_ld = L.Npad + 4; }
     prev_out = L.out_buf;
     prev_ld = L.out_ld;
   }
@@ -520,6 +531,7 @@ __device__ __forceinline__ void build_cin_row(const NgpPlan& P, float* smem, con
                                               int64_t M, int r) {
   float* c = smem + P.cin_buf + r * P.cin_ld;
   const float* h = smem + P.ly[P.head].out_buf + r * P.ly[P.head].out_ld;
+  if (P.sraw >= 0) smem[P.sraw + r] = h[0];
   for (int k = 0; k < P.geo; ++k) c[k] = h[1 + k];
   float v[27];
   float x = 0.f, y = 0.f, z = 1.f;
@@ -578,7 +590,7 @@ __global__ __launch_bounds__(256) void ngp_fwd_kernel(NgpPlan P, const float* __
     const int64_t m = m0 + r;
     if (m < M) {
       const float* o = smem + P.ly[P.nl - 1].out_buf + r * P.ly[P.nl - 1].out_ld;
-      const float sr = smem[P.ly[P.head].out_buf + r * P.ly[P.head].out_ld];
+      const float sr = P.sraw >= 0 ? smem[P.sraw + r] : smem[P.ly[P.head].out_buf + r * P.ly[P.head].out_ld];
       float c0 = o[0], c1 = o[1], c2 = o[2];
       if (P.sigmoid) { c0 = nerf_mlp::sigmoidf_(c0); c1 = nerf_mlp::sigmoidf_(c1); c2 = nerf_mlp::sigmoidf_(c2); }
       const float sg = expf(fminf(fmaxf(sr, -nerf_mlp::EXP_MAX), nerf_mlp::EXP_MAX));
