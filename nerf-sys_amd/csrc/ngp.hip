@@ -22,6 +22,7 @@
 // workgroup writes ONE slab of the packed gradient; a deterministic reduce sums the slabs.
 #include <cstdlib>
 #include <mutex>
+#include <set>
 
 #include "mlp_common.hpp"
 
@@ -811,14 +812,16 @@ __global__ void ngp_reduce_kernel(const float* __restrict__ partial, int64_t tot
   dw[i] = s;
 }
 
-// dynamic LDS above 64 KB must be allowed per kernel (once per process; immutable afterwards)
+// dynamic LDS above 64 KB must be allowed per kernel, once per process.  Keyed by the kernel's address: the
+// ngp_bwd_kernel<NSB> instantiations share one function type, so a per-type once_flag would set only the first.
 template <typename K>
 void allow_lds(K kernel) {
-  static std::once_flag once;
-  std::call_once(once, [&] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-  });
+  static std::mutex mu;
+  static std::set<const void*> done;
+  const void* f = reinterpret_cast<const void*>(kernel);
+  std::lock_guard<std::mutex> lock(mu);
+  if (done.insert(f).second)
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
 int bwd_grid(int64_t M) {

@@ -308,3 +308,36 @@ def test_table_grad_in_place_for_flat_adam_params():
     t._nerf_flat_grad = True
     m(x).square().sum().backward()
     assert torch.allclose(t.grad, ref + 0.5, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("depths", [(3, 3), (2, 3)])
+def test_ngp_deep_config_vs_oracle(N, depths):
+    """Deeper MetaNGP nets ((3, 3): 24 weight-gradient blocks -> the ngp_bwd_kernel<6> instantiation with a
+    158 KB backward LDS plan, whose dynamic-LDS attribute must be set separately from <4>'s) against the
+    oracle: forward and every gradient."""
+    from nerf_amd.ngp import InstantNGP
+    sd, cd = depths
+    torch.manual_seed(11)
+    box = torch.tensor([[-1.5] * 3, [1.5] * 3])
+    net = InstantNGP(scene_box=box, hidden=64, sigma_depth=sd, color_hidden=64, color_depth=cd,
+                     dir_encoding="spherical",
+                     hash_enc_conf=dict(levels=8, features_per_level=2, log2_hashmap_size=12, min_res=8, max_res=128,
+                                        interpolation="Linear")).to(DEV)
+    with torch.no_grad():
+        net.xyz_encoder.hash_table.uniform_(-0.1, 0.1)
+    M = 777
+    g = torch.Generator().manual_seed(3)
+    x_d = torch.cat([torch.rand(M, 3, generator=g) * 3 - 1.5,
+                     torch.nn.functional.normalize(torch.randn(M, 3, generator=g), dim=-1)], -1)
+    gup = torch.randn(M, 4, generator=g)
+    out = net(x_d.to(DEV))
+    (out * gup.to(DEV)).sum().backward()
+    w = OrderedDict((n, p.detach().cpu().clone().requires_grad_(True)) for n, p in net.named_parameters())
+    table = w.pop("xyz_encoder.hash_table")
+    res, _ = NO.hash_resolutions(8, 8, 128)
+    ref = NO.ngp_forward(w, table, x_d, box, res, 12, 2, sigma_depth=sd, color_depth=cd)
+    assert _err(out, ref) <= 2e-5 * max(1.0, ref.abs().max().item())
+    grads = torch.autograd.grad((ref * gup).sum(), list(w.values()) + [table])
+    for (n, _), gr in zip(list(w.items()) + [("xyz_encoder.hash_table", table)], grads):
+        got = dict(net.named_parameters())[n].grad
+        assert _err(got, gr) <= 1e-4 * max(1.0, gr.abs().max().item()), n
