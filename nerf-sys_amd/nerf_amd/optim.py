@@ -15,11 +15,12 @@ from typing import Dict, List
 import torch
 
 from . import kernels as K
+from .dp import allreduce_flat
 
 
 class FlatAdam:
     def __init__(self, groups: List[Dict], betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 grad_clip=1.0):
+                 grad_clip=1.0, world_size: int = 1):
         if len(groups) > 8:
             raise ValueError("at most 8 parameter groups (nerf_adam segments)")
         params = [p for g in groups for p in g["params"]]
@@ -49,6 +50,7 @@ class FlatAdam:
                 self.seg_lr.append(float(g["lr"]))
         self.params = params
         self.betas, self.eps, self.wd, self.grad_clip = betas, eps, weight_decay, grad_clip
+        self.world_size = int(world_size)
         self.step_count = 0
 
     def zero_grad(self):
@@ -58,7 +60,15 @@ class FlatAdam:
             if p.grad is None or not lo <= p.grad.data_ptr() < hi:
                 raise RuntimeError("a parameter's .grad left the flat buffer (do not set grads to None)")
 
+    def allreduce_grads(self):
+        """Data parallel (as for the vanilla step): ONE all-reduce of the flat gradient buffer, then
+        the mean over ranks (each rank's loss is its local-batch mean) — the gradient DDP would produce."""
+        if self.world_size > 1:
+            allreduce_flat(self.grad, self.world_size)
+            self.grad.mul_(1.0 / self.world_size)
+
     def step(self):
+        self.allreduce_grads()
         self.step_count += 1
         if self.grad_clip is not None and self.grad_clip > 0:
             K.grad_sqnorm(self.grad, self.partials)

@@ -84,3 +84,38 @@ def test_two_rank_allreduce_equals_full_batch():
     rays, gt, us = _batch()
     full = _flat_grad(O.init_vanilla_params(3), rays, gt, us, inv_count(rays.shape[0], 1))
     torch.testing.assert_close(dp, full, rtol=1e-4, atol=1e-7)
+
+
+def _flat_adam_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "nerf-sys_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from nerf_amd.optim import FlatAdam
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(5, 3)), torch.nn.Parameter(torch.randn(7))]
+    opt = FlatAdam([{"params": ps[:1], "lr": 1e-3}, {"params": ps[1:], "lr": 1e-2}], world_size=world)
+    with torch.no_grad():
+        for i, p in enumerate(ps):
+            p.grad.copy_(torch.full_like(p, float(rank + 1) * (i + 1)))
+    opt.allreduce_grads()
+    q.put((rank, [p.grad.clone() for p in ps]))
+    dist.destroy_process_group()
+
+
+def test_flat_adam_data_parallel_mean_gloo():
+    """FlatAdam's data-parallel exchange (the container / NGP path): one all-reduce of the flat gradient buffer
+    and the mean over ranks, landing in every parameter's .grad view."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_flat_adam_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        g0, g1 = out[r]
+        assert torch.allclose(g0, torch.full((5, 3), 1.5)) and torch.allclose(g1, torch.full((7,), 3.0))

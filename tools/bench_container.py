@@ -12,6 +12,7 @@ Prints one JSON line: rays/s, ms/step, per-kernel-class times (HIP events), the 
 roofline and a CPU baseline (the oracle's stratified NGP container step on a bounded sample).
 
   python tools/bench_container.py [--steps 20] [--warmup 40] [--batch 4096]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/bench_container.py  (data parallel)
 """
 import argparse
 import json
@@ -108,8 +109,10 @@ def cpu_baseline(seconds):
                       f"in {el:.1f}s"}
 
 
-def build_step(a, dev):
-    """The container, FlatAdam and one train step closure (step -> loss)."""
+def build_step(a, dev, rank=0, world=1):
+    """The container, FlatAdam and one train step closure (step -> loss).  world > 1: data parallel — every rank
+    draws its own ray batch (dp.shard_seed) and FlatAdam all-reduces the flat gradient."""
+    from nerf_amd.dp import shard_seed
     from nerf_amd.container import MetaContainer
     from nerf_amd.losses import compute_mse_loss
     from nerf_amd.optim import FlatAdam
@@ -129,13 +132,13 @@ def build_step(a, dev):
     model = model.to(dev).train()
     lr = {"encoding": 1e-2, "sigma": 2e-3, "color": 2e-3, "background": 1e-3}
     groups = [{"params": g["params"], "lr": lr[k]} for k, g in model.get_param_groups().items()]
-    opt = FlatAdam(groups, grad_clip=1.0)
+    opt = FlatAdam(groups, grad_clip=1.0, world_size=world)
     rb = RayBatcher(scene, dev)
     P = SimpleNamespace(ray_samples=96, chunk_points=262_144 * 17, color_space="linear")
 
     def one(step):
         model.maybe_update_expert_occupancies(step)
-        rays, gt = rb.batch(a.batch, seed=step)
+        rays, gt = rb.batch(a.batch, seed=shard_seed(step, rank, world))
         opt.zero_grad()
         loss = compute_mse_loss(P, model, {"rays": rays, "rgbs": gt})
         loss.backward()
@@ -147,20 +150,36 @@ def build_step(a, dev):
 
 def main():
     a = parse()
-    dev = torch.device("cuda", 0)
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
     from nerf_amd import ngp as G
 
-    one, model = build_step(a, dev)
+    one, model = build_step(a, dev, rank, world)
     for s in range(a.warmup):
         loss = one(s)
     assert model.occ_ready, "occupancy warm-up did not finish"
-    torch.cuda.synchronize()
+
+    def fence():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    fence()
     t0 = time.perf_counter()
     for s in range(a.warmup, a.warmup + a.steps):
         loss = one(s)
-    torch.cuda.synchronize()
+    fence()
     el = time.perf_counter() - t0
+    if world > 1:  # the job's time is the slowest rank's
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
     # per-kernel-class times from HIP events in separate steps
     G.TIMING.enabled = True
     for s in range(a.steps):
@@ -185,12 +204,12 @@ def main():
     out = {
         "metric": "rays/sec (train step), production MoE container: 4 Instant-NGP experts + occupancy rendering "
                   "+ background MLP (SURVEY §8f rows 1-3), 800x800 Lego-style",
-        "value": round(a.batch * a.steps / el, 1), "unit": "rays/s", "n_gpus": 1, "steps": a.steps,
+        "value": round(a.batch * world * a.steps / el, 1), "unit": "rays/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True, "dtype": "f32",
         "data": "synthetic",
         "config": {"workload": "MetaContainer(4 x MetaNGP 16x2^20, 2x64 / 2x64, SH), soft routing bm 1.05, "
                                "occupancy 128^3 x 4 levels, bg MLP 32, autograd train step + FlatAdam",
-                   "rays_per_step": a.batch},
+                   "rays_per_step": a.batch * world, "parallelism": f"dp{world}"},
         "kernels_ms_per_step": {k: round(v, 4) for k, v in ms.items()},
         "launches_per_step": {k: round(v, 2) for k, v in n_launch.items()},
         "mean_launch_ms": {k: round(v, 4) for k, v in launch.items()},
@@ -199,8 +218,12 @@ def main():
         "samples_per_step": round(rows.get("mlp_fwd", 0) / a.steps),
         "final_loss": round(float(loss.item()), 6),
     }
-    out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(a.cpu_seconds)
-    print(json.dumps(out), flush=True)
+    out["cpu_baseline"] = None if (a.no_cpu_baseline or world > 1) else cpu_baseline(a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
