@@ -416,7 +416,8 @@ int nerf_reptile_update(int n_tensors, float* const* theta, const float* const* 
  *     has_near / has_far = the override; eps 1e-6, invalid -> inf);
  *   write pass (pos = exclusive scan of flags, n+1 entries): kept pixel g -> row pos[g] of out_rays (8 floats,
  *     16-byte aligned), out_rgb (3 floats, pixel / 255, :112) and out_idx (image_index[image of g], :117).
- * c2w (n_images x 12), intrinsics (n_images x 4: fx fy cx cy), image_index (n_images), aabb (6): device. */
+ * c2w (n_images x 12), intrinsics (n_images x 4: fx fy cx cy), image_index (n_images), aabb (6): device.
+ * n_images * H * W < 2^31 (int32 row positions; RamRaysDataset builds runs of <= 2^26 pixels). */
 int nerf_dataset_rays(const float* c2w, const float* intrinsics, const int32_t* image_index, int n_images, int H,
                       int W, int center_pixels, const float* aabb, int has_near, float near_v, int has_far,
                       float far_v, const uint8_t* images, const uint8_t* masks, int32_t* flags, const int32_t* pos,

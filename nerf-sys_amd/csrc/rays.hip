@@ -349,6 +349,7 @@ extern "C" int nerf_dataset_rays(const float* c2w, const float* intrinsics, cons
   if (n_images == 0) return NERF_OK;
   NERF_CHECK_ARG(c2w && intrinsics && image_index && aabb);
   const int64_t n = (int64_t)n_images * H * W;
+  NERF_CHECK_ARG(n < INT32_MAX);  // row positions are an int32 scan
   DatasetArgs A{c2w, intrinsics, image_index, H, W, center_pixels, aabb, has_near, has_far, near_v, far_v, images,
                 masks};
   if (pos == nullptr) {
