@@ -305,6 +305,16 @@ int nerf_occ_march_multi(const NerfOccGrid* grids, const uint8_t* const* binarie
                          float cone_angle, int stratified, uint64_t seed, int max_steps, int32_t* counts,
                          const int32_t* offsets, int32_t* ray_idx, float* t0, float* t1, hipStream_t stream);
 
+/* nerf_occ_march_multi with the write pass replaced by a copy.  Count pass (offsets == NULL): counts as above, and
+ * the first `cap` segments [t0, t1] of pair j = k*N + r are kept in stage (K*N*cap float pairs, 8-byte aligned).
+ * Emit pass (offsets given, same arguments and seed): pairs with counts[j] <= cap are copied from stage, longer
+ * pairs are marched again; the output equals nerf_occ_march_multi's write pass exactly. */
+int nerf_occ_march_multi_staged(const NerfOccGrid* grids, const uint8_t* const* binaries, const float* boxes,
+                                const float* steps, int K, const float* rays, int64_t N, float near_plane,
+                                float far_plane, float cone_angle, int stratified, uint64_t seed, int max_steps,
+                                int32_t* counts, float* stage, int cap, const int32_t* offsets, int32_t* ray_idx,
+                                float* t0, float* t1, hipStream_t stream);
+
 /* Exclusive scan of n int32 into out[n+1] (out[n] = total); in / out 16-byte aligned. Reduce-then-scan over
  * 2048-element tiles: 3 launches, 12 B of HBM traffic per element. */
 int64_t nerf_scan_workspace_bytes(int64_t n);

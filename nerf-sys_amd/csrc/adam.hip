@@ -56,33 +56,91 @@ __global__ __launch_bounds__(1024) void sqnorm_kernel(const float* __restrict__ 
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
+__device__ __forceinline__ float clip_scale(const float* __restrict__ part, float max_norm, float* red) {
+  if (!(part && max_norm > 0.f)) return 1.0f;
+  const float s = block_sum(threadIdx.x < NPART ? part[threadIdx.x] : 0.f, red);
+  return fminf(max_norm / (sqrtf(s) + 1e-6f), 1.0f);
+}
+
+struct AdamHyper {
+  float b2, omb1, omb2, eps, wd, bc2s;
+};
+
+// one element, torch's single-tensor Adam order; elements outside every segment are returned unchanged
+__device__ __forceinline__ void adam_elem(int64_t i, const Segs& segs, const AdamHyper& h, float scale, float g,
+                                          float& p, float& m, float& v) {
+  if (i < segs.off[0] || i >= segs.off[segs.n]) return;
+  int sgi = 0;
+  while (sgi + 1 < segs.n && i >= segs.off[sgi + 1]) ++sgi;
+  const float lr = segs.lr[sgi];  // the step size lr / bc1
+  float gi = g * scale;
+  if (h.wd != 0.f) gi = gi + h.wd * p;
+  m = m + h.omb1 * (gi - m);
+  v = v * h.b2 + h.omb2 * (gi * gi);
+  const float denom = sqrtf(v) / h.bc2s + h.eps;
+  p = p + (-lr) * (m / denom);
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 nt_load(const float4* q) {
+  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(q));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void nt_store(float4 a, float4* q) {
+  f32x4 v;
+  v.x = a.x; v.y = a.y; v.z = a.z; v.w = a.w;
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(q));
+}
+
+__device__ __forceinline__ void adam4(int64_t e0, const Segs& segs, const AdamHyper& h, float scale, float4 g,
+                                      float4& p, float4& m, float4& v) {
+  if (e0 + 4 <= segs.off[0] || e0 >= segs.off[segs.n]) return;
+  adam_elem(e0, segs, h, scale, g.x, p.x, m.x, v.x);
+  adam_elem(e0 + 1, segs, h, scale, g.y, p.y, m.y, v.y);
+  adam_elem(e0 + 2, segs, h, scale, g.z, p.z, m.z, v.z);
+  adam_elem(e0 + 3, segs, h, scale, g.w, p.w, m.w, v.w);
+}
+
+// VEC: p, g, m, v 16-byte aligned -> float4 streams (28 B/element of HBM traffic; the scalar form ran at 4.7 TB/s
+// over 134 M elements), the n % 4 tail element-wise.
+template <bool VEC>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n, Segs segs,
-                                                   float b2, float omb1, float omb2, float eps, float wd, float bc2s,
-                                                   const float* __restrict__ part, float max_norm) {
+                                                   AdamHyper h, const float* __restrict__ part, float max_norm) {
   __shared__ float red[17];
-  float scale = 1.0f;
-  if (part && max_norm > 0.f) {
-    const float s = block_sum(threadIdx.x < NPART ? part[threadIdx.x] : 0.f, red);
-    const float norm = sqrtf(s);
-    scale = fminf(max_norm / (norm + 1e-6f), 1.0f);
+  const float scale = clip_scale(part, max_norm, red);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i0 = 0;
+  if (VEC) {
+    const int64_t n4 = n / 4;
+    float4* p4 = reinterpret_cast<float4*>(p);
+    float4* m4 = reinterpret_cast<float4*>(m);
+    float4* v4 = reinterpret_cast<float4*>(v);
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    // two float4 groups per thread per iteration (8 independent 16-B loads in flight), streaming stores
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + stride < n4; i += 2 * stride) {
+      const int64_t j = i + stride;
+      float4 pa = p4[i], ga = nt_load(g4 + i), ma = m4[i], va = v4[i];
+      float4 pb = p4[j], gb = nt_load(g4 + j), mb = m4[j], vb = v4[j];
+      adam4(4 * i, segs, h, scale, ga, pa, ma, va);
+      adam4(4 * j, segs, h, scale, gb, pb, mb, vb);
+      p4[i] = pa; nt_store(ma, m4 + i); nt_store(va, v4 + i);
+      p4[j] = pb; nt_store(mb, m4 + j); nt_store(vb, v4 + j);
+    }
+    for (; i < n4; i += stride) {
+      float4 pa = p4[i], ga = g4[i], ma = m4[i], va = v4[i];
+      adam4(4 * i, segs, h, scale, ga, pa, ma, va);
+      p4[i] = pa; m4[i] = ma; v4[i] = va;
+    }
+    i0 = 4 * n4;
   }
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    int sgi = 0;
-    while (sgi + 1 < segs.n && i >= segs.off[sgi + 1]) ++sgi;
-    if (i < segs.off[0] || i >= segs.off[segs.n]) continue;
-    const float lr = segs.lr[sgi];
-    float gi = g[i] * scale;
-    float pi = p[i];
-    if (wd != 0.f) gi = gi + wd * pi;
-    float mi = m[i];
-    mi = mi + omb1 * (gi - mi);
-    float vi = v[i] * b2 + omb2 * (gi * gi);
-    const float denom = sqrtf(vi) / bc2s + eps;
-    pi = pi + (-lr) * (mi / denom);  // lr here is the step size lr/bc1
-    m[i] = mi;
-    v[i] = vi;
-    p[i] = pi;
+  for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float pp = p[i], mm = m[i], vv = v[i];
+    adam_elem(i, segs, h, scale, g[i], pp, mm, vv);
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
   }
 }
 
@@ -106,13 +164,16 @@ extern "C" int nerf_adam(float* p, const float* g, float* m, float* v, int64_t n
   for (int i = 0; i < n_seg; ++i) s.lr[i] = (float)(seg_lr_host[i] / bc1);
   for (int i = 0; i < n_seg; ++i) NERF_CHECK_ARG(s.off[i] <= s.off[i + 1]);
   NERF_CHECK_ARG(s.off[0] >= 0 && s.off[n_seg] <= n);
-  const float bc2s = (float)std::sqrt(bc2);
-  int64_t blocks = nerf_cdiv(n, 256);
-  if (blocks > 2048) blocks = 2048;
+  const AdamHyper h{(float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), eps, weight_decay,
+                    (float)std::sqrt(bc2)};
+  const bool vec = nerf_aligned16(p) && nerf_aligned16(g) && nerf_aligned16(m) && nerf_aligned16(v);
+  int64_t blocks = nerf_cdiv(vec ? n / 4 : n, 256);
+  if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
-  adam_kernel<<<(unsigned)blocks, 256, 0, stream>>>(p, g, m, v, n, s, (float)beta2, (float)(1.0 - beta1),
-                                                      (float)(1.0 - beta2), eps, weight_decay, bc2s, partials,
-                                                      max_norm);
+  if (vec)
+    adam_kernel<true><<<(unsigned)blocks, 256, 0, stream>>>(p, g, m, v, n, s, h, partials, max_norm);
+  else
+    adam_kernel<false><<<(unsigned)blocks, 256, 0, stream>>>(p, g, m, v, n, s, h, partials, max_norm);
   return nerf_launch_status();
 }
 

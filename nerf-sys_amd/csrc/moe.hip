@@ -197,23 +197,28 @@ __device__ __forceinline__ void bg_enc(const float* __restrict__ d, int64_t ds, 
   e[15] = 0.5900435899266435f * x * (xx - 3.0f * yy);
 }
 
-// packed weights: W1 [H][16] | b1 [H] | W2 [3][H] | b2 [3]
-__device__ __forceinline__ void bg_forward_row(const float* sw, int H, const float e[16], float h[BG_MAXH], float o[3]) {
+// packed weights: W1 [H][16] | b1 [H] | W2 [3][H] | b2 [3].  The hidden layer is consumed as it is produced (o
+// accumulates h_j in j order, the same order as a separate second loop) so no H-long register array is indexed
+// with a runtime bound (that spills to scratch); hs (LDS, may be null) keeps h for the backward.
+__device__ __forceinline__ void bg_forward_row(const float* sw, int H, const float e[16], float o[3], float* hs) {
   const float* W1 = sw;
   const float* b1 = sw + 16 * H;
   const float* W2 = b1 + H;
   const float* b2 = W2 + 3 * H;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f;
   for (int j = 0; j < H; ++j) {
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) s += W1[j * 16 + i] * e[i];
-    h[j] = fmaxf(s + b1[j], 0.f);
+    const float h = fmaxf(s + b1[j], 0.f);
+    if (hs) hs[j] = h;
+    s0 += W2[j] * h;
+    s1 += W2[H + j] * h;
+    s2 += W2[2 * H + j] * h;
   }
-  for (int c = 0; c < 3; ++c) {
-    float s = 0.f;
-    for (int j = 0; j < H; ++j) s += W2[c * H + j] * h[j];
-    o[c] = s + b2[c];
-  }
+  o[0] = s0 + b2[0];
+  o[1] = s1 + b2[1];
+  o[2] = s2 + b2[2];
 }
 
 __global__ __launch_bounds__(256) void bg_fwd_kernel(const float* __restrict__ d, int64_t ds, int64_t N,
@@ -224,52 +229,71 @@ __global__ __launch_bounds__(256) void bg_fwd_kernel(const float* __restrict__ d
   __syncthreads();
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= N) return;
-  float e[16], h[BG_MAXH], o[3];
+  float e[16], o[3];
   bg_enc(d, ds, r, e);
-  bg_forward_row(sw, H, e, h, o);
+  bg_forward_row(sw, H, e, o, nullptr);
   for (int c = 0; c < 3; ++c) out[r * 3 + c] = 1.0f / (1.0f + expf(-o[c]));
 }
 
-// per-block weight-gradient slab (deterministic: fixed wave / lane reduction order)
+// Backward over BG_RAYS rays per workgroup: wave 0 recomputes each ray's row (e, h, dz, dh) into LDS, then the
+// 256 threads own parameters and sum their per-ray contributions over the block's rays in ray order (one slab per
+// block, deterministic).  The previous form (every thread looping over all 20H+3 parameters with a wave reduction
+// per parameter and runtime-indexed register arrays) took 0.22 ms for 4096 rays.
+constexpr int BG_RAYS = 64;
 __global__ __launch_bounds__(256) void bg_bwd_kernel(const float* __restrict__ d, int64_t ds, int64_t N,
                                                      const float* __restrict__ w, int H,
                                                      const float* __restrict__ gout, float* __restrict__ slab) {
   __shared__ float sw[16 * BG_MAXH + BG_MAXH + 3 * BG_MAXH + 3];
-  __shared__ float red[4][16 * BG_MAXH + BG_MAXH + 3 * BG_MAXH + 3];
+  __shared__ float es[BG_RAYS][17];
+  __shared__ float hs[BG_RAYS][BG_MAXH + 1];
+  __shared__ float dhs[BG_RAYS][BG_MAXH + 1];
+  __shared__ float dzs[BG_RAYS][4];
   const int P = 20 * H + 3;
   for (int i = threadIdx.x; i < P; i += blockDim.x) sw[i] = w[i];
   __syncthreads();
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  float e[16], h[BG_MAXH], o[3], dz[3] = {0.f, 0.f, 0.f}, dh[BG_MAXH];
-  for (int i = 0; i < 16; ++i) e[i] = 0.f;
-  for (int j = 0; j < H; ++j) { h[j] = 0.f; dh[j] = 0.f; }
-  if (r < N) {
-    bg_enc(d, ds, r, e);
-    bg_forward_row(sw, H, e, h, o);
-    for (int c = 0; c < 3; ++c) {
-      const float s = 1.0f / (1.0f + expf(-o[c]));
-      dz[c] = gout[r * 3 + c] * (s * (1.0f - s));
+  if (threadIdx.x < BG_RAYS) {
+    const int q = threadIdx.x;
+    const int64_t r = (int64_t)blockIdx.x * BG_RAYS + q;
+    float e[16], o[3], dz[3] = {0.f, 0.f, 0.f};
+    if (r < N) {
+      bg_enc(d, ds, r, e);
+      bg_forward_row(sw, H, e, o, hs[q]);
+      for (int c = 0; c < 3; ++c) {
+        const float sg = 1.0f / (1.0f + expf(-o[c]));
+        dz[c] = gout[r * 3 + c] * (sg * (1.0f - sg));
+      }
+      const float* W2 = sw + 17 * H;
+      for (int j = 0; j < H; ++j) {
+        const float g = W2[j] * dz[0] + W2[H + j] * dz[1] + W2[2 * H + j] * dz[2];
+        dhs[q][j] = hs[q][j] > 0.f ? g : 0.f;
+      }
+    } else {  // rows past N contribute zero
+#pragma unroll
+      for (int i = 0; i < 16; ++i) e[i] = 0.f;
+      for (int j = 0; j < H; ++j) { hs[q][j] = 0.f; dhs[q][j] = 0.f; }
     }
-    const float* W2 = sw + 17 * H;
-    for (int j = 0; j < H; ++j) {
-      const float g = W2[j] * dz[0] + W2[H + j] * dz[1] + W2[2 * H + j] * dz[2];
-      dh[j] = h[j] > 0.f ? g : 0.f;
-    }
-  }
-  // contributions, reduced over the wave then over the 4 waves
-  for (int p = 0; p < P; ++p) {
-    float v;
-    if (p < 16 * H) v = dh[p >> 4] * e[p & 15];
-    else if (p < 17 * H) v = dh[p - 16 * H];
-    else if (p < 20 * H) { const int q = p - 17 * H; v = dz[q / H] * h[q % H]; }
-    else v = dz[p - 20 * H];
-    v = wave_sum(v);
-    if (lane == 0) red[wave][p] = v;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) es[q][i] = e[i];
+    for (int c = 0; c < 3; ++c) dzs[q][c] = dz[c];
   }
   __syncthreads();
-  for (int p = threadIdx.x; p < P; p += blockDim.x)
-    slab[(int64_t)blockIdx.x * P + p] = (red[0][p] + red[1][p]) + (red[2][p] + red[3][p]);
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    float v = 0.f;
+    if (p < 16 * H) {
+      const int j = p >> 4, i = p & 15;
+      for (int q = 0; q < BG_RAYS; ++q) v += dhs[q][j] * es[q][i];
+    } else if (p < 17 * H) {
+      const int j = p - 16 * H;
+      for (int q = 0; q < BG_RAYS; ++q) v += dhs[q][j];
+    } else if (p < 20 * H) {
+      const int c = (p - 17 * H) / H, j = (p - 17 * H) - c * H;
+      for (int q = 0; q < BG_RAYS; ++q) v += dzs[q][c] * hs[q][j];
+    } else {
+      const int c = p - 20 * H;
+      for (int q = 0; q < BG_RAYS; ++q) v += dzs[q][c];
+    }
+    slab[(int64_t)blockIdx.x * P + p] = v;
+  }
 }
 
 __global__ void bg_reduce_kernel(const float* __restrict__ slab, int nblk, int P, float* __restrict__ dw) {
@@ -371,7 +395,7 @@ extern "C" int nerf_bg_mlp_fwd(const float* d, int64_t d_stride, int64_t N, cons
 
 extern "C" int64_t nerf_bg_mlp_workspace_bytes(int64_t N, int H) {
   if (N < 0 || H < 1 || H > BG_MAXH) return NERF_E_ARG;
-  return nerf_cdiv(N < 1 ? 1 : N, 256) * (20 * H + 3) * 4 + 256;
+  return nerf_cdiv(N < 1 ? 1 : N, BG_RAYS) * (20 * H + 3) * 4 + 256;
 }
 
 extern "C" int nerf_bg_mlp_bwd(const float* d, int64_t d_stride, int64_t N, const float* w, int H,
@@ -383,7 +407,7 @@ extern "C" int nerf_bg_mlp_bwd(const float* d, int64_t d_stride, int64_t N, cons
     return nerf_launch_status();
   }
   if (!d || !w || !d_out || !ws) return NERF_E_ARG;
-  const int64_t nblk = nerf_cdiv(N, 256);
+  const int64_t nblk = nerf_cdiv(N, BG_RAYS);
   if (ws_bytes < nblk * P * 4) return NERF_E_WORKSPACE;
   float* slab = reinterpret_cast<float*>(ws);
   bg_bwd_kernel<<<(unsigned)nblk, 256, 0, st>>>(d, d_stride, N, w, H, d_out, slab);

@@ -57,6 +57,7 @@ struct NgpPlan {
   int g0, g1;            // gradient tiles (ld 68)
   int dsig;              // d sigma_raw per tile row (64 floats; backward plan)
   int sraw;              // sigma_raw per tile row (64 floats; forward plan, -1 in the backward plan)
+  int bsum;              // bias-gradient partials [4 waves][nl][64] (backward plan)
   int smem_floats;
   int nsb;               // weight-gradient 32x32 blocks: layer, n-block, k-block
   int sb_layer[NGP_MAX_SB], sb_nb[NGP_MAX_SB], sb_kb[NGP_MAX_SB];
@@ -123,10 +124,11 @@ bool make_plan(const NerfNgpNet& n, bool save, NgpPlan& P) {
     P.g1 = take(68);
     P.dsig = s; s += NGP_ROWS;
     P.sraw = -1;
+    P.bsum = -1;
   } else {
     pp[0] = take(68);
     pp[1] = take(68);
-    P.g0 = P.g1 = P.dsig = -1;
+    P.g0 = P.g1 = P.dsig = P.bsum = -1;
     P.sraw = s; s += NGP_ROWS;
   }
   int prev_out = P.enc_buf, prev_ld = P.enc_ld;
@@ -142,17 +144,38 @@ bool make_plan(const NerfNgpNet& n, bool save, NgpPlan& P) {
     prev_out = L.out_buf;
     prev_ld = L.out_ld;
   }
+  // bias-gradient partials last, only when they fit (deep nets: one wave per layer sums all rows in registers)
+  if (save && (int64_t)(s + 4 * P.nl * 64) * 4 <= 160 * 1024) { P.bsum = s; s += 4 * P.nl * 64; }
   P.smem_floats = s;
   if ((int64_t)s * 4 > 160 * 1024) return false;
-  // weight-gradient blocks
-  int nsb = 0;
-  for (int l = 0; l < P.nl; ++l)
-    for (int nb = 0; nb < P.ly[l].Npad / 32; ++nb)
-      for (int kb = 0; kb < P.ly[l].Kpad / 32; ++kb) {
-        if (nsb >= NGP_MAX_SB) return false;
-        P.sb_layer[nsb] = l; P.sb_nb[nsb] = nb; P.sb_kb[nsb] = kb; ++nsb;
+  // weight-gradient blocks, dealt to the 4 waves: slot sb = wave + 4 j.  In the backward a layer's wgrad blocks run
+  // in the same barrier interval as its input-gradient MFMAs (wave (rb, kb) busy iff kb*32 < Kpad, Npad/2 MFMAs), so
+  // each block goes to the wave with the least work in that interval (then the fewest slots used): the critical
+  // MFMA chain of the production net drops from 352 to 288 per tile versus a layer-major deal.
+  int nblk = 0;
+  for (int l = 0; l < P.nl; ++l) nblk += (P.ly[l].Npad / 32) * (P.ly[l].Kpad / 32);
+  const int per_wave = (nblk + 3) / 4;
+  if (4 * per_wave > NGP_MAX_SB) return false;
+  int used[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 4 * per_wave; ++i) P.sb_layer[i] = -1;
+  for (int l = 0; l < P.nl; ++l) {
+    const NgpLayer& L = P.ly[l];
+    int cost[4];
+    for (int w = 0; w < 4; ++w) cost[w] = ((w >> 1) * 32 < L.Kpad) ? L.Npad / 2 : 0;
+    for (int nb = 0; nb < L.Npad / 32; ++nb)
+      for (int kb = 0; kb < L.Kpad / 32; ++kb) {
+        int best = -1;
+        for (int w = 0; w < 4; ++w) {
+          if (used[w] >= per_wave) continue;
+          if (best < 0 || cost[w] < cost[best] || (cost[w] == cost[best] && used[w] < used[best])) best = w;
+        }
+        const int sb = best + 4 * used[best];
+        P.sb_layer[sb] = l; P.sb_nb[sb] = nb; P.sb_kb[sb] = kb;
+        ++used[best];
+        cost[best] += 32;  // 64 rows / 2 per MFMA
       }
-  P.nsb = nsb;
+  }
+  P.nsb = 4 * per_wave;
   return true;
 }
 
@@ -710,7 +733,12 @@ __global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpPlan P, const float* __
   ngp_f32x16 accw[NSB];
 #pragma unroll
   for (int j = 0; j < NSB; ++j) accw[j] = zero16();
-  float bacc[3] = {0.f, 0.f, 0.f};  // bias grads of layers l = wave + 4j, column = lane
+  // bias gradients: wave w sums rows 16w..16w+15 of every tile into its own LDS partial (column = lane); without
+  // room for the partials (P.bsum < 0) wave l&3 sums all rows of layer l into bacc[l>>2]
+  float* bsum = smem + (P.bsum >= 0 ? P.bsum : 0) + wave * P.nl * 64;
+  if (P.bsum >= 0)
+    for (int l = 0; l < P.nl; ++l) bsum[l * 64 + lane] = 0.f;
+  float bacc[3] = {0.f, 0.f, 0.f};
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t m0 = tile * NGP_ROWS;
@@ -754,7 +782,13 @@ __global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpPlan P, const float* __
         const int sb = wave + 4 * j;
         if (sb < P.nsb && P.sb_layer[sb] == l) wgrad_block(accw[j], L, smem, G, P.sb_nb[sb], P.sb_kb[sb], li, lh);
       }
-      if ((l & 3) == wave && lane < L.Npad) {
+      if (P.bsum >= 0 && lane < L.Npad) {
+        const float* gc = smem + G + (16 * wave) * 68 + lane;
+        float s = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s += gc[r * 68];
+        bsum[l * 64 + lane] += s;
+      } else if (P.bsum < 0 && (l & 3) == wave && lane < L.Npad) {
         float s = 0.f;
         for (int r = 0; r < NGP_ROWS; ++r) s += smem[G + r * 68 + lane];
         bacc[l >> 2] += s;
@@ -784,7 +818,7 @@ __global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpPlan P, const float* __
 #pragma unroll
   for (int j = 0; j < NSB; ++j) {
     const int sb = wave + 4 * j;
-    if (sb < P.nsb) {
+    if (sb < P.nsb && P.sb_layer[sb] >= 0) {
       const NgpLayer& L = P.ly[P.sb_layer[sb]];
       const int k = P.sb_kb[sb] * 32 + li;
 #pragma unroll
@@ -796,20 +830,64 @@ __global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpPlan P, const float* __
         }
     }
   }
+  if (P.bsum >= 0) {
+    __syncthreads();
+    for (int l = wave; l < P.nl; l += 4) {
+      if (lane < P.ly[l].Npad) {
+        const float* b = smem + P.bsum + l * 64 + lane;
+        const int ws = P.nl * 64;
+        slab[P.ly[l].b_off + lane] = (b[0] + b[ws]) + (b[2 * ws] + b[3 * ws]);
+      }
+    }
+  } else {
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int l = wave + 4 * j;
-    if (l < P.nl && lane < P.ly[l].Npad) slab[P.ly[l].b_off + lane] = bacc[j];
+    for (int j = 0; j < 3; ++j) {
+      const int l = wave + 4 * j;
+      if (l < P.nl && lane < P.ly[l].Npad) slab[P.ly[l].b_off + lane] = bacc[j];
+    }
   }
 }
 
-__global__ void ngp_reduce_kernel(const float* __restrict__ partial, int64_t total, int nslab, float* __restrict__ dw,
-                                  int accumulate) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  float s = accumulate ? dw[i] : 0.f;
-  for (int b = 0; b < nslab; ++b) s += partial[(int64_t)b * total + i];
-  dw[i] = s;
+// dw = sum over the workgroup slabs.  A block owns 64 consecutive columns (16 float4) and 16 slab groups: thread
+// (g, c) sums slabs g, g+16, ... of its column in order, then column c's 16 group sums are added in order g = 0..15
+// (deterministic).  One thread per column over all slabs ran at 0.3 TB/s (256 dependent adds per thread).
+constexpr int RED_COLS4 = 16, RED_GROUPS = 16;
+template <bool VEC_OUT>
+__global__ __launch_bounds__(256) void ngp_reduce_kernel(const float* __restrict__ partial, int64_t total, int nslab,
+                                                         float* __restrict__ dw, int accumulate) {
+  __shared__ float4 red[RED_GROUPS][RED_COLS4];
+  const int c = threadIdx.x % RED_COLS4, g = threadIdx.x / RED_COLS4;
+  const int64_t i4 = (int64_t)blockIdx.x * RED_COLS4 + c;  // float4 column (total % 32 == 0)
+  const int64_t n4 = total / 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i4 < n4) {
+    const float4* p = reinterpret_cast<const float4*>(partial) + i4;
+#pragma unroll 4
+    for (int b = g; b < nslab; b += RED_GROUPS) {
+      const float4 v = p[(int64_t)b * n4];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  red[g][c] = s;
+  __syncthreads();
+  if (g == 0 && i4 < n4) {
+    float4 a = red[0][c];
+#pragma unroll
+    for (int k = 1; k < RED_GROUPS; ++k) {
+      const float4 v = red[k][c];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    if (VEC_OUT) {
+      float4* o = reinterpret_cast<float4*>(dw) + i4;
+      if (accumulate) { const float4 d = *o; a.x = d.x + a.x; a.y = d.y + a.y; a.z = d.z + a.z; a.w = d.w + a.w; }
+      *o = a;
+    } else {
+      float* o = dw + 4 * i4;
+      const float v[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = accumulate ? o[e] + v[e] : v[e];
+    }
+  }
 }
 
 // dynamic LDS above 64 KB must be allowed per kernel, once per process.  Keyed by the kernel's address: the
@@ -1007,6 +1085,10 @@ extern "C" int nerf_ngp_bwd(const NerfNgpNet* net, const float* w, const float* 
     ngp_bwd_kernel<6><<<grid, 256, sm, st>>>(P, w, enc, enc_stride, x_d, M, d_rgb_sigma, d_enc, partial, ntiles);
   else
     ngp_bwd_kernel<8><<<grid, 256, sm, st>>>(P, w, enc, enc_stride, x_d, M, d_rgb_sigma, d_enc, partial, ntiles);
-  ngp_reduce_kernel<<<(unsigned)nerf_cdiv(P.total, 256), 256, 0, st>>>(partial, P.total, grid, d_w, accumulate);
+  const unsigned rblocks = (unsigned)nerf_cdiv(P.total / 4, RED_COLS4);
+  if (nerf_aligned16(d_w))
+    ngp_reduce_kernel<true><<<rblocks, 256, 0, st>>>(partial, P.total, grid, d_w, accumulate);
+  else
+    ngp_reduce_kernel<false><<<rblocks, 256, 0, st>>>(partial, P.total, grid, d_w, accumulate);
   return nerf_launch_status();
 }

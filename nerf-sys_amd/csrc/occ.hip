@@ -66,7 +66,8 @@ __device__ __forceinline__ int64_t cell_of(const Grid& G, float px, float py, fl
 __device__ __forceinline__ int march_ray(const Grid& G, const uint8_t* __restrict__ bin, const float o[3],
                                          const float d[3], float t, float tf, float step, float cone, int max_steps,
                                          int64_t w, int32_t rid, int32_t* __restrict__ ray_idx,
-                                         float* __restrict__ t0, float* __restrict__ t1) {
+                                         float* __restrict__ t0, float* __restrict__ t1,
+                                         float2* __restrict__ stage = nullptr, int cap = 0) {
   // clip to the outermost level box
   const float big = (float)(1 << (G.L - 1));
   for (int a = 0; a < 3; ++a) {
@@ -95,6 +96,8 @@ __device__ __forceinline__ int march_ray(const Grid& G, const uint8_t* __restric
         t0[w] = t;
         t1[w] = t + dt;
         ++w;
+      } else if (stage && n < cap) {
+        stage[n] = make_float2(t, t + dt);
       }
       ++n;
       t = t + dt;
@@ -139,13 +142,18 @@ struct MarchExperts {
   float step[MARCH_MAX_EXPERTS];
 };
 
+// stage (count pass, may be null): the first cap segments of pair j = k*N + r go to stage[j*cap ...] so that the
+// emit pass copies them instead of marching again; overflow_only (write pass): only pairs with counts > cap march.
 __global__ void march_multi_kernel(MarchExperts E, const float* __restrict__ rays, int64_t N, float near_plane,
                                    float far_plane, float cone, int stratified, uint64_t seed, int max_steps,
                                    int32_t* __restrict__ counts, const int32_t* __restrict__ offsets,
-                                   int32_t* __restrict__ ray_idx, float* __restrict__ t0, float* __restrict__ t1) {
+                                   int32_t* __restrict__ ray_idx, float* __restrict__ t0, float* __restrict__ t1,
+                                   float2* __restrict__ stage, int cap, int overflow_only) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
   if (r >= N) return;
+  const int64_t j = (int64_t)k * N + r;
+  if (overflow_only && counts[j] <= cap) return;
   const float* ry = rays + r * 8;
   float tmin = -INFINITY, tmax = INFINITY;
   for (int a = 0; a < 3; ++a) {
@@ -161,11 +169,33 @@ __global__ void march_multi_kernel(MarchExperts E, const float* __restrict__ ray
     float t = fmaxf(near_plane, ry[6]);
     const float tf = fminf(far_plane, ry[7]);
     if (stratified) t += nerf_uniform(seed, 0x0CC00 + (uint64_t)k, (uint64_t)r) * E.step[k];
-    const int64_t j = (int64_t)k * N + r;
     n = march_ray(E.G[k], E.bin[k], o, d, t, tf, E.step[k], cone, max_steps, offsets ? offsets[j] : 0, (int32_t)r,
-                  ray_idx, offsets ? t0 : nullptr, t1);
+                  ray_idx, offsets ? t0 : nullptr, t1, offsets ? nullptr : (stage ? stage + j * cap : nullptr), cap);
   }
-  if (!offsets) counts[(int64_t)k * N + r] = n;
+  if (!offsets) counts[j] = n;
+}
+
+// emit pass of the staged march: one wave per pair copies its staged segments (coalesced) into the packed arrays;
+// pairs longer than cap are left to the overflow march.
+__global__ __launch_bounds__(256) void march_emit_kernel(const float2* __restrict__ stage, int cap,
+                                                         const int32_t* __restrict__ counts,
+                                                         const int32_t* __restrict__ offsets, int64_t N, int64_t KN,
+                                                         int32_t* __restrict__ ray_idx, float* __restrict__ t0,
+                                                         float* __restrict__ t1) {
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (j >= KN) return;
+  const int c = counts[j];
+  if (c > cap) return;
+  const int64_t o = offsets[j];
+  const int32_t r = (int32_t)(j % N);
+  const float2* sg = stage + j * cap;
+  for (int s = lane; s < c; s += 64) {
+    const float2 v = sg[s];
+    ray_idx[o + s] = r;
+    t0[o + s] = v.x;
+    t1[o + s] = v.y;
+  }
 }
 
 // ---- exclusive scan of int32 (n+1 outputs): reduce-then-scan over 2048-element tiles (256 threads x 8
@@ -605,7 +635,41 @@ extern "C" int nerf_occ_march_multi(const NerfOccGrid* grids, const uint8_t* con
   }
   march_multi_kernel<<<dim3((unsigned)nerf_cdiv(N, 64), K), 64, 0, st>>>(E, rays, N, near_plane, far_plane, cone_angle,
                                                                          stratified, seed, max_steps, counts, offsets,
-                                                                         ray_idx, t0, t1);
+                                                                         ray_idx, t0, t1, nullptr, 0, 0);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_occ_march_multi_staged(const NerfOccGrid* grids, const uint8_t* const* binaries,
+                                           const float* boxes, const float* steps, int K, const float* rays, int64_t N,
+                                           float near_plane, float far_plane, float cone_angle, int stratified,
+                                           uint64_t seed, int max_steps, int32_t* counts, float* stage, int cap,
+                                           const int32_t* offsets, int32_t* ray_idx, float* t0, float* t1,
+                                           hipStream_t st) {
+  if (K < 1 || K > MARCH_MAX_EXPERTS || N < 0 || max_steps < 1 || cap < 1 || !grids || !binaries || !boxes || !steps)
+    return NERF_E_ARG;
+  if (N == 0) return NERF_OK;
+  if (!rays || !counts || !stage || (offsets && (!ray_idx || !t0 || !t1))) return NERF_E_ARG;
+  if ((int64_t)K * N > INT32_MAX) return NERF_E_ARG;
+  if ((uintptr_t)stage & 7) return NERF_E_ALIGN;  // float2 stores
+  MarchExperts E{};
+  for (int k = 0; k < K; ++k) {
+    if (!grid_ok(&grids[k]) || !binaries[k] || !(steps[k] > 0.f)) return NERF_E_ARG;
+    E.G[k] = make_grid(&grids[k]);
+    E.bin[k] = binaries[k];
+    for (int a = 0; a < 6; ++a) E.box[k][a] = boxes[6 * k + a];
+    E.step[k] = steps[k];
+  }
+  float2* sg = reinterpret_cast<float2*>(stage);
+  const dim3 grid((unsigned)nerf_cdiv(N, 64), K);
+  if (!offsets) {
+    march_multi_kernel<<<grid, 64, 0, st>>>(E, rays, N, near_plane, far_plane, cone_angle, stratified, seed, max_steps,
+                                            counts, nullptr, nullptr, nullptr, nullptr, sg, cap, 0);
+  } else {
+    const int64_t KN = (int64_t)K * N;
+    march_emit_kernel<<<(unsigned)nerf_cdiv(KN, 4), 256, 0, st>>>(sg, cap, counts, offsets, N, KN, ray_idx, t0, t1);
+    march_multi_kernel<<<grid, 64, 0, st>>>(E, rays, N, near_plane, far_plane, cone_angle, stratified, seed, max_steps,
+                                            counts, offsets, ray_idx, t0, t1, nullptr, cap, 1);
+  }
   return nerf_launch_status();
 }
 

@@ -75,6 +75,7 @@ def lib():
             "nerf_packed_visibility": [P, P, P, P, I64, F, F, P, P],
             "nerf_packed_visibility_groups": [P, P, P, P, I64, I64, F, F, P, P, P],
             "nerf_occ_march_multi": [P, P, P, P, I, P, I64, F, F, F, I, U64, I, P, P, P, P, P, P],
+            "nerf_occ_march_multi_staged": [P, P, P, P, I, P, I64, F, F, F, I, U64, I, P, P, I, P, P, P, P, P],
             "nerf_packed_compact": [P, P, I64, P, P, P, P, P, P, P, P],
             "nerf_occ_cell_points": [P, P, I64, U64, P, P],
             "nerf_occ_update": [P, P, P, I64, F, P],
@@ -132,7 +133,7 @@ EXPORTS = ("nerf_rays_gen", "nerf_pick_pixels", "nerf_clamp_near_far", "nerf_ray
            "nerf_packed_points", "nerf_rays_aabb_hit", "nerf_flag_compact", "nerf_scatter_counts", "nerf_segments_union",
            "nerf_moe_blend", "nerf_moe_blend_finish", "nerf_moe_blend_bwd", "nerf_occ_threshold_floats",
            "nerf_sgd_multi", "nerf_reptile_workspace_bytes", "nerf_reptile_update", "nerf_dataset_rays",
-           "nerf_occ_march_multi", "nerf_packed_visibility_groups", "nerf_ngp_density",
+           "nerf_occ_march_multi", "nerf_occ_march_multi_staged", "nerf_packed_visibility_groups", "nerf_ngp_density",
            "nerf_occ_sample_cells", "nerf_moe_route_n",
            "nerf_packed_points_n")
 

@@ -161,6 +161,9 @@ class _BlendFn(torch.autograd.Function):
         return (None, None, None, None, *grads)
 
 
+MARCH_STAGE_CAP = 512  # staged segments per (expert, ray) pair: K*N*512*8 B (67 MB at 4 x 4096 pairs)
+
+
 def _march_experts(model, rays, sub_params, render_step_size, alpha_thre, cone_angle):
     """Every expert's occupancy marching (MetaNGP.occupancy_marching, meta_ngp.py:384-443, on the rays that hit its
     box, ray_rendering.py:397-422) in ONE launch pair: count -> scan -> ONE host read of the K+1 expert boundaries
@@ -190,7 +193,11 @@ def _march_experts(model, rays, sub_params, render_step_size, alpha_thre, cone_a
     counts = torch.empty(K * N, dtype=torch.int32, device=dev)
     args = (grids, bins, boxes, steps, K, ptr(rays), N, float(ex0.near_plane), float(ex0.far_plane), float(cone[0]),
             int(training), ctypes.c_uint64(seed), 8192)
-    check(L.nerf_occ_march_multi(*args, ptr(counts), None, None, None, None, stream()), "nerf_occ_march_multi(count)")
+    # staged march: the count pass keeps each (expert, ray) pair's first MARCH_STAGE_CAP segments, so the write pass
+    # is a copy (pairs with more segments are marched again)
+    stage = torch.empty(K * N * MARCH_STAGE_CAP * 2, dtype=torch.float32, device=dev)
+    check(L.nerf_occ_march_multi_staged(*args, ptr(counts), ptr(stage), MARCH_STAGE_CAP, None, None, None, None,
+                                        stream()), "nerf_occ_march_multi_staged(count)")
     offs = exclusive_scan(counts)
     bounds = offs[::N].cpu().tolist()                  # the one host read: K+1 expert boundaries
     M = bounds[-1]
@@ -199,8 +206,9 @@ def _march_experts(model, rays, sub_params, render_step_size, alpha_thre, cone_a
     ri = torch.empty(M, dtype=torch.int32, device=dev)
     t0 = torch.empty(M, dtype=torch.float32, device=dev)
     t1 = torch.empty(M, dtype=torch.float32, device=dev)
-    check(L.nerf_occ_march_multi(*args, None, ptr(offs), ptr(ri), ptr(t0), ptr(t1), stream()),
-          "nerf_occ_march_multi(write)")
+    check(L.nerf_occ_march_multi_staged(*args, ptr(counts), ptr(stage), MARCH_STAGE_CAP, ptr(offs), ptr(ri), ptr(t0),
+                                        ptr(t1), stream()), "nerf_occ_march_multi_staged(emit)")
+    del stage
     athr = [ex.alpha_thre if alpha_thre is None else alpha_thre for ex in subs]
     if training:
         # visibility (nerfacc sampling with sigma_fn, early_stop_eps 1e-4): sigma of every sample from its expert

@@ -311,12 +311,66 @@ class NgpLayout:
         # Adam groups inside the packed MLP: 'sigma' = trunk + heads, 'color' = colour MLP (meta_ngp.py:446-469)
         self.color_start = t[2 * (sigma_depth + 1)][0]
 
-    def pack(self, tensors):
-        flat = torch.cat([x.reshape(-1).to(torch.float32) for x in tensors])
-        key = str(flat.device)
+    def device_index(self, device):
+        key = str(device)
         if key not in self._dev:
-            self._dev[key] = self.index.to(flat.device)
-        return torch.zeros(self.total, dtype=torch.float32, device=flat.device).index_copy(0, self._dev[key], flat)
+            self._dev[key] = self.index.to(device)
+        return self._dev[key]
+
+    def pack(self, tensors):
+        return _PackFn.apply(self, *tensors)
+
+    def pack_raw(self, tensors):
+        flat = torch.cat([x.detach().reshape(-1).to(torch.float32) for x in tensors])
+        return torch.zeros(self.total, dtype=torch.float32, device=flat.device).index_copy(
+            0, self.device_index(flat.device), flat)
+
+    def flat_grad_target(self, tensors):
+        """(flat gradient buffer, element positions) when every tensor's .grad is a contiguous view of ONE
+        FlatAdam gradient buffer (tag ``_nerf_flat_grad``), else None."""
+        gs = [t.grad for t in tensors]
+        if not all(getattr(t, "_nerf_flat_grad", False) and g is not None and g.is_contiguous() for t, g in
+                   zip(tensors, gs)):
+            return None
+        base = gs[0]._base
+        if base is None or any(g._base is not base for g in gs):
+            return None
+        key = ("flat", base.data_ptr(), tuple(g.data_ptr() for g in gs))
+        if key not in self._dev:
+            b0 = base.data_ptr()
+            self._dev[key] = torch.cat([torch.arange((g.data_ptr() - b0) // 4, (g.data_ptr() - b0) // 4 + g.numel())
+                                        for g in gs]).to(base.device)
+        return base, self._dev[key]
+
+
+class _PackFn(torch.autograd.Function):
+    """Packs a MetaNGP's named tensors into the fused kernel's layout.  Backward: the packed gradient goes back to
+    the tensors' layout with ONE gather; for FlatAdam-owned parameters it is added straight into the flat gradient
+    buffer (one index_add instead of one autograd accumulation launch per tensor), returning no per-tensor grads."""
+
+    @staticmethod
+    def forward(ctx, layout, *tensors):
+        ctx.layout = layout
+        ctx.tensors = tensors
+        return layout.pack_raw(tensors)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, d_w):
+        layout, tensors = ctx.layout, ctx.tensors
+        need_all = all(ctx.needs_input_grad[1:])
+        g = d_w.index_select(0, layout.device_index(d_w.device))
+        tgt = layout.flat_grad_target(tensors) if need_all else None
+        if tgt is not None:
+            base, pos = tgt
+            base.index_add_(0, pos, g)
+            return (None,) * (1 + len(tensors))
+        out, o = [], 0
+        for t, need_i in zip(tensors, ctx.needs_input_grad[1:]):
+            k = t.numel()
+            out.append(g[o:o + k].view_as(t) if need_i else None)
+            o += k
+        return (None, *out)
 
 
 class _NgpFn(torch.autograd.Function):

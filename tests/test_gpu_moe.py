@@ -260,3 +260,44 @@ def test_container_occ_training_gradients(z):
     assert float(mc.bg_mlp[0].weight.grad.abs().sum()) > 0
     assert sum(float(s.xyz_encoder.hash_table.grad.abs().sum()) > 0 for s in mc.submodules
                if s.xyz_encoder.hash_table.grad is not None) >= 1
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_staged_march_equals_two_pass_march(z, train):
+    """nerf_occ_march_multi_staged (count pass keeps the first cap segments, emit pass copies them, longer pairs are
+    marched again) produces exactly the two-pass march's packed segments — with no overflow (cap 512) and with
+    nearly every pair overflowing (cap 1, 3)."""
+    import ctypes
+    from nerf_amd import container as C
+    from nerf_amd._lib import lib, ptr, stream
+    from nerf_amd.occupancy import exclusive_scan
+    mc = _occ_container(z, 2)
+    subs = list(mc.submodules)
+    n = 80
+    rays = _occ_rays(n, 9)
+    Kx = len(subs)
+    grids = (type(subs[0].occ_grid.grid) * Kx)(*[ex.occ_grid.grid for ex in subs])
+    bins = (ctypes.c_void_p * Kx)(*[ex.occ_grid.binaries.data_ptr() for ex in subs])
+    boxes = (ctypes.c_float * (6 * Kx))(*[float(v) for ex in subs for v in ex._aabb_host])
+    steps = (ctypes.c_float * Kx)(*[float(ex.render_step_size) for ex in subs])
+    args = (grids, bins, boxes, steps, Kx, ptr(rays), n, float(subs[0].near_plane), float(subs[0].far_plane), 0.004,
+            int(train), ctypes.c_uint64(1234), 8192)
+    L = lib()
+    counts = torch.empty(Kx * n, dtype=torch.int32, device=DEV)
+    assert L.nerf_occ_march_multi(*args, ptr(counts), None, None, None, None, stream()) == 0
+    offs = exclusive_scan(counts)
+    M = int(offs[-1])
+    assert M > 0 and int(counts.max()) > 3
+    ref = [torch.empty(M, dtype=dt, device=DEV) for dt in (torch.int32, torch.float32, torch.float32)]
+    assert L.nerf_occ_march_multi(*args, None, ptr(offs), *[ptr(t) for t in ref], stream()) == 0
+    for cap in (512, 3, 1):
+        c2 = torch.full_like(counts, -7)
+        stage = torch.empty(Kx * n * cap * 2, dtype=torch.float32, device=DEV)
+        assert L.nerf_occ_march_multi_staged(*args, ptr(c2), ptr(stage), cap, None, None, None, None, stream()) == 0
+        assert torch.equal(c2, counts), cap
+        out = [torch.full((M,), -5, dtype=dt, device=DEV) for dt in (torch.int32, torch.float32, torch.float32)]
+        assert L.nerf_occ_march_multi_staged(*args, ptr(c2), ptr(stage), cap, ptr(offs), *[ptr(t) for t in out],
+                                             stream()) == 0
+        for a, b in zip(out, ref):
+            assert torch.equal(a, b), cap
+    assert L.nerf_occ_march_multi_staged(*args, ptr(counts), ptr(stage), 0, None, None, None, None, stream()) < 0
