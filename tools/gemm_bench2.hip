@@ -54,6 +54,9 @@ int main(int argc, char** argv) {
       {"dgrd BN=256", 1, {}},
       {"wgrd lib lds", 2, {}},
       {"wgrd barrier-free R=8", 2, {}},
+      {"wgrd 256x256 tile", 2, {}},
+      {"wgrd 256x128 tile", 2, {}},
+      {"wgrd 128x256 tile", 2, {}},
   };
   const unsigned nb256 = (unsigned)(M / 128);
   auto run = [&](int v) {
@@ -68,6 +71,9 @@ int main(int argc, char** argv) {
       case 7: gemm_nt_kernel<128, 256, 2, EPI_MASK, 2><<<nb256, 256>>>(A, K, B, K, bias, C, N, mb, 8, nullptr, K, 1); break;
       case 8: gemm_wgrad_kernel<128, 128, 2><<<4 * 256, 256>>>(A, K, C, N, P, 256, P + 65536, slab, M / 256, M, 2, 4); break;
       case 9: gemm_wgrad_os_kernel<4, 2, 8, 8><<<256, 512>>>(A, K, C, N, P, 256, P + 65536, slab, M / 256, M, 4); break;
+      case 10: gemm_wgrad_kernel<256, 256, 2><<<256, 256>>>(A, K, C, N, P, 256, P + 65536, slab, M / 256, M, 1, 1); break;
+      case 11: gemm_wgrad_kernel<256, 128, 2><<<2 * 256, 256>>>(A, K, C, N, P, 256, P + 65536, slab, M / 256, M, 2, 2); break;
+      case 12: gemm_wgrad_kernel<128, 256, 2><<<2 * 256, 256>>>(A, K, C, N, P, 256, P + 65536, slab, M / 256, M, 1, 2); break;
     }
   };
   // correctness: each variant vs the library variant of its class, bitwise (same k order, same fmaf chain)
