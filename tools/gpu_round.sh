@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 STEP=${1:-all}
 BENCH_ARGS=${BENCH_ARGS:-"--steps 20 --warmup 5"}
 if [[ $STEP == all || $STEP == test ]]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
   tail -30 gpurun_out/pytest_gpu.log; [[ $rc -ne 0 ]] && exit $rc
   timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
   cat gpurun_out/smoke.log
