@@ -203,7 +203,11 @@ __device__ __forceinline__ void nt_epilogue(const nerf_f32x16 (&acc)[TM][TN], in
 // block 0 also writes Pb[s][n] = sum_m G[m][n] (bias gradient).  MFMA A = G^T (i = n, k-slot = m),
 // B = X (k-slot = m, j = k).  LDS tiles [16 rows][cols] read with ds_read_b32 (32 consecutive floats per
 // half-wave: conflict-free).
-template <int BN, int BK, int WAVES_N>
+// MR = rows per LDS slab (16, 32 or 64; rows_per_split % MR == 0).  The narrow tiles (one or two tiles
+// per split: 256 or 512 workgroups) are latency-bound at MR = 16 (too few bytes in flight per CU), so they
+// stage 32 / 64 rows; each slab is consumed as MR/16 sub-slabs of 16 rows in the MR = 16 row order, so the
+// per-element accumulation order, and hence every bit of P, does not depend on MR.
+template <int BN, int BK, int WAVES_N, int MR = 16>
 __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const float* __restrict__ G, int ldg,
                                                          const float* __restrict__ X, int ldx,
                                                          float* __restrict__ P, int ldp, float* __restrict__ Pb,
@@ -213,7 +217,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const float* __restrict
   constexpr int WTN = BN / WAVES_N, WTK = BK / WAVES_K;
   constexpr int TM = WTN / 32, TN = WTK / 32;
   static_assert(TM >= 1 && TN >= 1, "wave tile");
-  constexpr int MR = 16;
+  static_assert(MR == 16 || MR == 32 || MR == 64, "rows per slab");
   constexpr int G_F4 = MR * BN / 4, X_F4 = MR * BK / 4;
   constexpr int G_PER = (G_F4 + 255) / 256, X_PER = (X_F4 + 255) / 256;
   __shared__ __attribute__((aligned(16))) float smem[2 * MR * (BN + BK)];
@@ -282,8 +286,8 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const float* __restrict
     const float* Gs = smem + cur * MR * (BN + BK);
     const float* Xs = Gs + MR * BN;
 #pragma unroll
-    for (int ss = 0; ss < 8; ++ss) {
-      const int row = 8 * lh + ss;
+    for (int ss = 0; ss < MR / 2; ++ss) {
+      const int row = 16 * (ss >> 3) + 8 * lh + (ss & 7);
       float af[TM], bf[TN];
 #pragma unroll
       for (int a = 0; a < TM; ++a) af[a] = Gs[row * BN + wn * WTN + a * 32 + li];

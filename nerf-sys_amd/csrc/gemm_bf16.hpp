@@ -545,8 +545,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_bf16_wsr_kernel(const nerf_bf1
 // ------------------------------------------------------------------------------------------ gemm_wgrad_bf16
 // P[s][n][k] (row pitch ldp, fp32) = sum over rows m of split s of G[m][n] * X[m][k]; the tiles of column
 // block 0 also write Pb[s][n] = sum_m G[m][n].  MFMA A = G^T (i = n, k-slot = m), B = X (k-slot = m, j = k).
-// Requirements: rows_per_split % 32 == 0, M % 32 == 0, ldg/ldx % 8 == 0.
-template <int BN, int BK, int WAVES_N>
+// Requirements: rows_per_split % MR == 0, M % 32 == 0, ldg/ldx % 8 == 0.  MR = rows per LDS slab: the
+// narrow launches (one or two tiles per split) stage 64 rows to keep enough bytes in flight per CU; the
+// 16-row MFMA k-steps run in the same row order for every MR, so P does not depend on it.
+template <int BN, int BK, int WAVES_N, int MR = 32>
 __global__ __launch_bounds__(256, 2) void gemm_wgrad_bf16_kernel(const nerf_bf16* __restrict__ G, int ldg,
                                                                 const nerf_bf16* __restrict__ X, int ldx,
                                                                 float* __restrict__ P, int ldp, float* __restrict__ Pb,
@@ -556,7 +558,7 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_bf16_kernel(const nerf_bf16
   constexpr int WTN = BN / WAVES_N, WTK = BK / WAVES_K;
   constexpr int TM = WTN / 32, TN = WTK / 32;
   static_assert(TM >= 1 && TN >= 1, "wave tile");
-  constexpr int MR = 32;                         // rows (contraction) per LDS slab: two 16-row MFMA k-steps
+  static_assert(MR == 32 || MR == 64, "rows per slab");
   constexpr int PG = ((BN + 127) / 128) * 128 + 32, PX = ((BK + 127) / 128) * 128 + 32;  // pitch = 64 B mod 256 B
   constexpr int G_CH = MR * BN / 8, X_CH = MR * BK / 8;
   constexpr int G_PER = (G_CH + 255) / 256, X_PER = (X_CH + 255) / 256;

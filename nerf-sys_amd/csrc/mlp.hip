@@ -62,7 +62,7 @@ WS carve(void* base, int64_t M, int training) {
     w.dO16 = take(Mp * 32);
     w.WT = take(WT_FLOATS);
     w.S = n_splits(Mp);
-    w.rps = round_up(nerf_cdiv(Mp, w.S), 16);
+    w.rps = round_up(nerf_cdiv(Mp, w.S), 64);  // whole slabs for every wgrad MR
     w.partial = take((int64_t)w.S * layout().total);
   }
   w.bytes = (int64_t)((char*)p - (char*)base);
@@ -208,7 +208,7 @@ int wgrad(const float* G, int ldg, const float* X, int ldx, int tensor_w, const 
   const int64_t slab = L.total;
   if (N % 32 || K % 32) return NERF_E_ARG;
   if (N == 256 && K == 64) {  // trunk.0: one 256x64 tile per split (4 waves of 64x64)
-    gemm_wgrad_kernel<256, 64, 4><<<w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, 1, 1);
+    gemm_wgrad_kernel<256, 64, 4, 32><<<w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, 1, 1);
     return NERF_OK;
   }
   if (N >= 128 && K > 128 && K % 128 == 64) {  // trunk.4 (K = 320): 128x128 tiles + one 128x64 column
@@ -228,7 +228,7 @@ int wgrad(const float* G, int ldg, const float* X, int ldx, int tensor_w, const 
     gemm_wgrad_kernel<128, 64, 2><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, K / 64, nt);
   } else if (N == 32 && K % 128 == 0) {
     const int nt = K / 128;
-    gemm_wgrad_kernel<32, 128, 1><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, K / 128, nt);
+    gemm_wgrad_kernel<32, 128, 1, 64><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, K / 128, nt);
   } else {
     return NERF_E_ARG;
   }

@@ -66,7 +66,7 @@ WSB carve_b(void* base, int64_t M, int training) {
     w.dCIN = (float*)take(Mp * 32 * 4);
     w.WTb = (nerf_bf16*)take(WTB_ELEMS * 2);
     w.S = n_splits(Mp);
-    w.rps = round_up(nerf_cdiv(Mp, w.S), 32);
+    w.rps = round_up(nerf_cdiv(Mp, w.S), 64);  // whole slabs for every wgrad MR
     w.partial = (float*)take((int64_t)w.S * L.total * 4);
   }
   w.bytes = (int64_t)(p - (char*)base);
@@ -273,7 +273,7 @@ int wgradb(const nerf_bf16* G, int ldg, const nerf_bf16* X, int ldx, int tensor_
     const int kb = K - 64;
     TRY(wgradb(G, ldg, X, ldx, tensor_w, w, N, kb, st));
     const int nt = N / 128;
-    gemm_wgrad_bf16_kernel<128, 64, 2><<<nt * w.S, 256, 0, st>>>(G, ldg, X + kb, ldx, P + kb, ldp, nullptr, slab,
+    gemm_wgrad_bf16_kernel<128, 64, 2, 64><<<nt * w.S, 256, 0, st>>>(G, ldg, X + kb, ldx, P + kb, ldp, nullptr, slab,
                                                                 w.rps, w.Mp, 1, nt);
     return NERF_OK;
   }
@@ -283,11 +283,11 @@ int wgradb(const nerf_bf16* G, int ldg, const nerf_bf16* X, int ldx, int tensor_
                                                                  K / 128, nt);
   } else if (N >= 128 && K % 64 == 0) {
     const int nt = (N / 128) * (K / 64);
-    gemm_wgrad_bf16_kernel<128, 64, 2><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp,
-                                                                K / 64, nt);
+    gemm_wgrad_bf16_kernel<128, 64, 2, 64><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp,
+                                                                    K / 64, nt);
   } else if (N == 32 && K % 128 == 0) {
     const int nt = K / 128;
-    gemm_wgrad_bf16_kernel<32, 128, 1><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp,
+    gemm_wgrad_bf16_kernel<32, 128, 1, 64><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp,
                                                                 K / 128, nt);
   } else {
     return NERF_E_ARG;
