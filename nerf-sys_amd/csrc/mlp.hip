@@ -207,17 +207,22 @@ int wgrad(const float* G, int ldg, const float* X, int ldx, int tensor_w, const 
   const int ldp = L.cols[tensor_w];
   const int64_t slab = L.total;
   if (N % 32 || K % 32) return NERF_E_ARG;
-  if (N == 256 && K == 64) {  // trunk.0: one 256x64 tile per split (4 waves of 64x64)
-    gemm_wgrad_kernel<256, 64, 4, 32><<<w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp, 1, 1);
+  // one 256 x 64 block (trunk.0 and the K = 320 remainder of trunk.4): four 64 x 64 tiles per split (1024
+  // workgroups) staging 32 rows per slab.  Measured on MI355X at the fine net's M (per launch): 256x64 tiles
+  // at 16 / 32 rows 398 / 358 us, 128x64 323 us, 128x32 309 us, 64x64 at 16 rows 272 us, this 252 us.
+  auto narrow = [&](const float* Xn, float* Pn, float* Pbn) {
+    gemm_wgrad_kernel<64, 64, 2, 32><<<4 * w.S, 256, 0, st>>>(G, ldg, Xn, ldx, Pn, ldp, Pbn, slab, w.rps, w.Mp, 1, 4);
+  };
+  if (N == 256 && K == 64) {  // trunk.0
+    narrow(X, P, Pb);
     return NERF_OK;
   }
-  if (N >= 128 && K > 128 && K % 128 == 64) {  // trunk.4 (K = 320): 128x128 tiles + one 128x64 column
+  if (N >= 128 && K > 128 && K % 128 == 64) {  // trunk.4 (K = 320): 128x128 tiles + one 256x64 block
     const int kb = K - 64;
     const int e = wgrad(G, ldg, X, ldx, tensor_w, w, N, kb, st);
     if (e != NERF_OK) return e;
-    const int nt = N / 128;
-    gemm_wgrad_kernel<128, 64, 2><<<nt * w.S, 256, 0, st>>>(G, ldg, X + kb, ldx, P + kb, ldp, nullptr, slab, w.rps,
-                                                           w.Mp, 1, nt);
+    if (N != 256) return NERF_E_ARG;
+    narrow(X + kb, P + kb, nullptr);
     return NERF_OK;
   }
   if (N >= 128 && K % 128 == 0) {

@@ -261,6 +261,16 @@ int ntb(const nerf_bf16* A, int lda, const nerf_bf16* B, int ldb, const float* b
   return NERF_E_ARG;
 }
 
+// one 64-column block of K (trunk.0, the K = 320 remainder of trunk.4, colour.0)
+int narrowb(const nerf_bf16* G, int ldg, const nerf_bf16* X, int ldx, float* P, int ldp, float* Pb, int64_t slab,
+            const WSB& w, int N, hipStream_t st) {
+  // 128 x 64 tiles, 64 rows per slab; measured per fine launch on MI355X: 111 us vs 64 x 64 tiles at 32 / 64
+  // rows 119 / 133 us (the fp32 path prefers the smaller tile)
+  gemm_wgrad_bf16_kernel<128, 64, 2, 64><<<(N / 128) * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps,
+                                                                         w.Mp, 1, N / 128);
+  return NERF_OK;
+}
+
 int wgradb(const nerf_bf16* G, int ldg, const nerf_bf16* X, int ldx, int tensor_w, const WSB& w, int N, int K,
            hipStream_t st) {
   const Layout& L = layout();
@@ -272,19 +282,14 @@ int wgradb(const nerf_bf16* G, int ldg, const nerf_bf16* X, int ldx, int tensor_
   if (N >= 128 && K > 128 && K % 128 == 64) {  // trunk.4 (K = 320): 128x128 tiles + a 128x64 column
     const int kb = K - 64;
     TRY(wgradb(G, ldg, X, ldx, tensor_w, w, N, kb, st));
-    const int nt = N / 128;
-    gemm_wgrad_bf16_kernel<128, 64, 2, 64><<<nt * w.S, 256, 0, st>>>(G, ldg, X + kb, ldx, P + kb, ldp, nullptr, slab,
-                                                                w.rps, w.Mp, 1, nt);
-    return NERF_OK;
+    return narrowb(G, ldg, X + kb, ldx, P + kb, ldp, nullptr, slab, w, N, st);
   }
   if (N >= 128 && K % 128 == 0) {
     const int nt = (N / 128) * (K / 128);
     gemm_wgrad_bf16_kernel<128, 128, 2><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp,
                                                                  K / 128, nt);
-  } else if (N >= 128 && K % 64 == 0) {
-    const int nt = (N / 128) * (K / 64);
-    gemm_wgrad_bf16_kernel<128, 64, 2, 64><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp,
-                                                                    K / 64, nt);
+  } else if (N >= 128 && K == 64) {
+    return narrowb(G, ldg, X, ldx, P, ldp, Pb, slab, w, N, st);
   } else if (N == 32 && K % 128 == 0) {
     const int nt = K / 128;
     gemm_wgrad_bf16_kernel<32, 128, 1, 64><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp,
