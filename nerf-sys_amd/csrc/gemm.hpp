@@ -337,7 +337,8 @@ static __global__ void reduce_splits_kernel(const float* __restrict__ src, int64
   float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   const float4* p = reinterpret_cast<const float4*>(src) + i;
   const int64_t st = slab / 4;
-  for (int s = 0; s < S; ++s) {
+#pragma unroll 16
+  for (int s = 0; s < S; ++s) {  // loads batched by the unroll, adds kept in split order
     const float4 v = p[s * st];
     a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
   }

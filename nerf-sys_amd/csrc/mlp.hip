@@ -26,7 +26,7 @@ struct WS {
   float *X3E, *Y[8], *O16, *CIN, *C0, *O3;
   uint32_t* MB[8];  // ReLU bitmasks of the trunk outputs [Mp][8] (colour layer 0 re-derives its mask from C0 > 0)
   // backward
-  float *dA, *dB, *dO16, *WT, *partial;
+  float *dA, *dB, *dO16, *WT, *partial, *partial2;
   int S;
   int64_t rps;
   int64_t bytes;
@@ -64,6 +64,7 @@ WS carve(void* base, int64_t M, int training) {
     w.S = n_splits(Mp);
     w.rps = round_up(nerf_cdiv(Mp, w.S), 64);  // whole slabs for every wgrad MR
     w.partial = take((int64_t)w.S * layout().total);
+    w.partial2 = take((int64_t)w.S * (layout().total - layout().off[18]));  // colour sums of the second halves
   }
   w.bytes = (int64_t)((char*)p - (char*)base);
   return w;
@@ -240,6 +241,31 @@ int wgrad(const float* G, int ldg, const float* X, int ldx, int tensor_w, const 
   return NERF_OK;
 }
 
+// reduce_splits plus the second-half colour sums: float4 i >= c0 of the packed gradient also adds
+// sum_s src2[s][i - c0] after the S slab terms (fixed order: bitwise reproducible)
+__global__ void reduce_splits2_kernel(const float* __restrict__ src, int64_t slab, int S, float* __restrict__ dst,
+                                      int64_t n4, int accumulate, const float* __restrict__ src2, int64_t slab2,
+                                      int64_t c0) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4* p = reinterpret_cast<const float4*>(src) + i;
+#pragma unroll 16
+  for (int s = 0; s < S; ++s) {  // loads batched by the unroll, adds kept in split order
+    const float4 v = p[s * (slab / 4)];
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  if (i >= c0) {
+    const float4* q = reinterpret_cast<const float4*>(src2) + (i - c0);
+#pragma unroll 16
+    for (int s = 0; s < S; ++s) {
+      const float4 v = q[s * (slab2 / 4)];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  reinterpret_cast<float4*>(dst)[i] = a;
+}
+
 }  // namespace
 
 extern "C" int64_t nerf_mlp_layout(int64_t* table) {
@@ -325,8 +351,8 @@ extern "C" int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma,
   transpose_kernel<<<dim3(8, 8, nj), 256, 0, st>>>(jobs);
 
   // colour branch + head activations in one kernel: dO16 and the colour weight / bias slabs
-  color_bwd_kernel<float, float><<<W.S, 256, 0, st>>>(d_rgb_sigma, W.O3, W.O16, W.C0, W.CIN, Wt(18), Wt(20), W.dO16, W.partial,
-                                        L.total, L.off[18], L.off[19], L.off[20], L.off[21], W.rps, M, Mp);
+  color_bwd_kernel<float, float><<<2 * W.S, 256, 0, st>>>(d_rgb_sigma, W.O3, W.O16, W.C0, W.CIN, Wt(18), Wt(20), W.dO16, W.partial,
+                                        L.total, L.off[18], L.off[19], L.off[20], L.off[21], W.rps, M, Mp, W.partial2, L.total - L.off[18]);
   // heads -> dZ7
   float* dcur = W.dA;
   float* dnext = W.dB;
@@ -351,6 +377,7 @@ extern "C" int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma,
     }
   }
   const int64_t n4 = L.total / 4;
-  reduce_splits_kernel<<<(unsigned)nerf_cdiv(n4, 256), 256, 0, st>>>(W.partial, L.total, W.S, d_w, n4, accumulate);
+  reduce_splits2_kernel<<<(unsigned)nerf_cdiv(n4, 256), 256, 0, st>>>(W.partial, L.total, W.S, d_w, n4, accumulate,
+                                                                      W.partial2, L.total - L.off[18], L.off[18] / 4);
   return nerf_launch_status();
 }

@@ -39,7 +39,7 @@ __device__ __forceinline__ void tail_st4(__bf16* p, float4 v) {
 }
 
 template <typename TA, typename TD>
-__global__ __launch_bounds__(256) void color_bwd_kernel(const float* __restrict__ g, const float* __restrict__ O3,
+__global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restrict__ g, const float* __restrict__ O3,
                                                         const float* __restrict__ O16,
                                                         const TA* __restrict__ C0,
                                                         const TA* __restrict__ CIN,
@@ -48,18 +48,24 @@ __global__ __launch_bounds__(256) void color_bwd_kernel(const float* __restrict_
                                                         TD* __restrict__ dO16, float* __restrict__ partial,
                                                         int64_t slab, int64_t off_w0, int64_t off_b0,
                                                         int64_t off_w1, int64_t off_b1, int64_t rps, int64_t M,
-                                                        int64_t Mp) {
+                                                        int64_t Mp, float* __restrict__ partial2, int64_t cslab) {
+  // dC0 overwrites C0 in place and the dgeo halves reuse the CIN tile (one extra barrier each): 70.6 KB of
+  // LDS, two workgroups per CU.  Workgroup 2s + h walks half h of split s; half 0 writes the colour sums into
+  // slab s, half 1 into row s of partial2 (cslab floats: the colour region off_w0 .. total of one slab).
   __shared__ __attribute__((aligned(16))) float s_c0[CB_ROWS * CB_C0];
-  __shared__ __attribute__((aligned(16))) float s_dc0[CB_ROWS * CB_C0];
+  float* const s_dc0 = s_c0;
   __shared__ __attribute__((aligned(16))) float s_cin[CB_ROWS * CB_CIN];
   __shared__ __attribute__((aligned(16))) float s_wt[32 * CB_WT];  // Wc0^T rows c < 32: [c][j]
   __shared__ __attribute__((aligned(16))) float s_w1[3 * 128];
   __shared__ float s_do3[CB_ROWS * 4];
-  __shared__ float s_geo[2 * CB_ROWS * CB_GEO];
+  float* const s_geo = s_cin;
+  static_assert(2 * CB_ROWS * CB_GEO <= CB_ROWS * CB_CIN, "dgeo halves fit the CIN tile");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 31, lh = lane >> 5;
-  const int64_t r0 = (int64_t)blockIdx.x * rps;
-  int64_t r1 = r0 + rps;
+  const int64_t sp = blockIdx.x >> 1, half = blockIdx.x & 1;
+  const int64_t rph = ((rps + 2 * CB_ROWS - 1) / (2 * CB_ROWS)) * CB_ROWS;  // rows of half 0
+  const int64_t r0 = sp * rps + half * rph;
+  int64_t r1 = half ? sp * rps + rps : r0 + rph;
   if (r1 > Mp) r1 = Mp;
 
   for (int i = tid; i < 32 * 128; i += 256) {
@@ -137,6 +143,7 @@ __global__ __launch_bounds__(256) void color_bwd_kernel(const float* __restrict_
       }
       if (jw == 0) b1 += d0;
     }
+    __syncthreads();  // every row of C0 read by the dWc1 sums before dC0 overwrites it
     {
       const int r = tid >> 2, jb = (tid & 3) * 32;
       const float d0 = s_do3[r * 4 + 0], d1 = s_do3[r * 4 + 1], d2 = s_do3[r * 4 + 2];
@@ -178,6 +185,7 @@ __global__ __launch_bounds__(256) void color_bwd_kernel(const float* __restrict_
         accg = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.z, a1.z, accg, 0, 0, 0);
         accg = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.w, a1.w, accg, 0, 0, 0);
       }
+      __syncthreads();  // all waves done reading CIN (dWc0) before the dgeo halves overwrite it
       // lane li holds row rb*32 + li; register 4q + e holds column 8q + 4lh + e
       float* grow = s_geo + (kh * CB_ROWS + rb * 32 + li) * CB_GEO;
 #pragma unroll
@@ -207,7 +215,7 @@ __global__ __launch_bounds__(256) void color_bwd_kernel(const float* __restrict_
     }
   }
   // ---- this split's slab: weight sums, bias sums (lane halves combined)
-  float* P = partial + (int64_t)blockIdx.x * slab;
+  float* P = half ? partial2 + sp * cslab - off_w0 : partial + sp * slab;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int n = (r & 3) + 8 * (r >> 2) + 4 * lh;
