@@ -39,7 +39,8 @@ __device__ __forceinline__ void nt_epilogue(const nerf_f32x16 (&acc)[TM][TN], in
 // runs at 79 % of the fp32 MFMA peak at its in-kernel clock of 2.3 GHz, tools/clock_probe.hip): an
 // LDS-DMA (global_load_lds) ring with counted vmcnt, a weights-stationary persistent kernel with
 // activations streamed to registers, prefetch loads pinned above the MFMA block (inline asm), BK = 32,
-// a 128x256 tile and 2..3 waves/SIMD were all 2-13 % slower.
+// a 128x256 tile and 2..3 waves/SIMD were all 2-13 % slower; so were (C2 step, 27.5 ms base) s_setprio 1 over
+// the MFMA block (28.5 ms) and iglp_opt(0) / iglp_opt(1) in the k-loop (30.4 / 30.2 ms).
 template <int BM, int BN, int WAVES_M, int EPI, int BK = 16, int NBUF = 2>
 __device__ __forceinline__ void gemm_nt_body(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb,
                                              const float* __restrict__ bias, float* __restrict__ C, int ldc,
