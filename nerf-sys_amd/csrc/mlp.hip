@@ -241,31 +241,6 @@ int wgrad(const float* G, int ldg, const float* X, int ldx, int tensor_w, const 
   return NERF_OK;
 }
 
-// reduce_splits plus the second-half colour sums: float4 i >= c0 of the packed gradient also adds
-// sum_s src2[s][i - c0] after the S slab terms (fixed order: bitwise reproducible)
-__global__ void reduce_splits2_kernel(const float* __restrict__ src, int64_t slab, int S, float* __restrict__ dst,
-                                      int64_t n4, int accumulate, const float* __restrict__ src2, int64_t slab2,
-                                      int64_t c0) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n4) return;
-  float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-  const float4* p = reinterpret_cast<const float4*>(src) + i;
-#pragma unroll 16
-  for (int s = 0; s < S; ++s) {  // loads batched by the unroll, adds kept in split order
-    const float4 v = p[s * (slab / 4)];
-    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-  }
-  if (i >= c0) {
-    const float4* q = reinterpret_cast<const float4*>(src2) + (i - c0);
-#pragma unroll 16
-    for (int s = 0; s < S; ++s) {
-      const float4 v = q[s * (slab2 / 4)];
-      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-    }
-  }
-  reinterpret_cast<float4*>(dst)[i] = a;
-}
-
 }  // namespace
 
 extern "C" int64_t nerf_mlp_layout(int64_t* table) {

@@ -2,7 +2,9 @@
 // fp32 or bf16 (TA) and dO16 written as fp32 or bf16 (TD); all arithmetic and the weight-gradient sums are fp32.
 // Measured: fp32 path 28.2 -> 28.0 ms/step (six launches and ~1.7 GB of HBM traffic per step removed); the bf16
 // path keeps its bf16-MFMA chain, which is faster there (8.36 vs 8.74 ms/step with this kernel: one 256-thread
-// workgroup per CU walking 48 tiles is latency-bound at ~11 us per tile).
+// workgroup per CU walking 48 tiles is latency-bound at ~11 us per tile; the two-workgroups-per-split version
+// below still measured 8.23 ms there against 8.15-8.18 ms for the chain, whose launches overlap the coarse
+// backward better).
 #pragma once
 #include "gemm.hpp"
 #include "mlp_common.hpp"
@@ -238,5 +240,30 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
   }
   if (tid == 128) P[off_b1 + 2] = b1;
 }
+// reduce_splits plus the second-half colour sums: float4 i >= c0 of the packed gradient also adds
+// sum_s src2[s][i - c0] after the S slab terms (fixed order: bitwise reproducible)
+static __global__ void reduce_splits2_kernel(const float* __restrict__ src, int64_t slab, int S, float* __restrict__ dst,
+                                      int64_t n4, int accumulate, const float* __restrict__ src2, int64_t slab2,
+                                      int64_t c0) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4* p = reinterpret_cast<const float4*>(src) + i;
+#pragma unroll 16
+  for (int s = 0; s < S; ++s) {  // loads batched by the unroll, adds kept in split order
+    const float4 v = p[s * (slab / 4)];
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  if (i >= c0) {
+    const float4* q = reinterpret_cast<const float4*>(src2) + (i - c0);
+#pragma unroll 16
+    for (int s = 0; s < S; ++s) {
+      const float4 v = q[s * (slab2 / 4)];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  reinterpret_cast<float4*>(dst)[i] = a;
+}
+
 }  // namespace nerf_mlp
 
