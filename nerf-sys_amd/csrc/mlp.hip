@@ -219,10 +219,10 @@ int wgrad(const float* G, int ldg, const float* X, int ldx, int tensor_w, const 
     return NERF_OK;
   }
   if (N >= 128 && K > 128 && K % 128 == 64) {  // trunk.4 (K = 320): 128x128 tiles + one 256x64 block
+    if (N != 256) return NERF_E_ARG;
     const int kb = K - 64;
     const int e = wgrad(G, ldg, X, ldx, tensor_w, w, N, kb, st);
     if (e != NERF_OK) return e;
-    if (N != 256) return NERF_E_ARG;
     narrow(X + kb, P + kb, nullptr);
     return NERF_OK;
   }
@@ -325,7 +325,8 @@ extern "C" int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma,
   float* Wht = T;  jobs.j[nj++] = TJob{Wt(16), Wht, 32, 256, 256};  // [256][32]
   transpose_kernel<<<dim3(8, 8, nj), 256, 0, st>>>(jobs);
 
-  // colour branch + head activations in one kernel: dO16 and the colour weight / bias slabs
+  // colour branch + head activations in one kernel: dO16 and the colour weight / bias slabs (two workgroups per
+  // split; the second halves' colour sums go to W.partial2 and are added by the final reduce)
   color_bwd_kernel<float, float><<<2 * W.S, 256, 0, st>>>(d_rgb_sigma, W.O3, W.O16, W.C0, W.CIN, Wt(18), Wt(20), W.dO16, W.partial,
                                         L.total, L.off[18], L.off[19], L.off[20], L.off[21], W.rps, M, Mp, W.partial2, L.total - L.off[18]);
   // heads -> dZ7
