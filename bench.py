@@ -1,21 +1,36 @@
 #!/usr/bin/env python3
 """Benchmark: rays/sec of the full NeRF train step (BASELINE.json configs[1]: Lego-style 800x800,
 64 coarse + 128 fine hierarchical, fp32, two networks), data parallel over N GPUs (one process per
-GPU, RCCL all-reduce of the flat gradient buffer), weak scaling (4096 rays per GPU per step).
+GPU, ONE RCCL all-reduce of the flat gradient buffer per step).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--strong] [--path engine|dropin] [--precision fp32|bf16]
+
+With --gpus N > 1 and no torchrun environment, bench.py starts `torch.distributed.run` with N ranks itself
+(before any GPU call) and exits with its status; under the driver's own torchrun it runs as one rank.
+Weak scaling (default): 4096 rays per GPU per step.  --strong: 4096 rays per step in total, each rank taking
+the rank-strided slice of the same global draw (an/scripts/create_clusters.py:799).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
-  roofline      — the dominant kernel (fine-net trunk GEMM class with the largest time share), its
-                  algorithmic FLOP per launch / mean launch time from HIP events recorded by the
-                  library inside the timed steps, against the fp32 MFMA peak (157.3 TFLOP/s);
+  roofline      — the dominant kernel class of the fine net's trunk GEMMs: the class (fwd / dgrad / wgrad)
+                  with the largest mean launch time among the classes whose launches run alone on the
+                  device (with the default two-stream step the fine forward runs beside the coarse
+                  backward, so its wall durations are not per-kernel times and it is not eligible;
+                  --no-overlap makes it eligible).  Durations are HIP events the library records on the
+                  launch stream inside every timed step; achieved = algorithmic FLOP per launch / mean.
   cpu_baseline  — the CPU oracle (a restatement of the reference's PyTorch path, pinned to its golden
-                  vectors) running the same train step on a bounded sample on this host (rank 0, N=1).
+                  vectors) running the same train step (4096 rays, 64+128, 2 nets), median of >= 5 steps
+                  on this host (rank 0, N=1).
+  dropin        — (N=1) the reference's own loop body (an/pipelines/online_stage/runtime_adapt.py:286-310:
+                  render_rays -> compute_mse_loss -> backward -> clip_grad_norm_ -> torch Adam) on this
+                  repo's drop-in render_rays + VanillaNeRF autograd path, same workload, timed beside the
+                  fused engine.  --path dropin makes it the reported value.
 """
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -23,7 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "nerf-sys_amd"))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch initialises no GPU)
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "rays/sec (train step) + full-image PSNR, 800×800 Lego, 64+128 samples"
@@ -32,6 +47,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no spars
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak
 MAC_PER_EVAL = 500864
 FLOP_PER_RAY = 769327104       # 6*MAC*(64 coarse + 192 fine evaluations), SURVEY.md §8(d)
+K256 = [1, 2, 3, 5, 6, 7]      # trunk layers with a 256x256 weight (trunk.0: K=63, trunk.4: K=319)
 
 
 def parse():
@@ -39,54 +55,206 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=4096, help="rays per GPU per step")
+    ap.add_argument("--batch", type=int, default=4096,
+                    help="rays per GPU per step (weak scaling) or per step in total (--strong)")
+    ap.add_argument("--strong", action="store_true", help="strong scaling: --batch rays per step over all ranks")
     ap.add_argument("--samples", type=int, default=64)
     ap.add_argument("--importance", type=int, default=128)
     ap.add_argument("--train-views", type=int, default=100)
     ap.add_argument("--scene", default="blender", choices=["blender", "llff"],
                     help="blender = Lego-style 800x800 (configs[1]/[2]); llff = Fern-style 1008x756 NDC (configs[3])")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--path", default="engine", choices=["engine", "dropin"],
+                    help="engine = the fused train step (headline); dropin = the reference loop body on the "
+                         "drop-in render_rays / VanillaNeRF autograd surface")
+    ap.add_argument("--cpu-batch", type=int, default=4096)
+    ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in path measurement beside the engine")
     ap.add_argument("--no-psnr", action="store_true",
                     help="skip the full-image PSNR of one held-out view rendered after the timed steps")
     ap.add_argument("--no-overlap", action="store_true", help="run the coarse-net backward on the main stream")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (the product); gloo = rehearsal of N ranks sharing the visible GPUs")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
                     help="MLP GEMM precision: fp32 = BASELINE configs[1] (default, the headline), bf16 = configs[2]")
     return ap.parse_args()
 
 
-def cpu_baseline(seconds, S, NI):
-    """The CPU oracle's train step (same op graph: 2 nets, 64+128, MSE, clip, Adam) on 128-ray batches."""
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a):
+    """--gpus N > 1 outside torchrun: run N ranks under torch.distributed.run as a CHILD process (no exec, no
+    GPU touched in this process) and return its exit status."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(S, NI, n, steps):
+    """The CPU oracle's train step (same op graph: 2 nets, 64+128, MSE coarse+fine, clip, Adam) on an n-ray
+    batch through a Blender-style camera: one warm-up step on 128 rays, then the median of `steps` steps.
+    Threads = the host CPU share this process is given (OMP_NUM_THREADS on the GPU box), not os.cpu_count(),
+    which there reports the whole machine."""
     from oracle import nerf_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    torch.set_num_threads(threads)
     torch.manual_seed(0)
-    n = 128
     g = torch.Generator().manual_seed(0)
     o = torch.tensor([0.0, -4.0311, 0.5]).expand(n, 3)
     d = torch.nn.functional.normalize(torch.randn(n, 3, generator=g) * 0.15 + torch.tensor([0.0, 1.0, -0.12]), dim=-1)
     rays = torch.cat([o, d, torch.full((n, 1), 2.0), torch.full((n, 1), 6.0)], -1)
     gt = torch.rand(n, 3, generator=g)
     tr = O.OracleTrainer(O.init_vanilla_params(1), O.init_vanilla_params(2))
-    tr.step(rays, gt, S, n_importance=NI)  # warm-up
-    steps, t0 = 0, time.perf_counter()
-    while True:
+    tr.step(rays[:128], gt[:128], S, n_importance=NI)  # warm-up (allocator, thread pool)
+    times = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
         tr.step(rays, gt, S, n_importance=NI)
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or (steps >= 3 and el >= seconds * 0.5 and el / steps * (steps + 1) > seconds * 1.5):
-            break
-    return {"value": round(n * steps / el, 2), "unit": "rays/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{steps} oracle train steps x {n} rays (64+128, 2 nets, fp32) in {el:.1f}s"}
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": round(n / med, 2), "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"median of {steps} oracle train steps x {n} rays (64+128, 2 nets, fp32, MSE coarse+fine, "
+                      f"clip, Adam): {med:.2f} s/step (steps {', '.join(f'{t:.2f}' for t in times)} s)",
+            "host_cpus": os.cpu_count(), "cpu_model": _cpu_model(), "torch_threads": torch.get_num_threads()}
+
+
+def dropin_run(rb, dev, a, world, rank, n_local):
+    """The reference loop body (runtime_adapt.py:286-310) on the drop-in surface: HierarchicalNeRF (coarse +
+    fine VanillaNeRF, autograd through the HIP MLP / compositing / sampling ops) -> compute_mse_loss (coarse +
+    fine terms) -> backward -> clip_grad_norm_(1.0) -> torch.optim.Adam ('sigma' / 'color' groups).  The ray
+    batch comes from images resident in HBM (the reference's DataLoader + .to(device) is not timed)."""
+    from types import SimpleNamespace
+    from nerf_amd.losses import compute_mse_loss
+    from nerf_amd.vanilla import HierarchicalNeRF
+    torch.manual_seed(0)
+    model = HierarchicalNeRF().to(dev).train()
+    grp = model.get_param_groups()
+    opt = torch.optim.Adam([{"params": grp["sigma"]["params"], "lr": 2e-3},
+                            {"params": grp["color"]["params"], "lr": 2e-3}])
+    P = SimpleNamespace(ray_samples=a.samples, n_importance=a.importance, chunk_points=1 << 22, color_space="linear")
+
+    def one(step):
+        rays, gt = _batch(rb, a, step, rank, world, n_local)
+        loss = compute_mse_loss(P, model, {"rays": rays, "rgbs": gt})
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        return loss
+
+    for s in range(a.warmup):
+        one(s)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(a.warmup, a.warmup + a.steps):
+        loss = one(s)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"value": round(n_local * a.steps / el, 1), "unit": "rays/s", "ms_per_step": round(el / a.steps * 1e3, 3),
+            "final_loss": round(float(loss.item()), 6),
+            "path": "render_rays + HierarchicalNeRF(VanillaNeRF x2) autograd + compute_mse_loss + "
+                    "clip_grad_norm_ + torch.optim.Adam (runtime_adapt.py:286-310)"}
+
+
+def _batch(rb, a, step, rank, world, n_local):
+    from nerf_amd.dp import shard_seed
+    if a.strong:   # one global draw per step, rank-strided slice
+        return rb.batch(a.batch, seed=step, shard=(rank, world))
+    return rb.batch(n_local, seed=shard_seed(step, rank, world))  # disjoint per-rank streams
+
+
+def roofline(tm, bf16, overlap):
+    M = tm["M"]
+    mean = lambda xs: sum(xs) / len(xs)
+    flop256 = 2.0 * M * 256 * 256
+    cls = {
+        "fwd": mean([st[i] for st in tm["fwd"] for i in K256]),
+        "wgrad": mean([st[i] for st in tm["wgrad"] for i in K256]),
+        "dgrad": mean([st[i - 1] for st in tm["dgrad"] for i in K256]),
+    }
+    eligible = [k for k in cls if not (overlap and k == "fwd")]
+    dom = max(eligible, key=lambda k: cls[k])
+    names = {"fwd": "gemm_nt fwd (bias+ReLU)", "wgrad": "gemm_wgrad (split-M, 128x128 tiles)",
+             "dgrad": "gemm_nt dgrad (ReLU mask)"}
+    ms = cls[dom]
+    ach = flop256 / (ms * 1e-3) / 1e12
+    kern = f"{names[dom]}, fine net M={M}: trunk 256x256 layers {K256}"
+    if bf16:
+        names = {k: v.replace("gemm_nt", "gemm_nt_bf16").replace("gemm_wgrad", "gemm_wgrad_bf16") for k, v in names.items()}
+        kern = f"{names[dom]}, fine net M={M}: trunk 256x256 layers {K256}"
+        # bf16 layers are HBM-bound: algorithmic bytes per launch per sample row = bf16 rows in (256 * 2 B) +
+        # bf16 rows out (256 * 2 B) [+ the 32-B ReLU bitmask word row of dgrad]; wgrad reads two bf16 rows
+        row = {"fwd": 256 * 2 + 256 * 2 + 32, "dgrad": 256 * 2 + 256 * 2 + 32, "wgrad": 256 * 2 + 256 * 2}[dom]
+        by = M * float(row)
+        ach_gbs = by / (ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": kern, "achieved": round(ach_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": by, "mfma_tflops": round(ach, 1),
+                "mfma_frac_bf16": round(ach / BF16_MFMA_PEAK_TFLOPS, 4)}
+    else:
+        roof = {"bound": "mfma", "kernel": kern, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "flop_per_launch": flop256}
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic_bf16.json" if bf16 else "traffic.json")
+    if os.path.exists(tpath):
+        try:
+            traffic = json.load(open(tpath)).get(dom)
+        except Exception:
+            traffic = None
+    roof.update({"traffic": traffic, "class": dom, "mean_launch_ms": round(ms, 4),
+                 "classes_ms": {k: round(v, 4) for k, v in cls.items()},
+                 "classes_frac": {k: round(flop256 / (v * 1e-3) / 1e12 / (BF16_MFMA_PEAK_TFLOPS if bf16 else
+                                                                       FP32_MFMA_PEAK_TFLOPS), 4)
+                                  for k, v in cls.items()},
+                 "rule": "largest mean launch time among classes that run alone" +
+                         (" (fine fwd overlaps the coarse backward: excluded)" if overlap else "")})
+    return roof
 
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
+    nccl = a.dist_backend == "nccl"
+    dev = torch.device("cuda", local if nccl else local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
+    if world > 1:
+        if nccl:
+            dist.init_process_group("nccl", device_id=dev)  # RCCL on ROCm
+        else:
+            dist.init_process_group("gloo")
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[dev.index]) if nccl else dist.barrier()
+
+    if a.path == "dropin" and (world > 1 or a.precision != "fp32"):
+        raise SystemExit("--path dropin runs on one GPU in fp32 (the reference loop body has no gradient exchange)")
+    if a.strong and a.batch % world:
+        raise SystemExit("--strong needs --batch divisible by the number of GPUs")
+    n_local = a.batch // world if a.strong else a.batch
 
     from nerf_amd.scene import make_blender_scene, make_llff_scene
     from nerf_amd.trainer import NeRFTrainer, RayBatcher
@@ -97,103 +265,72 @@ def main():
         scene = make_llff_scene(n_train=min(a.train_views, 20), n_test=1, seed=0, device=dev)
     else:
         scene = make_blender_scene(n_train=a.train_views, n_test=1, H=800, W=800, seed=0, device=dev)
-    coarse, fine = VanillaNeRF().to(dev), VanillaNeRF().to(dev)
-    tr = NeRFTrainer(coarse, fine, n_samples=a.samples, n_importance=a.importance, world_size=world, device=dev,
-                     overlap=not a.no_overlap, precision=a.precision)
     rb = RayBatcher(scene, dev)
-
-    from nerf_amd.dp import shard_seed
-
-    def one(step):
-        sd = shard_seed(step, rank, world)  # disjoint per-rank ray batches
-        rays, gt = rb.batch(a.batch, seed=sd)
-        return tr.step(rays, gt, seed=sd)
-
-    for s in range(a.warmup):
-        loss = one(s)
-    torch.cuda.synchronize()
-    tr.enable_timing(a.steps)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for s in range(a.warmup, a.warmup + a.steps):
-        loss = one(s)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    final_loss = float(loss.item())
-
-    # ---- roofline of the dominant kernel: the trunk GEMM family (fwd / dgrad / wgrad classes take equal
-    # shares of the step).  The fine forward shares the device with the coarse backward on the side stream,
-    # so its wall durations are not per-kernel times; the fine backward runs alone.  The quoted kernel is the
-    # dgrad GEMM (gemm_nt, ReLU-mask epilogue) at the fine net's M = 786,432 rows (12,288 blocks): per step 7
-    # trunk launches (N = K = 256) + 1 head launch (N = 256, K = 32) -- exactly the launches the profiler's
-    # per-(kernel, grid) average covers (tools/prof_summary.py).
-    tm = tr.collect_timing()
-    M = tm["M"]
-    k256 = [1, 2, 3, 5, 6, 7]
-    mean = lambda xs: sum(xs) / len(xs)
-    cls = {
-        "gemm_nt fwd (trunk 256x256, bias+ReLU)": mean([st[i] for st in tm["fwd"] for i in k256]),
-        "gemm_wgrad (trunk 256x256, split-M)": mean([st[i] for st in tm["wgrad"] for i in k256]),
-        "gemm_nt dgrad (trunk 256x256, ReLU mask)": mean([st[i - 1] for st in tm["dgrad"] for i in k256]),
-    }
-    dom = "gemm_nt dgrad (ReLU mask), fine net M=786432: 7 trunk 256x256 + 1 head 256x32 launches/step"
-    flop_trunk, flop_head = 2.0 * M * 256 * 256, 2.0 * M * 256 * 32
-    tot_ms = sum(sum(st) for st in tm["dgrad"]) + sum(tm["dgrad_head"])
-    n_launch = sum(len(st) for st in tm["dgrad"]) + len(tm["dgrad_head"])
-    tot_flop = flop_trunk * sum(len(st) for st in tm["dgrad"]) + flop_head * len(tm["dgrad_head"])
-    ach = tot_flop / (tot_ms * 1e-3) / 1e12
-    flops_launch = tot_flop / n_launch
     bf16 = a.precision == "bf16"
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic_bf16.json" if bf16 else "traffic.json")
-    if os.path.exists(tpath):
-        try:
-            traffic = json.load(open(tpath)).get("gemm_nt dgrad (trunk 256x256, ReLU mask)")
-        except Exception:
-            traffic = None
-    if bf16:
-        # bf16 layers are HBM-bound: algorithmic bytes per launch = bf16 input-gradient rows in (K * 2 B) +
-        # bf16 rows out (256 * 2 B) + the ReLU bitmask word row (32 B) per sample row
-        by_trunk, by_head = M * (256 * 2 + 256 * 2 + 32.0), M * (32 * 2 + 256 * 2 + 32.0)
-        tot_by = by_trunk * sum(len(st) for st in tm["dgrad"]) + by_head * len(tm["dgrad_head"])
-        ach_gbs = tot_by / (tot_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "kernel": dom.replace("gemm_nt", "gemm_nt_bf16"), "achieved": round(ach_gbs, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "bytes_per_launch": tot_by / n_launch, "mfma_tflops": round(ach, 1),
-                "mfma_frac_bf16": round(ach / BF16_MFMA_PEAK_TFLOPS, 4)}
-    else:
-        roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                "flop_per_launch": flops_launch}
-    roof.update({"mean_launch_ms": round(tot_ms / n_launch, 4), "classes_ms": {k: round(v, 4) for k, v in cls.items()}})
-    peak_step = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
 
-    rays_total = a.batch * world * a.steps
-    value = rays_total / el
+    engine = None
+    if a.path == "engine" or world == 1:
+        coarse, fine = VanillaNeRF().to(dev), VanillaNeRF().to(dev)
+        tr = NeRFTrainer(coarse, fine, n_samples=a.samples, n_importance=a.importance, world_size=world, device=dev,
+                         overlap=not a.no_overlap, precision=a.precision)
+
+        def one(step):
+            rays, gt = _batch(rb, a, step, rank, world, n_local)
+            return tr.step(rays, gt, seed=step * world + rank)
+
+        for s in range(a.warmup):
+            loss = one(s)
+        torch.cuda.synchronize()
+        tr.enable_timing(a.steps)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s in range(a.warmup, a.warmup + a.steps):
+            loss = one(s)
+        barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        engine = {"value": round(n_local * world * a.steps / el, 1), "ms_per_step": round(el / a.steps * 1e3, 3),
+                  "final_loss": round(float(loss.item()), 6), "roofline": roofline(tr.collect_timing(), bf16, tr.overlap)}
+
+    drop = None
+    if world == 1 and (a.path == "dropin" or not a.no_dropin) and not bf16:
+        drop = dropin_run(rb, dev, a, world, rank, n_local)
+
+    peak_step = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
+    main_res = drop if a.path == "dropin" else engine
+    value = main_res["value"]
     out = {
-        "metric": METRIC, "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if bf16 else "f32", "data": "synthetic",
+        "metric": METRIC, "value": value, "unit": "rays/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": main_res["ms_per_step"], "higher_is_better": True,
+        "scaling": "strong" if a.strong else "weak", "vs_baseline": None, "dtype": "bf16" if bf16 else "f32",
+        "data": "synthetic",
         "config": {"workload": ("Fern-style 1008x756 forward-facing NDC (synthetic analytic scene, 20 views)"
                                 if a.scene == "llff" else "Lego-style 800x800 (synthetic analytic scene, 100 views)") +
                                ", 64 coarse + 128 fine hierarchical, 2 x (8x256 MLP), " +
                                ("bf16 MLP + fp32 compositing" if bf16 else "fp32") +
-                               ", train step incl. ray gen + Adam",
-                   "global_batch": a.batch * world, "rays_per_gpu": a.batch, "samples": [a.samples, a.importance],
-                   "parallelism": f"dp{world}", "precision": a.precision},
-        "roofline": roof,
+                               ", train step incl. ray gen + Adam" +
+                               (" [drop-in render_rays/autograd path]" if a.path == "dropin" else " [fused engine]"),
+                   "global_batch": a.batch if a.strong else a.batch * world, "rays_per_gpu": n_local,
+                   "samples": [a.samples, a.importance], "parallelism": f"dp{world}", "precision": a.precision,
+                   "path": a.path},
+        "rccl_ranks": world, "backend": ("nccl (RCCL)" if nccl else "gloo (rehearsal)") if world > 1 else None,
+        "roofline": engine["roofline"] if engine else None,
         "step_mfma_frac": round(value * FLOP_PER_RAY / world / 1e12 / peak_step, 4),
-        "final_loss": round(final_loss, 6),
+        "final_loss": main_res["final_loss"],
     }
-    if not a.no_psnr and rank == 0:
+    if a.path == "dropin" and engine:
+        out["engine"] = {k: engine[k] for k in ("value", "ms_per_step")}
+    elif drop:
+        out["dropin"] = drop
+    if out.get("dropin") or out.get("engine"):
+        e, d = (engine, drop)
+        out["dropin_vs_engine"] = round(d["value"] / e["value"], 4)
+    if not a.no_psnr and rank == 0 and engine:
         from nerf_amd.ray_rendering import render_image
         tr.sync_to_modules()
         coarse.eval()
@@ -207,13 +344,13 @@ def main():
                             "convergence: tools/train_psnr.py, profiles/r01/psnr_*.jsonl (fp32 28.1 dB / bf16 "
                             "28.1 dB after 3000 steps)")
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.samples, a.importance)
+        out["cpu_baseline"] = cpu_baseline(a.samples, a.importance, a.cpu_batch, a.cpu_steps)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.barrier()  # the other ranks wait for rank 0's PSNR render / report before tearing down
+        barrier()  # the other ranks wait for rank 0's PSNR render / report before tearing down
         dist.destroy_process_group()
 
 

@@ -202,9 +202,22 @@ def composite_fwd(rgb_sigma, t, bg=None, sigma_scale=1.0, gt=None, color_space="
 
 
 def composite_bwd(rgb_sigma, t, bg, g_rgb, g_depth=None, g_acc=None, g_w=None, sigma_scale=1.0, out=None):
+    need(rgb_sigma, "rgb_sigma"), need(t, "t"), need(g_rgb, "g_rgb")
     n, S = t.shape
+    if rgb_sigma.numel() != n * S * 4 or rgb_sigma.shape[-1] != 4:   # (N,S,4) or the MLP's (N*S,4)
+        raise ValueError(f"rgb_sigma must hold ({n},{S},4), got {tuple(rgb_sigma.shape)}")
+    if tuple(g_rgb.shape) != (n, 3):
+        raise ValueError(f"g_rgb must be ({n},3), got {tuple(g_rgb.shape)}")
+    for x, name, shape in ((bg, "bg", (n, 3)), (g_depth, "g_depth", (n,)), (g_acc, "g_acc", (n,)),
+                           (g_w, "g_w", (n, S))):
+        if x is not None:
+            need(x, name)
+            if tuple(x.shape) != shape:
+                raise ValueError(f"{name} must be {shape}, got {tuple(x.shape)}")
     if out is None:
         out = torch.empty_like(rgb_sigma)
+    else:
+        need(out, "out")
     check(lib().nerf_composite_bwd(ptr(rgb_sigma), ptr(t), ptr(bg), n, S, float(sigma_scale), ptr(g_rgb),
                                    ptr(g_depth), ptr(g_acc), ptr(g_w), ptr(out), stream()), "nerf_composite_bwd")
     return out

@@ -37,9 +37,14 @@ class RayBatcher:
         self.images = scene.images.to(device).contiguous()
         self.device = device
 
-    def batch(self, n, seed):
+    def batch(self, n, seed, shard=None):
+        """n random pixels from the counter RNG stream ``seed``.  ``shard=(rank, world)`` keeps the rank-strided
+        slice pix[rank::world] of that draw (an/scripts/create_clusters.py:799), so every world size sees
+        the same global batch (strong scaling)."""
         s = self.scene
         pix = K.pick_pixels(n, self.poses.shape[0], s.H, s.W, seed, self.device)
+        if shard is not None and shard[1] > 1:
+            pix = pix[shard[0]::shard[1]].contiguous()
         fx, fy, cx, cy = s.intrinsics
         rays, gt = K.rays_gen(self.poses, s.H, s.W, fx, fy, cx, cy, pix=pix, near=s.near if not s.ndc else 0.0,
                               far=s.far if not s.ndc else 1.0, images_u8=self.images)

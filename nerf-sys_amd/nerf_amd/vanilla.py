@@ -221,6 +221,28 @@ class VanillaNeRF(nn.Module):
         return out.view(*shp, 4)
 
 
+class HierarchicalNeRF(nn.Module):
+    """A coarse + fine pair behind ONE model object, for callers that only pass ``model`` (the reference's
+    compute_mse_loss(P, model, data), nerfs/losses.py:10-32): ``model(x_d, params)`` is the coarse expert and
+    ``render_rays(model, ..., n_importance=k)`` renders the fine pass with ``model.fine``.  Parameter groups
+    merge both nets ('sigma' / 'color', models/inr/meta_ngp.py:446-469)."""
+
+    def __init__(self, coarse: Optional[VanillaNeRF] = None, fine: Optional[VanillaNeRF] = None):
+        super().__init__()
+        self.coarse = coarse if coarse is not None else VanillaNeRF()
+        self.fine = fine if fine is not None else VanillaNeRF()
+        self.use_occ = False
+        self.use_bg_nerf = False
+        self.dim_out = 4
+
+    def get_param_groups(self):
+        gc, gf = self.coarse.get_param_groups(), self.fine.get_param_groups()
+        return {k: {"params": gc[k]["params"] + gf[k]["params"]} for k in gc}
+
+    def forward(self, x_d: torch.Tensor, params=None) -> torch.Tensor:
+        return self.coarse(x_d, params=params)
+
+
 _EXP_MAX = {torch.float16: 11.089866488, torch.bfloat16: 88.722839111, torch.float32: 88.722839111,
             torch.float64: 709.782712893}
 

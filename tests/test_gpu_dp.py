@@ -1,0 +1,116 @@
+"""The product trainer's data-parallel step at world size 2, on the GPU.
+
+Two processes share cuda:0 and talk over gloo (RCCL refuses two ranks on one device; gloo all-reduces CUDA
+tensors through the host).  Each runs ``NeRFTrainer(world_size=2)`` — the HIP step, the 1/(3 N_global) loss
+normaliser, ``allreduce_flat`` of the flat [grads | loss] buffer (the real ``dist.all_reduce``), clip and the HIP
+Adam — on its rank-strided half of a fixed batch (an/scripts/create_clusters.py:799) with injected jitter.
+The result must equal the single-process full-batch step: loss, reduced flat gradient, post-Adam parameters
+(both ranks bitwise equal to each other), and the second step's loss."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from oracle import nerf_oracle as O
+
+pytestmark = pytest.mark.gpu
+N, S, NI = 256, 64, 128
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _inputs():
+    g = torch.Generator().manual_seed(17)
+    o = torch.tensor([0.0, -4.0311, 0.5]).expand(N, 3)
+    d = torch.nn.functional.normalize(torch.randn(N, 3, generator=g) * 0.2 + torch.tensor([0.0, 1.0, -0.12]), dim=-1)
+    rays = torch.cat([o, d, torch.full((N, 1), 2.0), torch.full((N, 1), 6.0)], -1)
+    gt = torch.rand(N, 3, generator=g)
+    us = [torch.rand(N, S, generator=g) for _ in range(2)]
+    up = [torch.rand(N, NI, generator=g) for _ in range(2)]
+    return rays, gt, us, up
+
+
+def _run(world, rank, dev):
+    from nerf_amd.trainer import NeRFTrainer
+    from nerf_amd.vanilla import VanillaNeRF
+    rays, gt, us, up = _inputs()
+    sl = slice(rank, None, world)
+    tr = NeRFTrainer(VanillaNeRF().load_reference_state(O.init_vanilla_params(1)).to(dev),
+                     VanillaNeRF().load_reference_state(O.init_vanilla_params(2)).to(dev),
+                     n_samples=S, n_importance=NI, world_size=world, device=dev)
+    out = {"loss": [], "grad": [], "params": []}
+    for step in range(2):
+        loss = tr.step(rays[sl].contiguous().to(dev), gt[sl].contiguous().to(dev), seed=step,
+                       u_strat=us[step][sl].contiguous().to(dev), u_pdf=up[step][sl].contiguous().to(dev))
+        torch.cuda.synchronize()
+        out["loss"].append(float(loss.item()))
+        out["grad"].append(tr.grads.detach().cpu().clone())
+        out["params"].append(tr.params.detach().cpu().clone())
+    return out
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "nerf-sys_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        q.put((rank, _run(world, rank, dev)))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent on q.get
+        q.put((rank, repr(e)))
+        raise
+
+
+def test_trainer_world2_equals_full_batch():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert isinstance(res[r], dict), f"rank {r} failed: {res[r]}"
+        assert procs[r].exitcode == 0
+    full = _run(1, 0, torch.device("cuda", 0))
+    r0, r1 = res[0], res[1]
+    for step in range(2):
+        # every rank holds the same reduced buffer and applies the same update
+        assert torch.equal(r0["grad"][step], r1["grad"][step]), f"step {step}: ranks disagree on the reduced gradient"
+        assert torch.equal(r0["params"][step], r1["params"][step]), f"step {step}: ranks diverged"
+        assert r0["loss"][step] == r1["loss"][step]
+        lf = full["loss"][step]
+        assert abs(r0["loss"][step] - lf) <= 1e-6 * max(1.0, lf), (step, r0["loss"][step], lf)
+    # step 0: reduced flat gradient (same start point) within rounding of the full-batch one
+    g, gf = r0["grad"][0].double(), full["grad"][0].double()
+    P = g.numel() // 2
+    for k in range(2):
+        a, b = g[k * P:(k + 1) * P], gf[k * P:(k + 1) * P]
+        err = (a - b).abs().max().item()
+        assert err <= 1e-5 * b.abs().max().item(), f"net {k}: grad max err {err:.3e} vs scale {b.abs().max():.3e}"
+    # post-Adam parameters of step 0: the update difference the two measured gradients imply (Adam's first step is
+    # lr * g/(|g|+eps): rounding-level gradient differences at the 1e-8 noise floor can move an element by <= 2 lr)
+    norm = gf.norm().item()
+    coef = min(1.0, 1.0 / (norm + 1e-6))
+    phi = lambda x: x * coef / ((x * coef).abs() + 1e-8)
+    bound = 2e-3 * (phi(g) - phi(gf)).abs() * 1.02 + 2e-9 + 2.5e-7 * (1 + full["params"][0].double().abs())
+    perr = (r0["params"][0].double() - full["params"][0].double()).abs()
+    assert (perr <= bound).all(), f"post-Adam: {int((perr > bound).sum())} elements beyond the implied bound"

@@ -14,15 +14,15 @@ from collections import defaultdict
 root = sys.argv[1]
 M_FINE = 4096 * 192
 CLASSES = {
-    "gemm_nt fwd (trunk 256x256, bias+ReLU)": ("gemm_nt_kernel<128, 128, 2, 1,", 0),
-    "gemm_nt dgrad (trunk 256x256, ReLU mask)": ("gemm_nt_kernel<128, 128, 2, 2,", 0),
-    "gemm_wgrad (trunk 256x256, split-M)": ("gemm_wgrad_kernel<128, 128, 2,", 0),
+    "fwd": ("gemm_nt_kernel<128, 128, 2, 1,", 0),
+    "dgrad": ("gemm_nt_kernel<128, 128, 2, 2,", 0),
+    "wgrad": ("gemm_wgrad_kernel<128, 128, 2,", 0),
 }
 if len(sys.argv) > 2 and sys.argv[2] == "bf16":  # bf16 MLP (configs[2]) kernel names
     CLASSES = {
-        "gemm_nt fwd (trunk 256x256, bias+ReLU)": ("gemm_nt_bf16_wsr_kernel<256, 128, 1, 1,", 0),
-        "gemm_nt dgrad (trunk 256x256, ReLU mask)": ("gemm_nt_bf16_wsr_kernel<256, 128, 2, 1,", 0),
-        "gemm_wgrad (trunk 256x256, split-M)": ("gemm_wgrad_bf16_kernel<128, 128, 2,", 0),
+        "fwd": ("gemm_nt_bf16_wsr_kernel<256, 128, 1, 1,", 0),
+        "dgrad": ("gemm_nt_bf16_wsr_kernel<256, 128, 2, 1,", 0),
+        "wgrad": ("gemm_wgrad_bf16_kernel<128, 128, 2,", 0),
     }
 
 

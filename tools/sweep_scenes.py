@@ -31,6 +31,50 @@ FLOP_PER_RAY = 769327104
 PEAK = {"fp32": 157.3e12, "bf16": 2500e12}
 
 
+def _psnr(coarse, fine, scene, S=64, NI=128):
+    from nerf_amd.losses import image_psnr
+    from nerf_amd.ray_rendering import render_image
+    fx, fy, cx, cy = scene.intrinsics
+    ps = []
+    for v in range(scene.test_poses.shape[0]):
+        img, _, _ = render_image(coarse, H=scene.H, W=scene.W, fx=fx, fy=fy, cx=cx, cy=cy, c2w=scene.test_poses[v],
+                                 near=scene.near, far=scene.far, ray_samples=S, n_importance=NI, fine_model=fine)
+        ps.append(image_psnr(img, scene.test_images[v], "linear"))
+    return sum(ps) / len(ps)
+
+
+def train_scene(sid, *, steps, batch, train_views, test_views, precision, lr, dev, H=800, W=800,
+                initial_psnr=False):
+    """Train one seeded synthetic scene with the benchmarked step; returns its record (PSNR over the held-out
+    views, train-loop rays/s, the per-step loss trajectory)."""
+    from nerf_amd.scene import make_blender_scene
+    from nerf_amd.trainer import NeRFTrainer, RayBatcher
+    from nerf_amd.vanilla import VanillaNeRF
+    torch.manual_seed(sid)
+    scene = make_blender_scene(n_train=train_views, n_test=test_views, H=H, W=W, seed=sid, device=dev)
+    coarse, fine = VanillaNeRF().to(dev), VanillaNeRF().to(dev)
+    rec = {"scene_seed": sid}
+    if initial_psnr:
+        rec["psnr_init"] = round(_psnr(coarse.eval(), fine.eval(), scene), 3)
+    tr = NeRFTrainer(coarse, fine, n_samples=64, n_importance=128, lr_sigma=lr, lr_color=lr, device=dev,
+                     precision=precision)
+    rb = RayBatcher(scene, dev)
+    losses = torch.zeros(steps, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for step in range(steps):
+        rays, gt = rb.batch(batch, seed=step)
+        losses[step:step + 1].copy_(tr.step(rays, gt, seed=step))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    tr.sync_to_modules()
+    coarse.eval(), fine.eval()
+    ls = losses.cpu().tolist()
+    rec.update({"steps": steps, "train_s": round(el, 2), "rays_per_s": round(steps * batch / el, 1),
+                "loss": round(ls[-1], 6), "psnr": round(_psnr(coarse, fine, scene), 3), "losses": ls})
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scenes", type=int, default=8)
@@ -48,41 +92,14 @@ def main():
         dist.init_process_group("gloo")  # only the final result gather crosses ranks
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    from nerf_amd.losses import image_psnr
-    from nerf_amd.ray_rendering import render_image
-    from nerf_amd.scene import make_blender_scene
-    from nerf_amd.trainer import NeRFTrainer, RayBatcher
-    from nerf_amd.vanilla import VanillaNeRF
-
     results = []
     for sid in range(rank, a.scenes, world):
-        torch.manual_seed(sid)
-        scene = make_blender_scene(n_train=a.train_views, n_test=a.test_views, seed=sid, device=dev)
-        coarse, fine = VanillaNeRF().to(dev), VanillaNeRF().to(dev)
-        tr = NeRFTrainer(coarse, fine, n_samples=64, n_importance=128, lr_sigma=a.lr, lr_color=a.lr, device=dev,
-                         precision=a.precision)
-        rb = RayBatcher(scene, dev)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for step in range(a.steps):
-            rays, gt = rb.batch(a.batch, seed=step)
-            loss = tr.step(rays, gt, seed=step)
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        tr.sync_to_modules()
-        coarse.eval(), fine.eval()
-        fx, fy, cx, cy = scene.intrinsics
-        ps = []
-        for v in range(scene.test_poses.shape[0]):
-            img, _, _ = render_image(coarse, H=scene.H, W=scene.W, fx=fx, fy=fy, cx=cx, cy=cy, c2w=scene.test_poses[v],
-                                     near=scene.near, far=scene.far, ray_samples=64, n_importance=128, fine_model=fine)
-            ps.append(image_psnr(img, scene.test_images[v], "linear"))
-        rec = {"scene_seed": sid, "rank": rank, "steps": a.steps, "train_s": round(el, 2),
-               "rays_per_s": round(a.steps * a.batch / el, 1), "loss": round(float(loss.item()), 6),
-               "psnr": round(sum(ps) / len(ps), 3)}
+        rec = train_scene(sid, steps=a.steps, batch=a.batch, train_views=a.train_views, test_views=a.test_views,
+                          precision=a.precision, lr=a.lr, dev=dev)
+        rec["rank"] = rank
+        rec.pop("losses", None)
         print(json.dumps(rec), flush=True)
         results.append(rec)
-        del tr, coarse, fine, scene, rb
         torch.cuda.empty_cache()
     if world > 1:
         allr = [None] * world
