@@ -13,7 +13,10 @@
 // bitmasks; backward: dA/dB [Mp][256] bf16, dO16/dO3 [Mp][32] bf16, dCIN [Mp][32] fp32, dC0 [Mp][128]
 // bf16, bf16 transposed weights, S fp32 partial slabs of the packed gradient.
 #include "gemm_bf16.hpp"
+#include "mlp_bf16_fused.hpp"
 #include "mlp_common.hpp"
+
+#include <stdlib.h>
 
 namespace {
 using namespace nerf_mlp;
@@ -22,7 +25,7 @@ constexpr int64_t WTB_ELEMS = 7 * 65536 + 256 * 32 + 128 * 32 + 32 * 128;
 
 struct WSB {
   int64_t Mp;
-  nerf_bf16 *Wb, *X3E, *Y[8], *CIN, *C0;
+  nerf_bf16 *Wb, *Wf, *X3E, *Y[8], *CIN, *C0;
   float *O16, *O3;
   uint32_t *MB[8], *MC0;
   nerf_bf16 *dA, *dB, *dO16, *dO3, *dC0, *WTb;
@@ -44,6 +47,7 @@ WSB carve_b(void* base, int64_t M, int training) {
   };
   const Layout& L = layout();
   w.Wb = (nerf_bf16*)take(L.total * 2);
+  w.Wf = (nerf_bf16*)take(nerf_fused::frag_tab().off[nerf_fused::FT] * 2);
   w.X3E = (nerf_bf16*)take(Mp * 320 * 2);
   if (training) {
     for (int i = 0; i < 8; ++i) w.Y[i] = (i == 3) ? w.X3E : (nerf_bf16*)take(Mp * 256 * 2);
@@ -302,6 +306,57 @@ int wgradb(const nerf_bf16* G, int ldg, const nerf_bf16* X, int ldx, int tensor_
 
 }  // namespace
 
+// NERF_BF16_FUSED=0 selects the layer-by-layer forward (one GEMM launch per layer, activations through HBM) for
+// A/B measurements; the default is the fused single-launch forward (mlp_bf16_fused.hpp).
+bool fused_fwd_enabled() {
+  const char* e = getenv("NERF_BF16_FUSED");  // read per call: tests switch paths inside one process
+  return !(e && e[0] == '0');
+}
+
+int fused_forward(const float* w, const float* x_d, int64_t M, float* rgb_sigma, const WSB& W, int training,
+                  hipEvent_t* ev, hipStream_t st) {
+  using namespace nerf_fused;
+  const Layout& L = layout();
+  const FragTab T = frag_tab();
+  const int64_t Mp = W.Mp;
+  for (int t = 0; t < NT; ++t)
+    if (L.off[t] != lay_off(t)) return NERF_E_ARG;  // device-side compile-time offsets must match the layout
+  if (training) {  // the kernel addresses Y[i] / MB[i] from one base each
+    for (int i = 0; i < 8; ++i) {
+      if (i != 3 && W.Y[i] != W.Y[0] + (int64_t)(i < 3 ? i : i - 1) * Mp * 256) return NERF_E_ARG;
+      if (W.MB[i] != W.MB[0] + (int64_t)i * Mp * 8) return NERF_E_ARG;
+    }
+  }
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
+  }
+  frag_pack_kernel<<<(unsigned)nerf_cdiv(T.off[FT] / 8, 256), 256, 0, st>>>(w, W.Wf, T);
+  pe_prefill_bf16_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(x_d, M, Mp, W.X3E, W.CIN);
+  FusedArgs A{};
+  A.wf = W.Wf;
+  A.w = w;
+  A.X3E = W.X3E;
+  A.Y = training ? W.Y[0] : nullptr;
+  A.MB = training ? W.MB[0] : nullptr;
+  A.O16 = W.O16; A.CIN = W.CIN; A.C0 = W.C0; A.MC0 = training ? W.MC0 : nullptr; A.O3 = W.O3;
+  A.out = rgb_sigma;
+  A.M = M;
+  A.Mp = Mp;
+  A.ntiles = (int)(Mp / BMF);  // Mp is a multiple of 256: whole 128-row tiles
+  const int grid = A.ntiles < n_cu ? A.ntiles : n_cu;  // persistent, one workgroup per CU (LDS ~87 KB)
+  if (ev) (void)hipEventRecord(ev[0], st);
+  if (training)
+    mlp_fwd_fused_bf16_kernel<true><<<grid, 512, 0, st>>>(A);
+  else
+    mlp_fwd_fused_bf16_kernel<false><<<grid, 512, 0, st>>>(A);
+  if (ev)
+    for (int i = 1; i < 16; ++i) (void)hipEventRecord(ev[i], st);  // ev[0] -> ev[1] brackets the fused launch
+  return nerf_launch_status();
+}
+
 extern "C" int64_t nerf_mlp_workspace_bytes_bf16(int64_t M, int training) {
   if (M < 0) return -1;
   return carve_b(nullptr, M, training).bytes + 256;
@@ -318,6 +373,7 @@ extern "C" int nerf_mlp_fwd_bf16(const float* w, const float* x_d, int64_t M, fl
   const int64_t Mp = W.Mp;
   auto Wb = [&](int t) { return W.Wb + L.off[t]; };
   auto Bias = [&](int t) { return w + L.off[t]; };
+  if (fused_fwd_enabled()) return fused_forward(w, x_d, M, rgb_sigma, W, training, ev, st);
 
   to_bf16_kernel<<<(unsigned)nerf_cdiv(L.total / 4 + 1, 256), 256, 0, st>>>(w, L.total, W.Wb);
   pe_xyz_bf16_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(x_d, M, Mp, W.X3E);

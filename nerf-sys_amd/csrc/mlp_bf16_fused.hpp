@@ -1,0 +1,547 @@
+// Fused bf16 forward of the whole vanilla NeRF MLP (BASELINE.json configs[2]) — ONE launch per pass instead of
+// one GEMM launch per layer with every activation through HBM.  models/inr/meta_vanilla.py:109-154:
+//   enc (xyz PE) -> 8 x [Linear + ReLU] (skip cat([h, enc]) at trunk.4) -> head (sigma | 15 geo)
+//   -> cat([geo, dir PE]) -> Linear 42->128 + ReLU -> Linear 128->3 -> sigmoid ; sigma = trunc_exp
+//
+// A workgroup (4 waves, one per SIMD) owns a tile of 128 sample rows for the whole network.  The tile's
+// activations stay in LDS across the layers (H [128][256] bf16; E [128][64] holds the xyz encoding for trunk.0
+// / trunk.4 and then the colour input); the MFMA accumulators hold one layer's output tile (wave w: output
+// columns 64w..64w+63 of all 128 rows, 4 x 2 `v_mfma_f32_32x32x16_bf16` tiles of C^T as in gemm_bf16.hpp).
+// Weights stream from L2 in a fragment-major bf16 image (frag_pack_kernel): the 16-B A-operand fragment of
+// lane l for (32-row block nb, 16-deep k-step ks) sits at ((nb * KS + ks) * 64 + l) * 8, so one wave-load
+// reads 1 KiB contiguous.  Four k-steps of fragments are kept in flight in a register ring that runs across
+// layer boundaries (the next layer's first fragments load under the current layer's last MFMAs).  Biases
+// initialise the accumulators.  Epilogue per layer: barrier, ReLU + bf16 into H (16-B LDS stores after the
+// v_permlane32_swap pairing of gemm_bf16.hpp), barrier; in training the tile is then copied H -> HBM with
+// coalesced 512-B row stores (the activations nerf_mlp_bwd_bf16 reads) and the ReLU bitmask words go out from
+// the accumulator registers.
+//
+// HBM per sample row: reads enc (128 B, written by pe_prefill_bf16_kernel with the colour-input prefill,
+// 128 B), writes rgb_sigma (16 B); training adds the saved activations (8 x 512 B + heads ~0.5 KB).
+// MFMA work per 128-row tile: 4,112 32x32x16 MFMAs (trunk 3,840, heads 272); weights read from L2 once per
+// tile (~1 MB).
+#pragma once
+#include "gemm_bf16.hpp"
+#include "mlp_common.hpp"
+
+namespace nerf_fused {
+using namespace nerf_mlp;
+
+constexpr int FT = 11;                      // fragment tensors: trunk.0..7, head, colour0, colour1
+constexpr int BMF = 128;                    // rows per tile
+constexpr int HP = 264, EP = 72, CP = 136;  // LDS row pitches (bf16): 16 rows -> 16 distinct 16-B bank slots
+constexpr int FN[FT] = {256, 256, 256, 256, 256, 256, 256, 256, 32, 128, 32};
+constexpr int FK[FT] = {64, 256, 256, 256, 320, 256, 256, 256, 256, 64, 128};
+constexpr int FSRC[FT] = {0, 2, 4, 6, 8, 10, 12, 14, 16, 18, 20};  // weight tensor index in the packed layout
+
+struct FragTab {
+  int64_t off[FT + 1];  // bf16 element offsets of each tensor's fragment image (off[FT] = total)
+  int64_t src[FT];      // fp32 offsets of the source tensors in the packed layout
+};
+
+inline FragTab frag_tab() {
+  const Layout& L = layout();
+  FragTab T{};
+  int64_t o = 0;
+  for (int t = 0; t < FT; ++t) {
+    T.off[t] = o;
+    T.src[t] = L.off[FSRC[t]];
+    o += (int64_t)FN[t] * FK[t];
+  }
+  T.off[FT] = o;
+  return T;
+}
+
+// fp32 packed [N][K] -> fragment-major bf16: chunk c (8 values) = tensor t, (nb, ks) = c/64 split, lane c%64
+__global__ void frag_pack_kernel(const float* __restrict__ w, nerf_bf16* __restrict__ wf, FragTab T) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c * 8 >= T.off[FT]) return;
+  int t = 0;
+#pragma unroll
+  for (int i = 1; i < FT; ++i)
+    if (c * 8 >= T.off[i]) t = i;
+  const int K = FK[t], KS = K / 16;
+  const int64_t lc = c - T.off[t] / 8;
+  const int lane = (int)(lc & 63);
+  const int64_t fr = lc >> 6;
+  const int nb = (int)(fr / KS), ks = (int)(fr - (int64_t)nb * KS);
+  const int row = 32 * nb + (lane & 31), k0 = 16 * ks + 8 * (lane >> 5);
+  const float4* s = reinterpret_cast<const float4*>(w + T.src[t] + (int64_t)row * K + k0);
+  const float4 a = s[0], b = s[1];
+  *reinterpret_cast<uint4*>(wf + c * 8) = make_uint4(nerf_pack_bf16x2(a.x, a.y), nerf_pack_bf16x2(a.z, a.w),
+                                                     nerf_pack_bf16x2(b.x, b.y), nerf_pack_bf16x2(b.z, b.w));
+}
+
+// xyz PE (models/encodings.py:437-444, L = 10, include_input) -> X3E cols 256..319 (bf16) and the colour-input
+// prefill CIN[m] = [0 x 15, d, dir PE (L = 4), 0 ...] (meta_vanilla.py:109-121; the fused kernel fills the
+// 15 geo columns).  Rows M..Mp-1 are zero.
+__global__ void pe_prefill_bf16_kernel(const float* __restrict__ xd, int64_t M, int64_t Mp, nerf_bf16* __restrict__ X3E,
+                                       nerf_bf16* __restrict__ CIN) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= Mp) return;
+  float v[64], c[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) v[i] = c[i] = 0.f;
+  if (m < M) {
+    const float x[3] = {xd[m * 6], xd[m * 6 + 1], xd[m * 6 + 2]};
+    const float d[3] = {xd[m * 6 + 3], xd[m * 6 + 4], xd[m * 6 + 5]};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      v[k] = x[k];
+      float band = 1.0f;
+#pragma unroll
+      for (int l = 0; l < 10; ++l) {
+        float s, cs;
+        sincosf(x[k] * band, &s, &cs);
+        v[3 + k * 20 + l] = cs;
+        v[3 + k * 20 + 10 + l] = s;
+        band *= 2.0f;
+      }
+      c[15 + k] = d[k];
+      band = 1.0f;
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        float s, cs;
+        sincosf(d[k] * band, &s, &cs);
+        c[18 + k * 8 + l] = cs;
+        c[18 + k * 8 + 4 + l] = s;
+        band *= 2.0f;
+      }
+    }
+  }
+  uint4* q = reinterpret_cast<uint4*>(X3E + m * 320 + 256);
+  uint4* r = reinterpret_cast<uint4*>(CIN + m * 64);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    q[i] = make_uint4(nerf_pack_bf16x2(v[8 * i], v[8 * i + 1]), nerf_pack_bf16x2(v[8 * i + 2], v[8 * i + 3]),
+                      nerf_pack_bf16x2(v[8 * i + 4], v[8 * i + 5]), nerf_pack_bf16x2(v[8 * i + 6], v[8 * i + 7]));
+    r[i] = make_uint4(nerf_pack_bf16x2(c[8 * i], c[8 * i + 1]), nerf_pack_bf16x2(c[8 * i + 2], c[8 * i + 3]),
+                      nerf_pack_bf16x2(c[8 * i + 4], c[8 * i + 5]), nerf_pack_bf16x2(c[8 * i + 6], c[8 * i + 7]));
+  }
+}
+
+struct FusedArgs {
+  const nerf_bf16* wf;   // fragment image (frag_pack_kernel)
+  const float* w;        // fp32 packed parameters (biases)
+  nerf_bf16* X3E;        // [Mp][320]: cols 256..319 = enc (read); training: cols 0..255 = trunk.3 output
+  nerf_bf16* Y;          // training: Y0, Y1, Y2, Y4, ..., Y7 back to back ([Mp][256] each; Y3 lives in X3E)
+  uint32_t* MB;          // training: MB0..MB7 back to back ([Mp][8] ReLU bitmask words each)
+  float* O16;            // [Mp][32] fp32: col 0 = sigma pre-activation (training)
+  nerf_bf16* CIN;        // [Mp][64] colour input (prefill read; training: written back complete)
+  nerf_bf16* C0;         // [Mp][128] (training)
+  uint32_t* MC0;         // [Mp][4] (training)
+  float* O3;             // [Mp][32] fp32 colour-out pre-activations, cols 0..3 (training)
+  float* out;            // [M][4] rgb_sigma
+  int64_t M, Mp;
+  int ntiles;
+};
+
+typedef nerf_bf16x8 Ring[4][2];
+typedef unsigned short nerf_u16x2 __attribute__((ext_vector_type(2)));
+
+// fragment (nb, ks) of a tensor with KS k-steps
+// Fragment loads go through a buffer resource built once per kernel (raw buffer, 1 MB image): the per-lane offset
+// is one VGPR (lane * 16) and each fragment's byte offset a wave-uniform soffset that the compiler rematerialises
+// as a scalar constant next to its load — plain pointers made it precompute ~250 64-bit addresses per tile and
+// spill them.
+typedef unsigned int nerf_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ nerf_bf16x8 frag_ld(__amdgpu_buffer_rsrc_t rs, int tensor_off, int nb, int ks, int KS,
+                                               int lane) {
+  // voffset: the lane and the (wave-dependent) fragment column; soffset: tensor + k-step, a compile-time constant
+#ifdef NERF_EXP_SAMEFRAG  // timing experiment only: every load hits the same 4 KB (L1-resident), results wrong
+  const nerf_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, (ks & 3) * 1024, 0);
+#else
+  const nerf_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + nb * KS * 1024, tensor_off + ks * 1024, 0);
+#endif
+  return __builtin_bit_cast(nerf_bf16x8, v);
+}
+
+__device__ __forceinline__ nerf_bf16x8 lds_frag(const nerf_bf16* p) { return *reinterpret_cast<const nerf_bf16x8*>(p); }
+
+// accumulator init with the bias of columns 8q + 4lh + e of the 32-column block starting at col0
+// biases of every layer, staged in LDS once per workgroup: trunk.i at 256 i, head 2048, colour0 2080, colour1 2208
+constexpr int BOFF[FT] = {0, 256, 512, 768, 1024, 1280, 1536, 1792, 2048, 2080, 2208};
+constexpr int BTOT = 2240;
+__device__ __forceinline__ void acc_bias(nerf_f32x16& acc, const float* bias, int col0, int lh) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 b = *reinterpret_cast<const float4*>(bias + col0 + 8 * q + 4 * lh);
+    acc[4 * q + 0] = b.x; acc[4 * q + 1] = b.y; acc[4 * q + 2] = b.z; acc[4 * q + 3] = b.w;
+  }
+}
+
+// One stage of the pipeline: KS k-steps over the fragments of `wcur` (NBW fragment columns per wave starting at
+// nb0), A operands from LDS; the ring already holds k-steps 0..3 of this stage.  While consuming k-step ks the
+// ring slot is refilled with k-step ks + 4 of this stage or, past its end, with k-step ks + 4 - KS of the NEXT
+// stage (KSN k-steps, NBWN columns from nbn0 of `wnext`).  TA 32-row A blocks: rows ar0 + 32 a + li; k-steps
+// below KS_H read H (pitch_h), the rest E (pitch_e) — trunk.4's cat([h, enc]).
+template <int KS, int NBW, int TA, int KS_H, int KSN, int NBWN>
+__device__ __forceinline__ void stage(nerf_f32x16 (&acc)[4][2], Ring& ring, __amdgpu_buffer_rsrc_t rs, int wcur,
+                                      int nb0, int wnext, int nbn0, const nerf_bf16* Hs, const nerf_bf16* Es,
+                                      int pitch_h, int pitch_e, int ar0, int li, int lh, int lane) {
+  static_assert(KS % 4 == 0 && KSN % 4 == 0, "ring slot alignment across stages");
+  auto afrag = [&](int ks, int a) {
+    const int r = ar0 + 32 * a + li;
+    return ks < KS_H ? lds_frag(Hs + r * pitch_h + 16 * ks + 8 * lh) : lds_frag(Es + r * pitch_e + 16 * (ks - KS_H) + 8 * lh);
+  };
+  nerf_bf16x8 af[TA];
+#pragma unroll
+  for (int a = 0; a < TA; ++a) af[a] = afrag(0, a);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    nerf_bf16x8 an[TA];  // A fragments of the next k-step, read under this k-step's MFMAs
+    if (ks + 1 < KS) {
+#pragma unroll
+      for (int a = 0; a < TA; ++a) an[a] = afrag(ks + 1, a);
+    }
+    nerf_bf16x8 bf[NBW];
+#pragma unroll
+    for (int b = 0; b < NBW; ++b) bf[b] = ring[ks & 3][b];
+    if (ks + 4 < KS) {
+#pragma unroll
+      for (int b = 0; b < NBW; ++b) ring[ks & 3][b] = frag_ld(rs, wcur, nb0 + b, ks + 4, KS, lane);
+    } else if (ks + 4 - KS < KSN) {
+#pragma unroll
+      for (int b = 0; b < NBWN; ++b) ring[ks & 3][b] = frag_ld(rs, wnext, nbn0 + b, ks + 4 - KS, KSN, lane);
+    }
+#pragma unroll
+    for (int a = 0; a < TA; ++a)
+#pragma unroll
+      for (int b = 0; b < NBW; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[b], af[a], acc[a][b], 0, 0, 0);
+    if (ks + 1 < KS) {
+#pragma unroll
+      for (int a = 0; a < TA; ++a) af[a] = an[a];
+    }
+  }
+}
+
+// ReLU + bf16 of accumulator tiles acc[a][b] (rows ar0 + 32 a + li, cols c0 + 32 b + (C^T register layout)) into an
+// LDS tile (pitch): two values per v_cvt_pk_bf16_f32, ReLU as v_pk_max_i16 on the bf16 bit patterns (rounding keeps
+// the sign, so round-then-clamp == clamp-then-round), 16-B stores after pairing the lane halves (gemm_bf16.hpp).
+typedef float nerf_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 nerf_bf16x2 __attribute__((ext_vector_type(2)));
+typedef short nerf_s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t relu_pk(float x, float y) {
+  const nerf_f32x2 f = {x, y};
+  const nerf_s16x2 z = {0, 0};
+  const nerf_s16x2 r = __builtin_elementwise_max(__builtin_bit_cast(nerf_s16x2, __builtin_convertvector(f, nerf_bf16x2)), z);
+  return __builtin_bit_cast(uint32_t, r);
+}
+
+template <int TA, int NB>
+__device__ __forceinline__ void relu_to_lds(const nerf_f32x16 (&acc)[4][2], nerf_bf16* dst, int pitch, int ar0, int c0,
+                                            int li, int lh) {
+#pragma unroll
+  for (int a = 0; a < TA; ++a) {
+    const int r = ar0 + 32 * a + li;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      uint2 pk[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        pk[q] = make_uint2(relu_pk(acc[a][b][4 * q], acc[a][b][4 * q + 1]), relu_pk(acc[a][b][4 * q + 2], acc[a][b][4 * q + 3]));
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        uint2 x = pk[2 * pr], y = pk[2 * pr + 1];
+        const auto r0 = __builtin_amdgcn_permlane32_swap(x.x, y.x, false, false);
+        const auto r1 = __builtin_amdgcn_permlane32_swap(x.y, y.y, false, false);
+        x.x = r0[0]; y.x = r0[1];
+        x.y = r1[0]; y.y = r1[1];
+        *reinterpret_cast<uint4*>(dst + r * pitch + c0 + 32 * b + 16 * pr + 8 * lh) = make_uint4(x.x, x.y, y.x, y.y);
+      }
+    }
+  }
+}
+
+// copy ROWS x COLS bf16 from an LDS tile (pitch) to global rows m0.. (ld), 16 B per lane, row-contiguous
+template <int ROWS, int COLS>
+__device__ __forceinline__ void lds_to_global(const nerf_bf16* src, int pitch, nerf_bf16* __restrict__ dst, int64_t ld,
+                                              int64_t m0, int tid) {
+  constexpr int CH = COLS / 8, TOT = ROWS * CH;
+  static_assert(TOT % 256 == 0, "whole passes");
+#pragma unroll
+  for (int i = 0; i < TOT / 256; ++i) {
+    const int f = tid + 256 * i;
+    const int r = f / CH, c = f - r * CH;
+    *reinterpret_cast<uint4*>(dst + (m0 + r) * ld + 8 * c) = *reinterpret_cast<const uint4*>(src + r * pitch + 8 * c);
+  }
+}
+
+// global rows m0.. (ld) -> LDS tile (pitch), ROWS x COLS bf16, via registers (loads issued first)
+template <int ROWS, int COLS>
+struct TileLoad {
+  static constexpr int CH = COLS / 8, PER = ROWS * CH / 256;
+  uint4 v[PER];
+  __device__ __forceinline__ void issue(const nerf_bf16* __restrict__ src, int64_t ld, int64_t m0, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int f = tid + 256 * i;
+      const int r = f / CH, c = f - r * CH;
+      v[i] = *reinterpret_cast<const uint4*>(src + (m0 + r) * ld + 8 * c);
+    }
+  }
+  __device__ __forceinline__ void store(nerf_bf16* dst, int pitch, int tid) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int f = tid + 256 * i;
+      const int r = f / CH, c = f - r * CH;
+      *reinterpret_cast<uint4*>(dst + r * pitch + 8 * c) = v[i];
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------------------------- the kernel
+// Workgroup = 8 waves: waves 0-3 compute (MFMA), waves 4-7 move bytes ("io" waves, one per SIMD beside a compute
+// wave).  The compute waves issue no global stores on the layer path: every vector-memory op counts in one
+// in-order vmcnt, so a burst of activation stores in front of the next layer's weight-fragment loads would make
+// each of those loads wait for the stores to drain.  The io waves copy every finished layer tile LDS -> HBM
+// (with its ReLU bitmask words) while the compute waves run the next layer, and stage the next tile's
+// encoding / colour-input prefill into E.  Persistent: one workgroup per CU walks tiles blockIdx.x + k * grid.
+// Both roles pass the same 20 barriers per tile (2 per trunk layer, 2 around the head, 1 after colour layer 0,
+// 1 at the end of the tile) plus one in the prologue.
+constexpr int NCW = 4;  // compute waves; io waves NCW..2*NCW-1, io wave j owns tile rows 32 j .. 32 j + 31
+
+// compile-time offsets: packed fp32 layout (mlp_common.hpp make_layout) and the fragment image
+constexpr int64_t lay_off(int t) {
+  int64_t o = 0;
+  for (int i = 0; i < t; ++i) {
+    int r = 256, c = 1;
+    if (i < 16) {
+      c = (i % 2 == 0) ? KPAD[i / 2] : 1;
+    } else {
+      const int R[6] = {32, 32, 128, 128, 32, 32}, C[6] = {256, 1, 64, 1, 128, 1};
+      r = R[i - 16];
+      c = C[i - 16];
+    }
+    o += (int64_t)r * c;
+    o = (o + 31) & ~int64_t(31);
+  }
+  return o;
+}
+constexpr int64_t frag_off(int t) {
+  int64_t o = 0;
+  for (int i = 0; i < t; ++i) o += (int64_t)FN[i] * FK[i];
+  return o;
+}
+
+__device__ __forceinline__ void bar() { __syncthreads(); }
+
+// io wave j: copy rows 32 j .. 32 j + 31 of an LDS tile (COLS bf16 wide, pitch) to global rows m0 + r (ld); with
+// MB, also the ReLU bitmask word of every 32 columns (bit = value > 0) to MB[(m0 + r) * (COLS / 32) + g]
+template <int COLS, bool MASK>
+__device__ __forceinline__ void io_copy(const nerf_bf16* src, int pitch, nerf_bf16* __restrict__ dst, int64_t ld,
+                                        int64_t m0, uint32_t* __restrict__ mb, int j, int lane) {
+  constexpr int CH = COLS / 8, RPI = 64 / CH, IT = 32 / RPI, B = IT < 8 ? IT : 8;
+  const int rl = lane / CH, c = lane - rl * CH;
+#pragma unroll
+  for (int i0 = 0; i0 < IT; i0 += B) {
+    uint4 v[B];
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const int r = 32 * j + (i0 + i) * RPI + rl;
+      v[i] = *reinterpret_cast<const uint4*>(src + r * pitch + 8 * c);
+    }
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const int64_t m = m0 + 32 * j + (i0 + i) * RPI + rl;
+      *reinterpret_cast<uint4*>(dst + m * ld + 8 * c) = v[i];
+      if (MASK) {
+        // post-ReLU bf16: bit = value != 0 (a -0 is 0x8000); 2 values per v_pk_min_u16, quads combined by DPP
+        const uint32_t u[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+        uint32_t bits = 0;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const uint32_t nz = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(
+              __builtin_bit_cast(nerf_u16x2, u[h] & 0x7fff7fffu), nerf_u16x2{1, 1}));
+          bits |= ((nz & 1u) | (nz >> 15)) << (2 * h);
+        }
+        bits <<= 8 * (c & 3);
+        bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xf, 0xf, true);  // quad_perm [1,0,3,2]
+        bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x4E, 0xf, 0xf, true);  // quad_perm [2,3,0,1]
+        if ((c & 3) == 0) mb[m * (COLS / 32) + (c >> 2)] = bits;
+      }
+    }
+  }
+}
+
+// io wave j: 32 rows x 64 bf16 (128 B) of a [rows][ld] global array -> registers -> LDS (four named registers, not
+// an array: held across barriers and loop iterations, an array is left in scratch / promoted to LDS)
+struct IoRows64 {
+  uint4 v0, v1, v2, v3;
+  __device__ __forceinline__ void load(const nerf_bf16* __restrict__ src, int64_t ld, int64_t m0, int j, int lane) {
+    const nerf_bf16* p = src + (m0 + 32 * j + (lane >> 3)) * ld + 8 * (lane & 7);
+    v0 = *reinterpret_cast<const uint4*>(p);
+    v1 = *reinterpret_cast<const uint4*>(p + 8 * ld);
+    v2 = *reinterpret_cast<const uint4*>(p + 16 * ld);
+    v3 = *reinterpret_cast<const uint4*>(p + 24 * ld);
+  }
+  __device__ __forceinline__ void store(nerf_bf16* dst, int pitch, int j, int lane) const {
+    nerf_bf16* p = dst + (32 * j + (lane >> 3)) * pitch + 8 * (lane & 7);
+    *reinterpret_cast<uint4*>(p) = v0;
+    *reinterpret_cast<uint4*>(p + 8 * pitch) = v1;
+    *reinterpret_cast<uint4*>(p + 16 * pitch) = v2;
+    *reinterpret_cast<uint4*>(p + 24 * pitch) = v3;
+  }
+};
+
+template <bool TRAIN>
+__device__ __forceinline__ void io_role(const FusedArgs& A, nerf_bf16* Hs, nerf_bf16* Es, int tile, int G, int j,
+                                        int lane) {
+  const int64_t Mp = A.Mp;
+  IoRows64 enc, cin;
+  enc.load(A.X3E + 256, 320, (int64_t)tile * BMF, j, lane);
+  enc.store(Es, EP, j, lane);
+  bar();  // prologue
+  for (int t = tile; t < A.ntiles; t += G) {
+    const int64_t m0 = (int64_t)t * BMF;
+    const bool next = t + G < A.ntiles;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bar();  // A(i): the compute waves finished layer i's k-loop (E free after trunk.4)
+      if (i == 4) {
+        cin.store(Es, EP, j, lane);
+        if (next) enc.load(A.X3E + 256, 320, m0 + (int64_t)G * BMF, j, lane);
+      }
+      bar();  // B(i): layer i's output tile is in H
+      if (TRAIN) {
+        nerf_bf16* Y = (i == 3) ? A.X3E : A.Y + (int64_t)(i < 3 ? i : i - 1) * Mp * 256;
+        io_copy<256, true>(Hs, HP, Y, i == 3 ? 320 : 256, m0, A.MB + (int64_t)i * Mp * 8, j, lane);
+      }
+      if (i == 0) cin.load(A.CIN, 64, m0, j, lane);
+    }
+    bar();  // H1
+    bar();  // H2: colour input complete in E
+    if (TRAIN) io_copy<64, false>(Es, EP, A.CIN, 64, m0, nullptr, j, lane);
+    bar();  // C: colour layer 0 output in H; E free
+    if (next) enc.store(Es, EP, j, lane);
+    bar();  // D
+    if (TRAIN) io_copy<128, true>(Hs, CP, A.C0, 128, m0, A.MC0, j, lane);
+  }
+}
+
+template <bool TRAIN>
+__device__ __forceinline__ void compute_role(const FusedArgs& A, nerf_bf16* Hs, nerf_bf16* Es, float* Ssig,
+                                             const float* Bs, int tile, int G, int w, int li, int lh, int lane) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)A.wf, 0, (int)(frag_off(FT) * 2), 0x00020000);
+#define F(t) ((int)(frag_off(t) * 2))
+#define BI(t) (Bs + BOFF[t])
+  Ring ring;
+  nerf_f32x16 acc[4][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) ring[s][b] = frag_ld(rs, F(0), 2 * w + b, s, 4, lane);
+  bar();  // prologue: the first tile's encoding is in E, the biases in Bs
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc_bias(acc[a][b], BI(0), 64 * w + 32 * b, lh);
+
+  auto trunk_epi = [&](const float* next_bias) {
+    bar();  // A(i): every wave done reading H / E of this layer
+    relu_to_lds<4, 2>(acc, Hs, HP, 0, 64 * w, li, lh);
+    if (next_bias) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc_bias(acc[a][b], next_bias, 64 * w + 32 * b, lh);
+    }
+    bar();  // B(i)
+  };
+
+  for (int t = tile; t < A.ntiles; t += G) {
+    const int64_t m0 = (int64_t)t * BMF;
+    // trunk: (KS, NBW, TA, KS_H, KSN, NBWN)
+    stage<4, 2, 4, 0, 16, 2>(acc, ring, rs, F(0), 2 * w, F(1), 2 * w, Hs, Es, HP, EP, 0, li, lh, lane);
+    trunk_epi(BI(1));
+    stage<16, 2, 4, 16, 16, 2>(acc, ring, rs, F(1), 2 * w, F(2), 2 * w, Hs, Es, HP, EP, 0, li, lh, lane);
+    trunk_epi(BI(2));
+    stage<16, 2, 4, 16, 16, 2>(acc, ring, rs, F(2), 2 * w, F(3), 2 * w, Hs, Es, HP, EP, 0, li, lh, lane);
+    trunk_epi(BI(3));
+    stage<16, 2, 4, 16, 20, 2>(acc, ring, rs, F(3), 2 * w, F(4), 2 * w, Hs, Es, HP, EP, 0, li, lh, lane);
+    trunk_epi(BI(4));
+    stage<20, 2, 4, 16, 16, 2>(acc, ring, rs, F(4), 2 * w, F(5), 2 * w, Hs, Es, HP, EP, 0, li, lh, lane);
+    trunk_epi(BI(5));
+    stage<16, 2, 4, 16, 16, 2>(acc, ring, rs, F(5), 2 * w, F(6), 2 * w, Hs, Es, HP, EP, 0, li, lh, lane);
+    trunk_epi(BI(6));
+    stage<16, 2, 4, 16, 16, 2>(acc, ring, rs, F(6), 2 * w, F(7), 2 * w, Hs, Es, HP, EP, 0, li, lh, lane);
+    trunk_epi(BI(7));
+    // the head's fragments are one 32-column block shared by every wave (nb 0)
+    stage<16, 2, 4, 16, 16, 1>(acc, ring, rs, F(7), 2 * w, F(8), 0, Hs, Es, HP, EP, 0, li, lh, lane);
+    trunk_epi(nullptr);
+
+    // ---- head: O16 = h7 W_head^T + b (sigma | 15 geo | 0), wave w -> rows 32w..32w+31
+    acc_bias(acc[0][0], BI(8), 0, lh);
+    stage<16, 1, 1, 16, 4, 1>(acc, ring, rs, F(8), 0, F(9), w, Hs, Es, HP, EP, 32 * w, li, lh, lane);
+    bar();  // H1: every wave done reading H (colour layer 0 overwrites it)
+    const int r = 32 * w + li;
+    if (lh == 0) Ssig[r] = acc[0][0][0];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)  // geo (cols 1..15) -> colour input cols 0..14
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = 8 * q + 4 * lh + e;
+        if (c >= 1) Es[r * EP + c - 1] = (nerf_bf16)acc[0][0][4 * q + e];
+      }
+    bar();  // H2: colour input complete
+
+    // ---- colour layer 0: C0 = ReLU(CIN W_c0^T + b), wave w -> cols 32w..32w+31 of all rows (tile in H, pitch CP)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) acc_bias(acc[a][0], BI(9), 32 * w, lh);
+    stage<4, 1, 4, 0, 8, 1>(acc, ring, rs, F(9), w, F(10), 0, Hs, Es, HP, EP, 0, li, lh, lane);
+    relu_to_lds<4, 1>(acc, Hs, CP, 0, 32 * w, li, lh);
+    bar();  // C
+
+    // ---- colour out: O3 = C0 W_c1^T + b, wave w -> rows 32w..32w+31; next tile's trunk.0 fragments prefetched
+    acc_bias(acc[0][0], BI(10), 0, lh);
+    stage<8, 1, 1, 8, 4, 2>(acc, ring, rs, F(10), 0, F(0), 2 * w, Hs, Hs, CP, CP, 32 * w, li, lh, lane);
+    const int64_t m = m0 + r;
+    if (lh == 0) {
+      const float sraw = Ssig[r];
+      if (TRAIN) {
+        // the backward reads sigma_raw (O16 col 0) and the colour-out pre-activations (O3 cols 0..2)
+        A.O16[m * 32] = sraw;
+        *reinterpret_cast<float4*>(A.O3 + m * 32) = make_float4(acc[0][0][0], acc[0][0][1], acc[0][0][2], acc[0][0][3]);
+      }
+      if (m < A.M) {
+        const float sg = expf(fminf(fmaxf(sraw, -EXP_MAX), EXP_MAX));
+        reinterpret_cast<float4*>(A.out)[m] =
+            make_float4(sigmoidf_(acc[0][0][0]), sigmoidf_(acc[0][0][1]), sigmoidf_(acc[0][0][2]), sg);
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc_bias(acc[a][b], BI(0), 64 * w + 32 * b, lh);
+    bar();  // D: the next tile's encoding is in E
+  }
+#undef F
+#undef BI
+}
+
+template <bool TRAIN>
+__global__ __launch_bounds__(512, 1) void mlp_fwd_fused_bf16_kernel(FusedArgs A) {
+  __shared__ __attribute__((aligned(16))) nerf_bf16 Hs[BMF * HP];
+  __shared__ __attribute__((aligned(16))) nerf_bf16 Es[BMF * EP];
+  __shared__ float Ssig[BMF];
+  __shared__ __attribute__((aligned(16))) float Bs[BTOT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tile = blockIdx.x;
+  if (tile >= A.ntiles) return;
+  for (int i = tid; i < BTOT; i += 512) {  // biases -> LDS (read by the compute waves after the prologue barrier)
+    int t = 0;
+#pragma unroll
+    for (int k = 1; k < FT; ++k)
+      if (i >= BOFF[k]) t = k;
+    Bs[i] = A.w[lay_off(FSRC[t] + 1) + (i - BOFF[t])];
+  }
+  if (w >= NCW)
+    io_role<TRAIN>(A, Hs, Es, tile, gridDim.x, w - NCW, lane);
+  else
+    compute_role<TRAIN>(A, Hs, Es, Ssig, Bs, tile, gridDim.x, w, lane & 31, lane >> 5, lane);
+}
+
+}  // namespace nerf_fused

@@ -101,3 +101,33 @@ def test_bf16_engine_tracks_fp32_loss(K):
     assert torch.isfinite(a).all()
     assert a[-10:].mean() < a[:5].mean()  # it learns
     assert (a[-10:].mean() - b[-10:].mean()).abs() <= 0.15 * b[-10:].mean()
+
+
+def test_fused_forward_matches_layered(K, wpk, monkeypatch):
+    """The single-launch fused bf16 forward (mlp_bf16_fused.hpp) against the layer-by-layer bf16 GEMM path
+    (NERF_BF16_FUSED=0): the same bf16 rounding points and k order, only the bias enters the fp32 accumulator
+    first instead of last — outputs agree to bf16 rounding flips, the saved activations feed the same backward."""
+    M = 5000  # two row tiles short of a multiple of 256: pad rows in the last tile
+    x = _xd(M, 9).to(DEV)
+    g = torch.Generator().manual_seed(13)
+    gup = (torch.randn(M, 4, generator=g) * 1e-3).to(DEV)
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("NERF_BF16_FUSED", mode)
+        ws = K.mlp_workspace(M, True, DEV, "bf16")
+        out = K.mlp_fwd(wpk, x, ws, True, precision="bf16")
+        d_w = K.mlp_bwd(wpk, M, gup, ws, precision="bf16")
+        inf = K.mlp_fwd(wpk, x, K.mlp_workspace(M, False, DEV, "bf16"), False, precision="bf16")
+        assert torch.equal(out, inf), f"mode {mode}: inference != training forward"
+        res[mode] = (out.cpu(), d_w.cpu())
+    (o0, g0), (o1, g1) = res["0"], res["1"]
+    assert (o1[:, :3] - o0[:, :3]).abs().max().item() <= 5e-3
+    assert ((o1[:, 3] - o0[:, 3]).abs() <= 2e-2 * o0[:, 3].abs() + 1e-6).all()
+    from nerf_amd.vanilla import PackedLayout
+    a, b = PackedLayout.get().unpack(g1), PackedLayout.get().unpack(g0)
+    for name in b:
+        ref, got = b[name].double(), a[name].double()
+        if ref.norm() == 0:
+            continue
+        rel = ((got - ref).norm() / ref.norm()).item()
+        assert rel <= 2e-2, f"{name}: fused vs layered gradient rel {rel:.3e}"
