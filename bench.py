@@ -190,6 +190,21 @@ def roofline(tm, bf16, overlap):
         "wgrad": mean([st[i] for st in tm["wgrad"] for i in K256]),
         "dgrad": mean([st[i - 1] for st in tm["dgrad"] for i in K256]),
     }
+    fused = None
+    if bf16 and cls["fwd"] < 0.02 * cls["dgrad"]:
+        # the bf16 forward is ONE fused launch (mlp_bf16_fused.hpp): events 0 -> 1 bracket it, the per-layer
+        # events are empty.  Algorithmic work per sample row: 2 x 500,864 MAC of MFMA; HBM: reads the encoding +
+        # colour-input prefill (256 B), writes the saved activations for the backward (7 trunk outputs + the
+        # trunk.3 output 4,096 B, ReLU masks 256 B, colour input 128 B, colour layer 0 256 B + mask 16 B, sigma /
+        # colour-out pre-activations 20 B) and rgb_sigma (16 B) = 5,044 B.
+        fms = mean([st[0] for st in tm["fwd"]])
+        fby = 5044.0 * M
+        fused = {"kernel": "mlp_fwd_fused_bf16 (whole MLP forward, one persistent launch)", "mean_launch_ms": round(fms, 4),
+                 "mfma_tflops": round(2.0 * MAC_PER_EVAL * M / (fms * 1e-3) / 1e12, 1),
+                 "mfma_frac_bf16": round(2.0 * MAC_PER_EVAL * M / (fms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4),
+                 "hbm_gbs": round(fby / (fms * 1e-3) / 1e9, 1), "hbm_frac": round(fby / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                 "bytes_per_launch": fby}
+        del cls["fwd"]
     eligible = [k for k in cls if not (overlap and k == "fwd")]
     dom = max(eligible, key=lambda k: cls[k])
     names = {"fwd": "gemm_nt fwd (bias+ReLU)", "wgrad": "gemm_wgrad (split-M, 128x128 tiles)",
@@ -218,6 +233,8 @@ def roofline(tm, bf16, overlap):
             traffic = json.load(open(tpath)).get(dom)
         except Exception:
             traffic = None
+    if fused:
+        roof["fused_fwd"] = fused
     roof.update({"traffic": traffic, "class": dom, "mean_launch_ms": round(ms, 4),
                  "classes_ms": {k: round(v, 4) for k, v in cls.items()},
                  "classes_frac": {k: round(flop256 / (v * 1e-3) / 1e12 / (BF16_MFMA_PEAK_TFLOPS if bf16 else

@@ -69,7 +69,13 @@ WSB carve_b(void* base, int64_t M, int training) {
     w.dC0 = (nerf_bf16*)take(Mp * 128 * 2);
     w.dCIN = (float*)take(Mp * 32 * 4);
     w.WTb = (nerf_bf16*)take(WTB_ELEMS * 2);
-    w.S = n_splits(Mp);
+#ifndef NERF_BF16_SPLIT_ROWS
+#define NERF_BF16_SPLIT_ROWS 2048
+#endif
+    {
+      int64_t sp = Mp / NERF_BF16_SPLIT_ROWS;
+      w.S = (int)(sp < 1 ? 1 : (sp > 256 ? 256 : sp));
+    }
     w.rps = round_up(nerf_cdiv(Mp, w.S), 64);  // whole slabs for every wgrad MR
     w.partial = (float*)take((int64_t)w.S * L.total * 4);
   }

@@ -136,23 +136,19 @@ struct FusedArgs {
   int ntiles;
 };
 
+__device__ __forceinline__ void bar() { __syncthreads(); }
+
 typedef nerf_bf16x8 Ring[4][2];
 typedef unsigned short nerf_u16x2 __attribute__((ext_vector_type(2)));
 
-// fragment (nb, ks) of a tensor with KS k-steps
-// Fragment loads go through a buffer resource built once per kernel (raw buffer, 1 MB image): the per-lane offset
-// is one VGPR (lane * 16) and each fragment's byte offset a wave-uniform soffset that the compiler rematerialises
-// as a scalar constant next to its load — plain pointers made it precompute ~250 64-bit addresses per tile and
-// spill them.
+// Fragment (nb, kk) of a tensor with KS k-steps.  Loads go through a buffer resource built once per kernel (raw
+// buffer over the 1 MB image): voffset = lane * 16 + the wave's fragment column (VGPR), soffset = tensor + k-step
+// (wave-uniform SGPR, a few scalar ops next to the load) — plain pointers made the compiler precompute ~250 64-bit
+// addresses per tile and spill them.
 typedef unsigned int nerf_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ nerf_bf16x8 frag_ld(__amdgpu_buffer_rsrc_t rs, int tensor_off, int nb, int ks, int KS,
+__device__ __forceinline__ nerf_bf16x8 frag_ld(__amdgpu_buffer_rsrc_t rs, int tensor_off, int nb, int kk, int KS,
                                                int lane) {
-  // voffset: the lane and the (wave-dependent) fragment column; soffset: tensor + k-step, a compile-time constant
-#ifdef NERF_EXP_SAMEFRAG  // timing experiment only: every load hits the same 4 KB (L1-resident), results wrong
-  const nerf_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, (ks & 3) * 1024, 0);
-#else
-  const nerf_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + nb * KS * 1024, tensor_off + ks * 1024, 0);
-#endif
+  const nerf_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + nb * KS * 1024, tensor_off + kk * 1024, 0);
   return __builtin_bit_cast(nerf_bf16x8, v);
 }
 
@@ -170,46 +166,86 @@ __device__ __forceinline__ void acc_bias(nerf_f32x16& acc, const float* bias, in
   }
 }
 
-// One stage of the pipeline: KS k-steps over the fragments of `wcur` (NBW fragment columns per wave starting at
-// nb0), A operands from LDS; the ring already holds k-steps 0..3 of this stage.  While consuming k-step ks the
-// ring slot is refilled with k-step ks + 4 of this stage or, past its end, with k-step ks + 4 - KS of the NEXT
-// stage (KSN k-steps, NBWN columns from nbn0 of `wnext`).  TA 32-row A blocks: rows ar0 + 32 a + li; k-steps
-// below KS_H read H (pitch_h), the rest E (pitch_e) — trunk.4's cat([h, enc]).
-template <int KS, int NBW, int TA, int KS_H, int KSN, int NBWN>
+// k-step order of a stage (position p -> k-step kk), so that a wave starts on the columns IT wrote in the previous
+// epilogue and the barrier that publishes everyone else's columns overlaps those MFMAs:
+//   K_ID    identity (inputs already published: trunk.0 / colour 0 read E)
+//   K_ROT16 (p + 4 w) & 15        a 256-wide H input: wave w wrote columns 64w..64w+63 = k-steps 4w..4w+3
+//   K_L4    trunk.4 (K = 320): the own 4 h k-steps, the 4 enc k-steps (E, k-steps 16..19), the other 12 h k-steps
+//   K_ROT8  (p + 2 w) & 7         colour out over C0: wave w wrote columns 32w..32w+31 = k-steps 2w, 2w+1
+#ifndef NERF_FUSED_ROT
+#define NERF_FUSED_ROT 0
+#endif
+enum { K_ID = 0, K_ROT16 = 1, K_L4 = 2, K_ROT8 = 3 };
+template <int KIND>
+__device__ __forceinline__ int kpos(int p, int w) {
+  if (!NERF_FUSED_ROT) return p;
+  if (KIND == K_ROT16) return (p + 4 * w) & 15;
+  if (KIND == K_L4) return p < 4 ? 4 * w + p : (p < 8 ? 12 + p : ((4 * w + p - 4) & 15));
+  if (KIND == K_ROT8) return (p + 2 * w) & 7;
+  return p;
+}
+// A operand source of position p: 0 = H (k-step kk of the Hs tile), 1 = E (k-step kk - EOFF of the Es tile)
+template <int KIND, int ESRC>
+__device__ __forceinline__ constexpr bool from_e(int p) {
+  return ESRC == 1 || (KIND == K_L4 && (NERF_FUSED_ROT ? (p >= 4 && p < 8) : p >= 16));
+}
+// position of the in-stage barrier: after the wave's own k-steps with rotation, before position 0 without
+template <int BARROT>
+__device__ __forceinline__ constexpr int barpos() { return BARROT < 0 ? -1 : (NERF_FUSED_ROT ? BARROT : 0); }
+
+// One stage of the pipeline: KS positions over the fragments of tensor `wcur` (NBW fragment columns per wave from nb0)
+// in KIND order; A operands from LDS (TA 32-row blocks, rows ar0 + 32 a + li).  The ring holds positions 0..3 on
+// entry; consuming position p refills its slot with position p + 4 of this stage or, past the end, with position
+// p + 4 - KS of the NEXT stage (KSN positions in KINDN order, NBWN columns from nbn0 of tensor wnext).  BAR >= 0:
+// the workgroup barrier that publishes the other waves' epilogue sits between positions BAR - 1 and BAR.
+template <int KS, int NBW, int TA, int KIND, int ESRC, int BARROT, int KSN, int NBWN, int KINDN>
 __device__ __forceinline__ void stage(nerf_f32x16 (&acc)[4][2], Ring& ring, __amdgpu_buffer_rsrc_t rs, int wcur,
                                       int nb0, int wnext, int nbn0, const nerf_bf16* Hs, const nerf_bf16* Es,
-                                      int pitch_h, int pitch_e, int ar0, int li, int lh, int lane) {
+                                      int pitch_h, int pitch_e, int ar0, int li, int lh, int lane, int w) {
   static_assert(KS % 4 == 0 && KSN % 4 == 0, "ring slot alignment across stages");
-  auto afrag = [&](int ks, int a) {
+  constexpr int EOFF = (KIND == K_L4) ? 16 : 0;
+  constexpr int BAR = barpos<BARROT>();
+  auto afrag = [&](int p, int a) {
     const int r = ar0 + 32 * a + li;
-    return ks < KS_H ? lds_frag(Hs + r * pitch_h + 16 * ks + 8 * lh) : lds_frag(Es + r * pitch_e + 16 * (ks - KS_H) + 8 * lh);
+    const int kk = kpos<KIND>(p, w);
+    return from_e<KIND, ESRC>(p) ? lds_frag(Es + r * pitch_e + 16 * (kk - EOFF) + 8 * lh)
+                                 : lds_frag(Hs + r * pitch_h + 16 * kk + 8 * lh);
   };
   nerf_bf16x8 af[TA];
+  if (BAR != 0) {
 #pragma unroll
-  for (int a = 0; a < TA; ++a) af[a] = afrag(0, a);
+    for (int a = 0; a < TA; ++a) af[a] = afrag(0, a);
+  }
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    nerf_bf16x8 an[TA];  // A fragments of the next k-step, read under this k-step's MFMAs
-    if (ks + 1 < KS) {
+  for (int p = 0; p < KS; ++p) {
+    if (p == BAR) {  // everyone's previous epilogue is in LDS past this point
+      bar();
 #pragma unroll
-      for (int a = 0; a < TA; ++a) an[a] = afrag(ks + 1, a);
+      for (int a = 0; a < TA; ++a) af[a] = afrag(p, a);
+    }
+    nerf_bf16x8 an[TA];  // A fragments of the next position, read under this position's MFMAs
+    if (p + 1 < KS && p + 1 != BAR) {
+#pragma unroll
+      for (int a = 0; a < TA; ++a) an[a] = afrag(p + 1, a);
     }
     nerf_bf16x8 bf[NBW];
 #pragma unroll
-    for (int b = 0; b < NBW; ++b) bf[b] = ring[ks & 3][b];
-    if (ks + 4 < KS) {
+    for (int b = 0; b < NBW; ++b) bf[b] = ring[p & 3][b];
+    if (p + 4 < KS) {
+      const int kk = kpos<KIND>(p + 4, w);
 #pragma unroll
-      for (int b = 0; b < NBW; ++b) ring[ks & 3][b] = frag_ld(rs, wcur, nb0 + b, ks + 4, KS, lane);
-    } else if (ks + 4 - KS < KSN) {
+      for (int b = 0; b < NBW; ++b) ring[p & 3][b] = frag_ld(rs, wcur, nb0 + b, kk, KS, lane);
+    } else if (p + 4 - KS < KSN) {
+      const int kk = kpos<KINDN>(p + 4 - KS, w);
 #pragma unroll
-      for (int b = 0; b < NBWN; ++b) ring[ks & 3][b] = frag_ld(rs, wnext, nbn0 + b, ks + 4 - KS, KSN, lane);
+      for (int b = 0; b < NBWN; ++b) ring[p & 3][b] = frag_ld(rs, wnext, nbn0 + b, kk, KSN, lane);
     }
 #pragma unroll
     for (int a = 0; a < TA; ++a)
 #pragma unroll
       for (int b = 0; b < NBW; ++b)
         acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[b], af[a], acc[a][b], 0, 0, 0);
-    if (ks + 1 < KS) {
+    if (p + 1 < KS && p + 1 != BAR) {
 #pragma unroll
       for (int a = 0; a < TA; ++a) af[a] = an[a];
     }
@@ -325,13 +361,16 @@ constexpr int64_t frag_off(int t) {
   return o;
 }
 
-__device__ __forceinline__ void bar() { __syncthreads(); }
-
 // io wave j: copy rows 32 j .. 32 j + 31 of an LDS tile (COLS bf16 wide, pitch) to global rows m0 + r (ld); with
 // MB, also the ReLU bitmask word of every 32 columns (bit = value > 0) to MB[(m0 + r) * (COLS / 32) + g]
-template <int COLS, bool MASK>
+template <int COLS, bool MASK_>
 __device__ __forceinline__ void io_copy(const nerf_bf16* src, int pitch, nerf_bf16* __restrict__ dst, int64_t ld,
                                         int64_t m0, uint32_t* __restrict__ mb, int j, int lane) {
+#ifdef NERF_EXP_NOMASK
+  constexpr bool MASK = false;
+#else
+  constexpr bool MASK = MASK_;
+#endif
   constexpr int CH = COLS / 8, RPI = 64 / CH, IT = 32 / RPI, B = IT < 8 ? IT : 8;
   const int rl = lane / CH, c = lane - rl * CH;
 #pragma unroll
@@ -345,7 +384,11 @@ __device__ __forceinline__ void io_copy(const nerf_bf16* src, int pitch, nerf_bf
 #pragma unroll
     for (int i = 0; i < B; ++i) {
       const int64_t m = m0 + 32 * j + (i0 + i) * RPI + rl;
+#ifdef NERF_EXP_NOSTORE
+      if (v[i].x == 0x12345678u && v[i].y == 0x9abcdef0u) *reinterpret_cast<uint4*>(dst + m * ld + 8 * c) = v[i];
+#else
       *reinterpret_cast<uint4*>(dst + m * ld + 8 * c) = v[i];
+#endif
       if (MASK) {
         // post-ReLU bf16: bit = value != 0 (a -0 is 0x8000); 2 values per v_pk_min_u16, quads combined by DPP
         const uint32_t u[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
@@ -385,6 +428,10 @@ struct IoRows64 {
   }
 };
 
+// Barriers per tile (compute and io waves pass the same sequence): B_k (k = 0..7, "every trunk epilogue k is in
+// LDS"; B_k sits inside the stage after k), H2 (colour input complete), C (colour layer 0 output complete, inside
+// colour out), D (end of tile: the next tile's encoding is in E).  Trunk epilogue k writes H[k & 1]; the io waves
+// copy it to HBM after B_k and must be done before it is overwritten (epilogue k + 2, after B_{k+1}).
 template <bool TRAIN>
 __device__ __forceinline__ void io_role(const FusedArgs& A, nerf_bf16* Hs, nerf_bf16* Es, int tile, int G, int j,
                                         int lane) {
@@ -397,26 +444,24 @@ __device__ __forceinline__ void io_role(const FusedArgs& A, nerf_bf16* Hs, nerf_
     const int64_t m0 = (int64_t)t * BMF;
     const bool next = t + G < A.ntiles;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      bar();  // A(i): the compute waves finished layer i's k-loop (E free after trunk.4)
-      if (i == 4) {
+    for (int k = 0; k < 8; ++k) {
+      bar();  // B_k
+      if (k == 4) {  // trunk.4 (the last reader of the encoding) is done: colour-input prefill -> E
         cin.store(Es, EP, j, lane);
         if (next) enc.load(A.X3E + 256, 320, m0 + (int64_t)G * BMF, j, lane);
       }
-      bar();  // B(i): layer i's output tile is in H
       if (TRAIN) {
-        nerf_bf16* Y = (i == 3) ? A.X3E : A.Y + (int64_t)(i < 3 ? i : i - 1) * Mp * 256;
-        io_copy<256, true>(Hs, HP, Y, i == 3 ? 320 : 256, m0, A.MB + (int64_t)i * Mp * 8, j, lane);
+        nerf_bf16* Y = (k == 3) ? A.X3E : A.Y + (int64_t)(k < 3 ? k : k - 1) * Mp * 256;
+        io_copy<256, true>(Hs + (k & 1) * BMF * HP, HP, Y, k == 3 ? 320 : 256, m0, A.MB + (int64_t)k * Mp * 8, j, lane);
       }
-      if (i == 0) cin.load(A.CIN, 64, m0, j, lane);
+      if (k == 0) cin.load(A.CIN, 64, m0, j, lane);
     }
-    bar();  // H1
     bar();  // H2: colour input complete in E
     if (TRAIN) io_copy<64, false>(Es, EP, A.CIN, 64, m0, nullptr, j, lane);
-    bar();  // C: colour layer 0 output in H; E free
+    bar();  // C: colour layer 0 output in H[1]; colour 0 done reading E
     if (next) enc.store(Es, EP, j, lane);
+    if (TRAIN) io_copy<128, true>(Hs + BMF * HP, CP, A.C0, 128, m0, A.MC0, j, lane);
     bar();  // D
-    if (TRAIN) io_copy<128, true>(Hs, CP, A.C0, 128, m0, A.MC0, j, lane);
   }
 }
 
@@ -427,6 +472,8 @@ __device__ __forceinline__ void compute_role(const FusedArgs& A, nerf_bf16* Hs, 
       __builtin_amdgcn_make_buffer_rsrc((void*)A.wf, 0, (int)(frag_off(FT) * 2), 0x00020000);
 #define F(t) ((int)(frag_off(t) * 2))
 #define BI(t) (Bs + BOFF[t])
+  nerf_bf16* H0 = Hs;
+  nerf_bf16* H1 = Hs + BMF * HP;
   Ring ring;
   nerf_f32x16 acc[4][2];
 #pragma unroll
@@ -434,69 +481,66 @@ __device__ __forceinline__ void compute_role(const FusedArgs& A, nerf_bf16* Hs, 
 #pragma unroll
     for (int b = 0; b < 2; ++b) ring[s][b] = frag_ld(rs, F(0), 2 * w + b, s, 4, lane);
   bar();  // prologue: the first tile's encoding is in E, the biases in Bs
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc_bias(acc[a][b], BI(0), 64 * w + 32 * b, lh);
 
-  auto trunk_epi = [&](const float* next_bias) {
-    bar();  // A(i): every wave done reading H / E of this layer
-    relu_to_lds<4, 2>(acc, Hs, HP, 0, 64 * w, li, lh);
-    if (next_bias) {
+  auto bias_trunk = [&](int t) {
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc_bias(acc[a][b], next_bias, 64 * w + 32 * b, lh);
-    }
-    bar();  // B(i)
+      for (int b = 0; b < 2; ++b) acc_bias(acc[a][b], BI(t), 64 * w + 32 * b, lh);
   };
-
   for (int t = tile; t < A.ntiles; t += G) {
     const int64_t m0 = (int64_t)t * BMF;
-    // trunk: (KS, NBW, TA, KS_H, KSN, NBWN)
-    stage<4, 2, 4, 0, 16, 2>(acc, ring, rs, F(0), 2 * w, F(1), 2 * w, Hs, Es, HP, EP, 0, li, lh, lane);
-    trunk_epi(BI(1));
-    stage<16, 2, 4, 16, 16, 2>(acc, ring, rs, F(1), 2 * w, F(2), 2 * w, Hs, Es, HP, EP, 0, li, lh, lane);
-    trunk_epi(BI(2));
-    stage<16, 2, 4, 16, 16, 2>(acc, ring, rs, F(2), 2 * w, F(3), 2 * w, Hs, Es, HP, EP, 0, li, lh, lane);
-    trunk_epi(BI(3));
-    stage<16, 2, 4, 16, 20, 2>(acc, ring, rs, F(3), 2 * w, F(4), 2 * w, Hs, Es, HP, EP, 0, li, lh, lane);
-    trunk_epi(BI(4));
-    stage<20, 2, 4, 16, 16, 2>(acc, ring, rs, F(4), 2 * w, F(5), 2 * w, Hs, Es, HP, EP, 0, li, lh, lane);
-    trunk_epi(BI(5));
-    stage<16, 2, 4, 16, 16, 2>(acc, ring, rs, F(5), 2 * w, F(6), 2 * w, Hs, Es, HP, EP, 0, li, lh, lane);
-    trunk_epi(BI(6));
-    stage<16, 2, 4, 16, 16, 2>(acc, ring, rs, F(6), 2 * w, F(7), 2 * w, Hs, Es, HP, EP, 0, li, lh, lane);
-    trunk_epi(BI(7));
+    // trunk: <KS, NBW, TA, KIND, ESRC, BAR, KSN, NBWN, KINDN>; epilogue k -> H[k & 1]
+    bias_trunk(0);
+    stage<4, 2, 4, K_ID, 1, -1, 16, 2, K_ROT16>(acc, ring, rs, F(0), 2 * w, F(1), 2 * w, H1, Es, HP, EP, 0, li, lh, lane, w);
+    relu_to_lds<4, 2>(acc, H0, HP, 0, 64 * w, li, lh);
+    bias_trunk(1);
+    stage<16, 2, 4, K_ROT16, 0, 4, 16, 2, K_ROT16>(acc, ring, rs, F(1), 2 * w, F(2), 2 * w, H0, Es, HP, EP, 0, li, lh, lane, w);
+    relu_to_lds<4, 2>(acc, H1, HP, 0, 64 * w, li, lh);
+    bias_trunk(2);
+    stage<16, 2, 4, K_ROT16, 0, 4, 16, 2, K_ROT16>(acc, ring, rs, F(2), 2 * w, F(3), 2 * w, H1, Es, HP, EP, 0, li, lh, lane, w);
+    relu_to_lds<4, 2>(acc, H0, HP, 0, 64 * w, li, lh);
+    bias_trunk(3);
+    stage<16, 2, 4, K_ROT16, 0, 4, 20, 2, K_L4>(acc, ring, rs, F(3), 2 * w, F(4), 2 * w, H0, Es, HP, EP, 0, li, lh, lane, w);
+    relu_to_lds<4, 2>(acc, H1, HP, 0, 64 * w, li, lh);
+    bias_trunk(4);
+    stage<20, 2, 4, K_L4, 2, 8, 16, 2, K_ROT16>(acc, ring, rs, F(4), 2 * w, F(5), 2 * w, H1, Es, HP, EP, 0, li, lh, lane, w);
+    relu_to_lds<4, 2>(acc, H0, HP, 0, 64 * w, li, lh);
+    bias_trunk(5);
+    stage<16, 2, 4, K_ROT16, 0, 4, 16, 2, K_ROT16>(acc, ring, rs, F(5), 2 * w, F(6), 2 * w, H0, Es, HP, EP, 0, li, lh, lane, w);
+    relu_to_lds<4, 2>(acc, H1, HP, 0, 64 * w, li, lh);
+    bias_trunk(6);
+    stage<16, 2, 4, K_ROT16, 0, 4, 16, 2, K_ROT16>(acc, ring, rs, F(6), 2 * w, F(7), 2 * w, H1, Es, HP, EP, 0, li, lh, lane, w);
+    relu_to_lds<4, 2>(acc, H0, HP, 0, 64 * w, li, lh);
+    bias_trunk(7);
     // the head's fragments are one 32-column block shared by every wave (nb 0)
-    stage<16, 2, 4, 16, 16, 1>(acc, ring, rs, F(7), 2 * w, F(8), 0, Hs, Es, HP, EP, 0, li, lh, lane);
-    trunk_epi(nullptr);
+    stage<16, 2, 4, K_ROT16, 0, 4, 16, 1, K_ROT16>(acc, ring, rs, F(7), 2 * w, F(8), 0, H0, Es, HP, EP, 0, li, lh, lane, w);
+    relu_to_lds<4, 2>(acc, H1, HP, 0, 64 * w, li, lh);
 
-    // ---- head: O16 = h7 W_head^T + b (sigma | 15 geo | 0), wave w -> rows 32w..32w+31
+    // ---- head: O16 = h7 W_head^T + b (sigma | 15 geo | 0), wave w -> rows 32w..32w+31 (own trunk.7 columns first)
     acc_bias(acc[0][0], BI(8), 0, lh);
-    stage<16, 1, 1, 16, 4, 1>(acc, ring, rs, F(8), 0, F(9), w, Hs, Es, HP, EP, 32 * w, li, lh, lane);
-    bar();  // H1: every wave done reading H (colour layer 0 overwrites it)
+    stage<16, 1, 1, K_ROT16, 0, 4, 4, 1, K_ID>(acc, ring, rs, F(8), 0, F(9), w, H1, Es, HP, EP, 32 * w, li, lh, lane, w);
     const int r = 32 * w + li;
     if (lh == 0) Ssig[r] = acc[0][0][0];
 #pragma unroll
-    for (int q = 0; q < 2; ++q)  // geo (cols 1..15) -> colour input cols 0..14
+    for (int q = 0; q < 2; ++q)  // geo (cols 1..15) -> colour input cols 0..14 (E holds the prefill since B_4)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int c = 8 * q + 4 * lh + e;
         if (c >= 1) Es[r * EP + c - 1] = (nerf_bf16)acc[0][0][4 * q + e];
       }
-    bar();  // H2: colour input complete
+    bar();  // H2: colour input complete; every wave done reading H[1] (trunk.7 output)
 
-    // ---- colour layer 0: C0 = ReLU(CIN W_c0^T + b), wave w -> cols 32w..32w+31 of all rows (tile in H, pitch CP)
+    // ---- colour layer 0: C0 = ReLU(CIN W_c0^T + b), wave w -> cols 32w..32w+31 of all rows, tile in H[1] (pitch CP)
 #pragma unroll
     for (int a = 0; a < 4; ++a) acc_bias(acc[a][0], BI(9), 32 * w, lh);
-    stage<4, 1, 4, 0, 8, 1>(acc, ring, rs, F(9), w, F(10), 0, Hs, Es, HP, EP, 0, li, lh, lane);
-    relu_to_lds<4, 1>(acc, Hs, CP, 0, 32 * w, li, lh);
-    bar();  // C
+    stage<4, 1, 4, K_ID, 1, -1, 8, 1, K_ROT8>(acc, ring, rs, F(9), w, F(10), 0, H1, Es, HP, EP, 0, li, lh, lane, w);
+    relu_to_lds<4, 1>(acc, H1, CP, 0, 32 * w, li, lh);
 
-    // ---- colour out: O3 = C0 W_c1^T + b, wave w -> rows 32w..32w+31; next tile's trunk.0 fragments prefetched
+    // ---- colour out: O3 = C0 W_c1^T + b, wave w -> rows 32w..32w+31 (barrier C after its own 2 k-steps);
+    // the next tile's trunk.0 fragments are prefetched into the ring
     acc_bias(acc[0][0], BI(10), 0, lh);
-    stage<8, 1, 1, 8, 4, 2>(acc, ring, rs, F(10), 0, F(0), 2 * w, Hs, Hs, CP, CP, 32 * w, li, lh, lane);
+    stage<8, 1, 1, K_ROT8, 0, 2, 4, 2, K_ID>(acc, ring, rs, F(10), 0, F(0), 2 * w, H1, Es, CP, EP, 32 * w, li, lh, lane, w);
     const int64_t m = m0 + r;
     if (lh == 0) {
       const float sraw = Ssig[r];
@@ -511,10 +555,6 @@ __device__ __forceinline__ void compute_role(const FusedArgs& A, nerf_bf16* Hs, 
             make_float4(sigmoidf_(acc[0][0][0]), sigmoidf_(acc[0][0][1]), sigmoidf_(acc[0][0][2]), sg);
       }
     }
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) acc_bias(acc[a][b], BI(0), 64 * w + 32 * b, lh);
     bar();  // D: the next tile's encoding is in E
   }
 #undef F
@@ -523,7 +563,7 @@ __device__ __forceinline__ void compute_role(const FusedArgs& A, nerf_bf16* Hs, 
 
 template <bool TRAIN>
 __global__ __launch_bounds__(512, 1) void mlp_fwd_fused_bf16_kernel(FusedArgs A) {
-  __shared__ __attribute__((aligned(16))) nerf_bf16 Hs[BMF * HP];
+  __shared__ __attribute__((aligned(16))) nerf_bf16 Hs[2 * BMF * HP];  // H[0], H[1]: trunk epilogues alternate
   __shared__ __attribute__((aligned(16))) nerf_bf16 Es[BMF * EP];
   __shared__ float Ssig[BMF];
   __shared__ __attribute__((aligned(16))) float Bs[BTOT];
