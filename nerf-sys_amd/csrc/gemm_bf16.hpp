@@ -39,7 +39,7 @@ template <int TM, int TN, int WTM, int WTN, int EPI, int OUT_BF16>
 __device__ __forceinline__ void ntb_epilogue(nerf_f32x16 (&acc)[TM][TN], int64_t mw, int nw, int li, int lh,
                                              const float* __restrict__ bias, void* __restrict__ Cv, int ldc,
                                              const uint32_t* __restrict__ mbits, int ldmb,
-                                             uint32_t* __restrict__ mbits_out) {
+                                             uint32_t* __restrict__ mbits_out, const uint32_t* pre_words = nullptr) {
   const int64_t m0 = mw;
   const int n0 = nw;
   constexpr int wm = 0, wn = 0;
@@ -57,7 +57,7 @@ __device__ __forceinline__ void ntb_epilogue(nerf_f32x16 (&acc)[TM][TN], int64_t
     for (int a = 0; a < TM; ++a) {
       const int64_t m = m0 + wm * WTM + a * 32 + li;
       uint32_t word = 0;
-      if (EPI == EPI_MASK) word = mbits[m * ldmb + g];
+      if (EPI == EPI_MASK) word = pre_words ? pre_words[a * TN + b] : mbits[m * ldmb + g];
       uint2 pk[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -218,20 +218,14 @@ __device__ __forceinline__ nerf_bf16x8 ntb_lds_read(uint32_t byte_addr) {
   return v;
 }
 __device__ __forceinline__ void ntb_wait_vmcnt(int n) {
+  // s_waitcnt needs an immediate: dispatch the (wave-uniform) count to one of the encodings
   switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+#define NTB_W(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    NTB_W(0) NTB_W(1) NTB_W(2) NTB_W(3) NTB_W(4) NTB_W(5) NTB_W(6) NTB_W(7) NTB_W(8) NTB_W(9) NTB_W(10) NTB_W(11)
+    NTB_W(12) NTB_W(13) NTB_W(14) NTB_W(15) NTB_W(16) NTB_W(17) NTB_W(18) NTB_W(19) NTB_W(20) NTB_W(21) NTB_W(22)
+    NTB_W(23) NTB_W(24) NTB_W(25) NTB_W(26) NTB_W(27) NTB_W(28) NTB_W(29) NTB_W(30) NTB_W(31) NTB_W(32)
+#undef NTB_W
+    default: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
   }
 }
 
@@ -495,12 +489,46 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_bf16_wsr_kernel(const nerf_bf1
   for (int s0 = 0; s0 < STAGES - 1; ++s0)
     if (s0 < total) issue(s0);
 
+  // epilogue stores per lane (bf16 outputs: one 16-B store per pair of 32-column halves; fp32: 4 per tile) plus the
+  // ReLU bitmask word stores of the forward; they are younger than the DMA of the next STAGES - 1 slabs, and vmcnt
+  // counts in issue order, so a wait that ignored them would drain the stores at every panel boundary
+#ifndef NERF_WSR_STORE_AWARE
+#define NERF_WSR_STORE_AWARE 1
+#endif
+  // exact count only: an over-count would let a wait pass before its slab landed
+  const int NST = TM * TN * (OUT_BF16 ? 2 : 4) + ((EPI == EPI_BIAS_RELU && mbits_out) ? TM * TN : 0);
+  constexpr int NML = (EPI == EPI_MASK) ? TM * TN : 0;  // mask-word loads issued at each panel start
+  uint32_t words[TM * TN];
   for (int g = 0; g < total; ++g) {
     const int younger = (total - 1 - g) < (STAGES - 2) ? (total - 1 - g) : (STAGES - 2);
-    ntb_wait_vmcnt(younger * 2);
+    // vector-memory ops issued after slab g's DMA (at iteration g - STAGES + 1) and still possibly in flight:
+    // the DMA of the younger slabs, the epilogue stores of iterations g - STAGES + 1 .. g - 1 and the mask-word
+    // loads of panel starts g - STAGES + 2 .. g - 1
+    int extra = 0;
+    if (NERF_WSR_STORE_AWARE) {
+#pragma unroll
+      for (int e = 1; e <= STAGES - 1; ++e) {
+        if (g - e >= 0 && (g - e) % NK == NK - 1) extra += NST;
+        if (e <= STAGES - 2 && g - e >= 0 && (g - e) % NK == 0) extra += NML;
+      }
+    }
+    ntb_wait_vmcnt(younger * 2 + extra);
     __builtin_amdgcn_s_barrier();
-    if (g + STAGES - 1 < total) issue(g + STAGES - 1);
     const int pi = g / NK, kt = g - pi * NK;
+    if (EPI == EPI_MASK && kt == 0) {  // this panel's ReLU mask words, long before its epilogue needs them
+      const int64_t mp = (int64_t)(grp + pi * n_groups) * BM + wm * WTM;
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int t = 0; t < TN; ++t) {
+          // inline-asm load: a compiler-visible load used NK - 1 iterations later makes the waitcnt pass emit
+          // vmcnt(0) at the epilogue (it cannot count across the loop back-edge), draining the DMA ring every panel;
+          // the slab waits above already cover it (it is older than the DMA of slab kt = NK - 1)
+          const uint32_t* pm = mbits + (mp + a * 32 + li) * ldmb + ((n0 + wn * WTN + t * 32) >> 5);
+          asm volatile("global_load_dword %0, %1, off" : "=v"(words[a * TN + t]) : "v"(pm) : "memory");
+        }
+    }
+    if (g + STAGES - 1 < total) issue(g + STAGES - 1);
     const uint32_t st = rbase + (uint32_t)((g % STAGES) * STAGE_E * 2);
     nerf_bf16x8 af[2][TM], bf[2][TN];
 #pragma unroll
@@ -530,8 +558,12 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_bf16_wsr_kernel(const nerf_bf1
           acc[a][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[ks][t], af[ks][a], acc[a][t], 0, 0, 0);
     if (kt == NK - 1) {
       const int64_t m0 = (int64_t)(grp + pi * n_groups) * BM;
+      if (EPI == EPI_MASK) {
+#pragma unroll
+        for (int i = 0; i < TM * TN; ++i) asm volatile("" : "+v"(words[i]));  // uses stay behind the slab wait
+      }
       ntb_epilogue<TM, TN, WTM, WTN, EPI, OUT_BF16>(acc, m0 + wm * WTM, n0 + wn * WTN, li, lh, bias, Cv, ldc, mbits,
-                                                    ldmb, mbits_out);
+                                                    ldmb, mbits_out, EPI == EPI_MASK ? words : nullptr);
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll

@@ -296,7 +296,10 @@ int wgradb(const nerf_bf16* G, int ldg, const nerf_bf16* X, int ldx, int tensor_
   }
   if (N >= 128 && K % 128 == 0) {
     const int nt = (N / 128) * (K / 128);
-    gemm_wgrad_bf16_kernel<128, 128, 2><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp,
+#ifndef NERF_WGRAD_MR
+#define NERF_WGRAD_MR 32
+#endif
+    gemm_wgrad_bf16_kernel<128, 128, 2, NERF_WGRAD_MR><<<nt * w.S, 256, 0, st>>>(G, ldg, X, ldx, P, ldp, Pb, slab, w.rps, w.Mp,
                                                                  K / 128, nt);
   } else if (N >= 128 && K == 64) {
     return narrowb(G, ldg, X, ldx, P, ldp, Pb, slab, w, N, st);

@@ -104,6 +104,12 @@ class NeRFTrainer:
         # 28.1-28.5 ms vs 29.6 ms on one stream; joining the streams before the fine backward instead of at
         # the end of the step serialises it (34.2 ms); stream priorities change nothing.
         self.overlap = bool(overlap) and self.n_nets == 2 and self.device.type == "cuda"
+        # what the coarse backward runs beside: the fine forward (default) or the fine backward (NERF_OVERLAP=bwd,
+        # A/B runs).  Measured on MI355X: fp32 27.4 (fwd) vs 28.4 ms (bwd); bf16 7.30 vs 7.36 ms (the fused bf16
+        # forward is one persistent launch holding every CU's LDS, so the coarse backward mostly queues behind it
+        # either way).
+        import os
+        self.overlap_with = os.environ.get("NERF_OVERLAP") or "fwd"
         self._side = torch.cuda.Stream(device=self.device) if self.overlap else None
 
     # ---- helpers
@@ -170,7 +176,8 @@ class NeRFTrainer:
                                                   color_space=self.color_space, inv_count=inv_count,
                                                   loss_sum=self.loss_buf)
         side_done = None
-        if self.overlap and NI > 0:
+
+        def coarse_bwd_on_side():
             main = torch.cuda.current_stream(self.device)
             fork = torch.cuda.Event()
             fork.record(main)
@@ -178,8 +185,12 @@ class NeRFTrainer:
             with torch.cuda.stream(self._side):
                 d_rs_c = K.composite_bwd(rs_c, t_c, bg, drgb_c, sigma_scale=self.sigma_scale)
                 K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=False, precision=self.precision)
-                side_done = torch.cuda.Event()
-                side_done.record(self._side)
+                done = torch.cuda.Event()
+                done.record(self._side)
+            return done
+
+        if self.overlap and NI > 0 and self.overlap_with == "fwd":
+            side_done = coarse_bwd_on_side()
         if NI > 0:
             t_f = K.sample_pdf(t_c, w_c, NI, u=u_pdf, det=False, seed=seed ^ 0x5EED)
             xd_f = K.build_xd(rays, t_f)
@@ -187,6 +198,8 @@ class NeRFTrainer:
             ev = self._next_events()
             rs_f = K.mlp_fwd(self.w(fine_k), xd_f, ws_f, True, events=ev["fwd"] if ev else None,
                              precision=self.precision)
+            if self.overlap and self.overlap_with == "bwd":
+                side_done = coarse_bwd_on_side()
             _, _, _, _, _, drgb_f = K.composite_fwd(rs_f, t_f, bg, self.sigma_scale, gt=gt,
                                                     color_space=self.color_space, inv_count=inv_count,
                                                     loss_sum=self.loss_buf)
