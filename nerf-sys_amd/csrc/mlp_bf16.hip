@@ -14,6 +14,7 @@
 // bf16, bf16 transposed weights, S fp32 partial slabs of the packed gradient.
 #include "gemm_bf16.hpp"
 #include "mlp_bf16_fused.hpp"
+#include "mlp_bf16_bwd.hpp"
 #include "mlp_common.hpp"
 
 #include <stdlib.h>
@@ -28,7 +29,7 @@ struct WSB {
   nerf_bf16 *Wb, *Wf, *X3E, *Y[8], *CIN, *C0;
   float *O16, *O3;
   uint32_t *MB[8], *MC0;
-  nerf_bf16 *dA, *dB, *dO16, *dO3, *dC0, *WTb;
+  nerf_bf16 *dA, *dB, *dO16, *dO3, *dC0, *WTb, *WTf;
   float *dCIN, *partial;
   int S;
   int64_t rps;
@@ -69,6 +70,7 @@ WSB carve_b(void* base, int64_t M, int training) {
     w.dC0 = (nerf_bf16*)take(Mp * 128 * 2);
     w.dCIN = (float*)take(Mp * 32 * 4);
     w.WTb = (nerf_bf16*)take(WTB_ELEMS * 2);
+    w.WTf = (nerf_bf16*)take(7 * nerf_bwd::FRAG_LAYER * 2);
 #ifndef NERF_BF16_SPLIT_ROWS
 #define NERF_BF16_SPLIT_ROWS 2048
 #endif
@@ -315,6 +317,13 @@ int wgradb(const nerf_bf16* G, int ldg, const nerf_bf16* X, int ldx, int tensor_
 
 }  // namespace
 
+// NERF_BF16_FUSED_BWD=0 selects the layered backward (a dgrad and a wgrad GEMM launch per trunk layer) for A/B
+// measurements; the default fuses both per layer (mlp_bf16_bwd.hpp).
+bool fused_bwd_enabled() {
+  const char* e = getenv("NERF_BF16_FUSED_BWD");
+  return !(e && e[0] == '0');
+}
+
 // NERF_BF16_FUSED=0 selects the layer-by-layer forward (one GEMM launch per layer, activations through HBM) for
 // A/B measurements; the default is the fused single-launch forward (mlp_bf16_fused.hpp).
 bool fused_fwd_enabled() {
@@ -454,6 +463,48 @@ extern "C" int nerf_mlp_bwd_bf16(const float* w, int64_t M, const float* d_rgb_s
   TRY((ntb<EPI_MASK, 1>(W.dO16, 32, Wht, 32, nullptr, dcur, 256, W.MB[7], nullptr, Mp, 256, 32, st)));
   if (ev) (void)hipEventRecord(ev[3], st);
   TRY(wgradb(W.dO16, 32, W.Y[7], 256, 16, W, 32, 256, st));
+  if (fused_bwd_enabled()) {
+    // trunk.7 .. trunk.1: one fused launch per layer (mlp_bf16_bwd.hpp); trunk.0 and the encoding columns of
+    // trunk.4 (no input gradient) stay on the narrow wgrad kernel
+    nerf_bwd::WTSrc src{};
+    for (int i = 1; i < 8; ++i) {
+      src.off[i - 1] = L.off[2 * i];
+      src.ld[i - 1] = KPAD[i];
+    }
+    nerf_bwd::wt_frag_pack_kernel<<<(unsigned)nerf_cdiv(7 * nerf_bwd::FRAG_LAYER / 8, 256), 256, 0, st>>>(w, W.WTf, src);
+    const int S8 = (W.S + 7) / 8 * 8;
+    for (int i = 7; i >= 1; --i) {
+      nerf_bwd::LayerArgs A{};
+      A.G = dcur;
+      A.X = (i == 4) ? W.X3E : W.Y[i - 1];
+      A.ldx = (i == 4 || i - 1 == 3) ? 320 : 256;
+      A.WTf = W.WTf + (int64_t)(i - 1) * nerf_bwd::FRAG_LAYER;
+      A.D = dnext;
+      A.P = W.partial + L.off[2 * i];
+      A.Pb = W.partial + L.off[2 * i + 1];
+      A.ldp = L.cols[2 * i];
+      A.slab = L.total;
+      A.rps = W.rps;
+      A.Mp = Mp;
+      A.S = W.S;
+      if (A.rps % nerf_bwd::TR) return NERF_E_ARG;
+      if (ev) (void)hipEventRecord(ev[4 * i], st);
+      nerf_bwd::bwd_layer_bf16_kernel<<<2 * S8, 768, 0, st>>>(A);
+      if (ev) {
+        (void)hipEventRecord(ev[4 * i + 1], st);
+        (void)hipEventRecord(ev[4 * i + 2], st);
+        (void)hipEventRecord(ev[4 * i + 3], st);
+      }
+      if (i == 4) TRY(narrowb(dcur, 256, W.X3E + 256, 320, A.P + 256, A.ldp, nullptr, L.total, W, 256, st));
+      nerf_bf16* t = dcur; dcur = dnext; dnext = t;
+    }
+    if (ev) (void)hipEventRecord(ev[0], st);
+    TRY(wgradb(dcur, 256, W.X3E + 256, 320, 0, W, 256, KPAD[0], st));
+    if (ev) (void)hipEventRecord(ev[1], st);
+    const int64_t n4 = L.total / 4;
+    reduce_splits_kernel<<<(unsigned)nerf_cdiv(n4, 256), 256, 0, st>>>(W.partial, L.total, W.S, d_w, n4, accumulate);
+    return nerf_launch_status();
+  }
   // trunk
   for (int i = 7; i >= 0; --i) {
     const nerf_bf16* X = (i == 0) ? W.X3E + 256 : (i == 4 ? W.X3E : W.Y[i - 1]);

@@ -131,3 +131,28 @@ def test_fused_forward_matches_layered(K, wpk, monkeypatch):
             continue
         rel = ((got - ref).norm() / ref.norm()).item()
         assert rel <= 2e-2, f"{name}: fused vs layered gradient rel {rel:.3e}"
+
+
+@pytest.mark.parametrize("M", [1, 5000, 40001, 786432])
+def test_fused_backward_matches_layered(K, wpk, monkeypatch, M):
+    """The fused per-layer bf16 backward (mlp_bf16_bwd.hpp: input + weight gradient of a trunk layer in one launch,
+    ReLU mask from the saved input) against the layered dgrad / wgrad launches (NERF_BF16_FUSED_BWD=0): the same
+    bf16 operands, the same MFMA k order and the same split-M slabs, so the packed gradient is BITWISE equal.
+    Sizes: one row; a ragged tile; 19 splits (not a multiple of the 8-split block pairing: idle pairs exit); the
+    C2 fine-net size (256 splits of 3,072 rows, 512 workgroups)."""
+    x = _xd(M, 21).to(DEV)
+    g = torch.Generator().manual_seed(23)
+    gup = (torch.randn(M, 4, generator=g) * 1e-3).to(DEV)
+    ws = K.mlp_workspace(M, True, DEV, "bf16")
+    K.mlp_fwd(wpk, x, ws, True, precision="bf16")
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("NERF_BF16_FUSED_BWD", mode)
+        res[mode] = K.mlp_bwd(wpk, M, gup, ws, precision="bf16")
+        torch.cuda.synchronize()
+    assert torch.isfinite(res["1"]).all()
+    if not torch.equal(res["0"], res["1"]):
+        from nerf_amd.vanilla import PackedLayout
+        a, b = PackedLayout.get().unpack(res["1"].cpu()), PackedLayout.get().unpack(res["0"].cpu())
+        bad = {n: float((a[n] - b[n]).abs().max()) for n in b if not torch.equal(a[n], b[n])}
+        raise AssertionError(f"fused backward != layered at M={M}: {bad}")
