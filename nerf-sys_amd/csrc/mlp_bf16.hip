@@ -70,7 +70,7 @@ WSB carve_b(void* base, int64_t M, int training) {
     w.dC0 = (nerf_bf16*)take(Mp * 128 * 2);
     w.dCIN = (float*)take(Mp * 32 * 4);
     w.WTb = (nerf_bf16*)take(WTB_ELEMS * 2);
-    w.WTf = (nerf_bf16*)take(7 * nerf_bwd::FRAG_LAYER * 2);
+    w.WTf = (nerf_bf16*)take(7 * nerf_bwd::WT_LAYER * 2);
 #ifndef NERF_BF16_SPLIT_ROWS
 #define NERF_BF16_SPLIT_ROWS 2048
 #endif
@@ -471,14 +471,14 @@ extern "C" int nerf_mlp_bwd_bf16(const float* w, int64_t M, const float* d_rgb_s
       src.off[i - 1] = L.off[2 * i];
       src.ld[i - 1] = KPAD[i];
     }
-    nerf_bwd::wt_frag_pack_kernel<<<(unsigned)nerf_cdiv(7 * nerf_bwd::FRAG_LAYER / 8, 256), 256, 0, st>>>(w, W.WTf, src);
+    nerf_bwd::wt_pack_kernel<<<(unsigned)nerf_cdiv(7 * nerf_bwd::WT_LAYER / 8, 256), 256, 0, st>>>(w, W.WTf, src);
     const int S8 = (W.S + 7) / 8 * 8;
     for (int i = 7; i >= 1; --i) {
       nerf_bwd::LayerArgs A{};
       A.G = dcur;
       A.X = (i == 4) ? W.X3E : W.Y[i - 1];
       A.ldx = (i == 4 || i - 1 == 3) ? 320 : 256;
-      A.WTf = W.WTf + (int64_t)(i - 1) * nerf_bwd::FRAG_LAYER;
+      A.WT = W.WTf + (int64_t)(i - 1) * nerf_bwd::WT_LAYER;
       A.D = dnext;
       A.P = W.partial + L.off[2 * i];
       A.Pb = W.partial + L.off[2 * i + 1];

@@ -14,27 +14,30 @@
 // Work split: the 256 x 256 fp32 accumulators of a split (256 KiB) are more than one workgroup can hold next to its
 // other state, so a split is served by a PAIR of workgroups, h = 0 / 1 owning input columns k in [128 h, 128 h + 128)
 // of both dW and dX.  Blocks b and b + 8 form a pair (round-robin XCD dealing puts them on one XCD: the G tile both
-// stream is then read from HBM once and hit in L2 by the partner — speed only, never correctness).
+// stream is then read from HBM once and hit in L2 by the partner — PMC: 788 MB fetched per fine launch against
+// 806 MB of G + X; speed only, never correctness).
 // Workgroup = 12 waves (3 per SIMD, <= 168 VGPRs each):
 //   compute waves c = 0..7 own input-column block kb = 4 h + (c & 3) (32 columns) and half mh = c >> 2:
 //     wgrad  acc[j] (j = 0..3) = dW[32 (4 mh + j)..][32 kb..]: 4 x v_mfma_f32_32x32x16_bf16 accumulators (64 VGPRs),
 //            A = G^T, B = X^T fragments by ds_read_b64_tr_b16 (transposing reads, gfx950);
-//     dgrad  dX[rows 32 mh..][32 kb..] = G W_i[:, kb]: 1 accumulator, A = W_i^T fragments streamed from L2 (a
-//            fragment-major image, one contiguous KiB per wave-load) through a 4-deep register ring, B = G row fragments;
+//     dgrad  dX[rows 32 mh..][32 kb..] = G W_i[:, kb]: 1 accumulator, A = W_i^T fragments from the workgroup's
+//            LDS-resident W^T half (64 KiB, loaded once), B = G row fragments;
 //     epilogue: ReLU mask from the X tile in LDS, bf16, 16-B stores of D.
-//   io waves j = 0..3 (waves 8..11) move the tiles HBM -> LDS by LDS-DMA (global_load_lds_dwordx4): a compute wave then holds
-//     only L2-latency loads in its in-order vmcnt queue (a wait on a weight fragment never waits for HBM).
-// Tiles of 64 rows: G [64][256] (32 KiB) + X half [64][128] (16 KiB) per stage, 3 stages (144 KiB) -> two tiles in
-// flight while one is computed; one workgroup barrier per tile.
+//     A compute wave issues no global load at all: its only vector-memory operations are the D stores.  (A first
+//     version streamed W^T fragments from L2 through a register ring; queued behind the CU's tile traffic an L2 hit
+//     took longer than the ring's 4 k-steps of cover and the kernel ran at 332 us per fine launch.)
+//   io waves j = 0..3 (waves 8..11) stream the tiles HBM -> registers -> LDS: two register sets of one tile each
+//     (48 VGPRs); a set is written into the free LDS stage and reloaded at once, so two tiles are always in flight.
+// Tiles of 64 rows: G [64][256] (32 KiB) + X half [64][128] (16 KiB) per stage, 2 stages + W^T half = 160 KiB;
+// one workgroup barrier per tile.
 // LDS images are unpadded and XOR-swizzled per 16-B chunk: chunk c of row r sits at slot c ^ swz(r),
 // swz(r) = 4 (r & 3) + ((r >> 2) & 3).  Conflict-free for all three access shapes: a ds_read_b128 lane group (16
 // rows, one chunk: 16 distinct swz), a ds_read_b64_tr_b16 half-wave (4 rows r0..r0+3, r0 % 4 == 0, x 4 aligned
-// chunks: slot = (c ^ 4 q) + (p ^ k) -> 16 distinct slots) and the epilogue's mask reads (as the first).  The DMA
-// writes lane-linear 1-KiB pieces, so the permutation is applied to the SOURCE address.
+// chunks: slot = (c ^ 4 q) + (p ^ k) -> 16 distinct slots) and the epilogue's mask reads (as the first).
 //
 // MFMA order: the weight-gradient k-steps walk the split's rows 16 at a time in row order and the input gradient
 // contracts n in 16-wide steps in order, exactly as gemm_wgrad_bf16 / gemm_nt_bf16_wsr do: the result is bitwise
-// the layered path's.
+// the layered path's (tests/test_gpu_bf16.py::test_fused_backward_matches_layered).
 #pragma once
 #include <type_traits>
 
@@ -47,38 +50,38 @@ constexpr int TR = 64;                  // rows per tile
 constexpr int GBY = TR * 512;           // G tile bytes (64 rows x 256 bf16)
 constexpr int XBY = TR * 256;           // X half tile bytes (64 rows x 128 bf16)
 constexpr int STB = GBY + XBY;          // 48 KiB per stage
-constexpr int NSTG = 3;
-constexpr int FRAG_LAYER = 8 * 16 * 64 * 8;  // bf16 elements of one layer's W^T fragment image (128 KiB)
+constexpr int NSTG = 2;
+constexpr int WOFF = NSTG * STB;        // W^T half: [128 k][256 n] bf16, 64 KiB
+constexpr int LDS_BYTES = WOFF + 128 * 512;
+static_assert(LDS_BYTES <= 163840, "LDS");
+constexpr int WT_LAYER = 256 * 256;     // bf16 elements of one layer's W^T image
 
 __device__ __forceinline__ int swz(int r) { return 4 * (r & 3) + ((r >> 2) & 3); }
 
-// W_i^T fragment image of trunk layers i = 1..7 (image i - 1): fragment (kb, ks), lane l, element j holds
-// W_i[n = 16 ks + 8 (l >> 5) + j][k = 32 kb + (l & 31)] (bf16) — the A operand of dX^T = W^T G^T; for trunk.4 only
-// the first 256 input columns (the trunk.3 output; the encoding columns need no input gradient).
+// W_i^T of trunk layers i = 1..7 (image i - 1), row-major bf16: WT[k][n] = W_i[n][k] for k < 256 (trunk.4: its first
+// 256 input columns, the trunk.3 output; the encoding columns need no input gradient).
 struct WTSrc {
   int64_t off[7];  // fp32 offset of W_i (i = 1..7) in the packed layout
   int ld[7];       // its row pitch (KPAD[i])
 };
-__global__ void wt_frag_pack_kernel(const float* __restrict__ w, nerf_bf16* __restrict__ wf, WTSrc S) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 16-B chunk index
-  if (c >= 7 * FRAG_LAYER / 8) return;
-  const int img = (int)(c / (FRAG_LAYER / 8));
-  const int r = (int)(c - (int64_t)img * (FRAG_LAYER / 8));
-  const int lane = r & 63, ks = (r >> 6) & 15, kb = r >> 10;
-  const float* src = w + S.off[img] + (int64_t)(16 * ks + 8 * (lane >> 5)) * S.ld[img] + 32 * kb + (lane & 31);
+__global__ void wt_pack_kernel(const float* __restrict__ w, nerf_bf16* __restrict__ wt, WTSrc S) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 8 consecutive n of one k
+  if (c >= 7 * WT_LAYER / 8) return;
+  const int img = (int)(c / (WT_LAYER / 8));
+  const int r = (int)(c - (int64_t)img * (WT_LAYER / 8));
+  const int k = r >> 5, n0 = 8 * (r & 31);
+  const float* src = w + S.off[img] + (int64_t)n0 * S.ld[img] + k;
   float v[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = src[(int64_t)j * S.ld[img]];
-  *reinterpret_cast<uint4*>(wf + c * 8) = make_uint4(nerf_pack_bf16x2(v[0], v[1]), nerf_pack_bf16x2(v[2], v[3]),
+  *reinterpret_cast<uint4*>(wt + c * 8) = make_uint4(nerf_pack_bf16x2(v[0], v[1]), nerf_pack_bf16x2(v[2], v[3]),
                                                      nerf_pack_bf16x2(v[4], v[5]), nerf_pack_bf16x2(v[6], v[7]));
 }
-
-typedef unsigned int nerf_bwd_u32x4 __attribute__((ext_vector_type(4)));
 
 struct LayerArgs {
   const nerf_bf16* G;    // dZ_i [Mp][256]
   const nerf_bf16* X;    // X_i, row pitch ldx (cols 0..255 used)
-  const nerf_bf16* WTf;  // this layer's W^T fragment image (FRAG_LAYER bf16)
+  const nerf_bf16* WT;   // this layer's W^T image [256][256]
   nerf_bf16* D;          // dZ_{i-1} [Mp][256]
   float* P;              // weight-gradient slab 0 of this tensor (row pitch ldp)
   float* Pb;             // bias-gradient slab 0
@@ -86,37 +89,6 @@ struct LayerArgs {
   int64_t rps, Mp;       // rows per split (multiple of 64), padded rows (multiple of 256)
   int ldx, ldp, S;
 };
-
-// io wave j: DMA pieces of tile t (rows m0 .. m0 + 63) into stage st: G pieces 8 j .. 8 j + 7 (2 rows each), X-half
-// pieces 4 j .. 4 j + 3 (4 rows each); lane L of a piece writes LDS slot L, so it fetches the chunk that the swizzle
-// puts there.
-__device__ __forceinline__ void io_issue(const LayerArgs& A, char* st, int64_t m0, int h, int j, int lane) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int p = 8 * j + i;
-    const int row = 2 * p + (lane >> 5);
-    const int c = (lane & 31) ^ swz(row);
-    const nerf_bf16* src = A.G + (m0 + row) * 256 + 8 * c;
-    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(st + p * 1024), 16, 0, 0);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int p = 4 * j + i;
-    const int row = 4 * p + (lane >> 4);
-    const int c = (lane & 15) ^ swz(row);
-    const nerf_bf16* src = A.X + (m0 + row) * (int64_t)A.ldx + 128 * h + 8 * c;
-    __builtin_amdgcn_global_load_lds((const void*)src,
-                                     (__attribute__((address_space(3))) void*)(st + GBY + p * 1024), 16, 0, 0);
-  }
-}
-
-__device__ __forceinline__ nerf_bf16x8 tr_frag(const char* base, int o0, int o1) {
-  typedef __attribute__((address_space(3))) nerf_s16x4 lds_s16x4;
-  const nerf_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + o0));
-  const nerf_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + o1));
-  const short v8 __attribute__((ext_vector_type(8))) = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(nerf_bf16x8, v8);
-}
 
 // inline-asm LDS reads (byte address + immediate offset); the caller waits lgkmcnt before the use
 template <int OFF>
@@ -127,17 +99,17 @@ __device__ __forceinline__ nerf_bf16x8 tr_frag_asm(uint32_t a0, uint32_t a1) {
   const short v8 __attribute__((ext_vector_type(8))) = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(nerf_bf16x8, v8);
 }
+__device__ __forceinline__ nerf_bf16x8 lds_b128(uint32_t a) {
+  nerf_bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (I < N) {
     f(std::integral_constant<int, I>{});
     static_for<I + 1, N>(f);
   }
-}
-__device__ __forceinline__ nerf_bf16x8 lds_b128(uint32_t a) {
-  nerf_bf16x8 v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
-  return v;
 }
 
 typedef unsigned short nerf_u16x2b __attribute__((ext_vector_type(2)));
@@ -148,9 +120,8 @@ __device__ __forceinline__ uint32_t relu_mask2(uint32_t v, uint32_t x) {
   return v & __builtin_bit_cast(uint32_t, m);
 }
 
-// raw workgroup barrier: __syncthreads() carries a workgroup fence, and the io waves' outstanding LDS-DMA would make
-// that fence wait for vmcnt(0) (draining the prefetch); the empty asm statements keep memory operations from being
-// moved across it at the IR level, the sched_barriers at the machine level
+// raw workgroup barrier (no fence): every wave waits for its own LDS writes before it; the empty asm statements keep
+// memory operations from being moved across it at the IR level, the sched_barriers at the machine level
 __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -160,19 +131,32 @@ __device__ __forceinline__ void raw_barrier() {
 }
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
-__device__ __forceinline__ void bwd_compute(const LayerArgs& A, const char* lds, int s, int h, int c, int nT,
+// every wave: this workgroup's W^T half (rows k = 128 h .. 128 h + 127 of the image) -> LDS, swizzled by row
+__device__ __forceinline__ void load_wt(const LayerArgs& A, char* lds, int h, int tid) {
+  constexpr int CH = 128 * 32;  // 16-B chunks
+  for (int i0 = 0; i0 < CH; i0 += 768 * 4) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * 768 + tid;
+      if (i < CH) v[u] = *reinterpret_cast<const uint4*>(A.WT + (int64_t)(128 * h + (i >> 5)) * 256 + 8 * (i & 31));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * 768 + tid;
+      if (i < CH) {
+        const int r = i >> 5, c = i & 31;
+        *reinterpret_cast<uint4*>(lds + WOFF + r * 512 + 16 * (c ^ swz(r))) = v[u];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void bwd_compute(const LayerArgs& A, char* lds, int s, int h, int c, int nT,
                                             int64_t r0, int lane) {
   const int li = lane & 31, lh = lane >> 5;
   const int kl = c & 3, mh = c >> 2;  // local 32-column block, row half / n-block half
   const int kb = 4 * h + kl;          // global 32-column block of this wave
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)A.WTf, 0, FRAG_LAYER * 2, 0x00020000);
-  auto wfrag = [&](int ks) {
-    const nerf_bwd_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + kb * 16 * 1024, ks * 1024, 0);
-    return __builtin_bit_cast(nerf_bf16x8, v);
-  };
-  nerf_bf16x8 ring[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) ring[i] = wfrag(i);
 
   nerf_f32x16 acc[4];  // dW[32 (4 mh + j)..][32 kb..], j = 0..3
 #pragma unroll
@@ -196,18 +180,17 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, const char* lds,
     for (int j = 0; j < 4; ++j) ga[tt][j] = base + 64 * (j ^ q);  // n-block 4 mh + j, + 8192 ks
     xa[tt] = GBY + (trow + 4 * tt) * 256 + 64 * (kl ^ q) + 16 * (tc ^ e) + tbyte;  // + 4096 ks
   }
-  // row fragments of G (dgrad B operand) and the X mask reads: row 32 mh + li, chunk ch -> slot ch ^ swz(li)
-  const int gs = swz(li);
-  const int rowg = (32 * mh + li) * 512, rowx = GBY + (32 * mh + li) * 256;
+  // row fragments: G row 32 mh + li and W^T row 32 kl + li, chunk 2 ks + lh -> slot (2 ks) ^ u with u = lh ^ swz(li)
+  // (swz(32 a + li) = swz(li)); the X mask reads: X row 32 mh + li, chunk 4 kl + 2 pr + lh -> (4 kl + 2 pr) ^ u
+  const int u = lh ^ swz(li);
+  const uint32_t lbase = (uint32_t)(uintptr_t)lds;
+  const uint32_t wrow = lbase + WOFF + (32 * kl + li) * 512;
 
   // The pipeline below is ordered by hand: LDS reads are inline asm with immediate offsets and counted lgkmcnt waits
   // (the ds_read_tr intrinsic got no offset folding: one address VGPR per read), each wait asm passes the fragments
-  // it covers through "+v" so no MFMA can be hoisted above it, and sched_barrier fences keep the stages in order (the
-  // default scheduler, minimising registers for 3 waves per SIMD, sank every weight-fragment load next to its MFMA).
-  const uint32_t lbase = (uint32_t)(uintptr_t)lds;
-  const int u = lh ^ gs;  // row-fragment chunk 2 ks + lh -> slot (2 ks) ^ u
+  // it covers through "+v" so no MFMA can be hoisted above it, and sched_barrier fences keep the stages in order.
   for (int t = 0; t < nT; ++t) {
-    raw_barrier();  // tile t is in stage t % 3; every wave is done with tile t - 1
+    raw_barrier();  // T_t: tile t is in stage t % 2; every wave is done with tile t - 1
     const uint32_t Lb = lbase + (uint32_t)((t % NSTG) * STB);
     uint32_t gat[2][4], xat[2];
 #pragma unroll
@@ -216,7 +199,13 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, const char* lds,
 #pragma unroll
       for (int j = 0; j < 4; ++j) gat[tt][j] = Lb + ga[tt][j];
     }
-    const uint32_t rg = Lb + rowg, rx = Lb + rowx;
+    const uint32_t rg = Lb + (32 * mh + li) * 512, rx = Lb + GBY + (32 * mh + li) * 256;
+    nerf_bf16x8 wfr[4], gfr[4];  // input-gradient fragments, read 3 k-steps ahead
+    auto dg_reads = [&](int ks) {
+      const uint32_t o = 16 * ((2 * ks) ^ u);
+      wfr[ks & 3] = lds_b128(wrow + o);
+      gfr[ks & 3] = lds_b128(rg + o);
+    };
     // ---- weight gradient: 4 k-steps of 16 rows, fragments of k-step ks + 1 read under the MFMAs of ks (10 reads)
     nerf_bf16x8 xf[2], gf[2][4];
     auto wg_reads = [&](auto KS, int b) {
@@ -225,8 +214,6 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, const char* lds,
 #pragma unroll
       for (int j = 0; j < 4; ++j) gf[b][j] = tr_frag_asm<8192 * ks>(gat[0][j], gat[1][j]);
     };
-    nerf_bf16x8 gr[3];
-    auto grow = [&](int ks) { return lds_b128(rg + 16 * ((2 * ks) ^ u)); };
     wg_reads(std::integral_constant<int, 0>{}, 0);
     static_for<0, 4>([&](auto KS) {
       constexpr int ks = decltype(KS)::value;
@@ -235,10 +222,11 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, const char* lds,
         wg_reads(std::integral_constant<int, ks + 1>{}, cb ^ 1);
         asm volatile("s_waitcnt lgkmcnt(10)" : "+v"(xf[cb]), "+v"(gf[cb][0]), "+v"(gf[cb][1]), "+v"(gf[cb][2]),
                      "+v"(gf[cb][3])::"memory");
-      } else {  // the input gradient's first two row fragments go out under the last weight-gradient MFMAs
-        gr[0] = grow(0);
-        gr[1] = grow(1);
-        asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(xf[cb]), "+v"(gf[cb][0]), "+v"(gf[cb][1]), "+v"(gf[cb][2]),
+      } else {  // the input gradient's first three fragment pairs go out under the last weight-gradient MFMAs
+        dg_reads(0);
+        dg_reads(1);
+        dg_reads(2);
+        asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(xf[cb]), "+v"(gf[cb][0]), "+v"(gf[cb][1]), "+v"(gf[cb][2]),
                      "+v"(gf[cb][3])::"memory");
       }
       SCHED_FENCE();
@@ -246,31 +234,31 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, const char* lds,
       for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf[cb][j], xf[cb], acc[j], 0, 0, 0);
       SCHED_FENCE();
     });
-    // ---- input gradient: dX^T[32 kb..][rows 32 mh..] over n in 16 k-steps; row fragments read 2 k-steps ahead,
-    // weight fragments 4 k-steps ahead (the ring runs on into the next tile: W is the same for every tile)
+    // ---- input gradient: dX^T[32 kb..][rows 32 mh..] over n in 16 k-steps
     nerf_f32x16 dacc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) dacc[r] = 0.f;
     nerf_bf16x8 xm[2];
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) {
-      const nerf_bf16x8 wf = ring[ks & 3];
-      ring[ks & 3] = wfrag((ks + 4) & 15);
-      nerf_bf16x8& g = gr[ks % 3];
-      if (ks + 2 < 16) {
-        gr[(ks + 2) % 3] = grow(ks + 2);
-        asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(g)::"memory");
-      } else if (ks == 14) {  // the epilogue's ReLU-mask chunks (local chunk 4 kl + 2 pr + lh of the X half)
+    static_for<0, 16>([&](auto KS) {
+      constexpr int ks = decltype(KS)::value;
+      nerf_bf16x8& wf = wfr[ks & 3];
+      nerf_bf16x8& g = gfr[ks & 3];
+      if constexpr (ks + 3 < 16) {
+        dg_reads(ks + 3);
+        asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(wf), "+v"(g)::"memory");
+      } else if constexpr (ks == 13) {  // the epilogue's ReLU-mask chunks
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr) xm[pr] = lds_b128(rx + 16 * ((4 * kl + 2 * pr) ^ u));
-        asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(g)::"memory");
+        asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(wf), "+v"(g)::"memory");
+      } else if constexpr (ks == 14) {
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(wf), "+v"(g)::"memory");
       } else {
-        asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(g)::"memory");
+        asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(wf), "+v"(g)::"memory");
       }
       SCHED_FENCE();
       dacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, g, dacc, 0, 0, 0);
       SCHED_FENCE();
-    }
+    });
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xm[0]), "+v"(xm[1])::"memory");
     // ---- epilogue: lane li owns row 32 mh + li, register 4 q + e = column 8 q + 4 lh + e of the wave's block
     nerf_bf16* Dt = A.D + (r0 + (int64_t)t * TR + 32 * mh + li) * 256 + 32 * kb + 8 * lh;
@@ -303,58 +291,106 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, const char* lds,
   }
 }
 
-// io wave j: the DMA stream, plus (workgroup h = 0 only) the bias gradient Pb[n] = sum_m G[m][n] of columns
-// n = 64 j + 32 e + (lane & 31), e = 0 / 1, from the G tile already in LDS: lane half lh sums the rows 16 ks + 8 lh + jj
-// of every 16-row k-step in row order and the halves are added at the end — the summation order of gemm_wgrad_bf16's
-// bias column sums (its G^T fragment of lane (li, lh) holds those 8 rows), so Pb is bitwise the layered path's.
-__device__ __forceinline__ void bwd_io(const LayerArgs& A, char* lds, int s, int h, int j, int nT, int64_t r0, int lane) {
-  const int lh = lane >> 5;
-  float bs[2] = {0.f, 0.f};
-  if (nT > 0) io_issue(A, lds, r0, h, j, lane);
-  if (nT > 1) io_issue(A, lds + STB, r0 + TR, h, j, lane);
-  for (int t = 0; t < nT; ++t) {
-    if (t + 1 < nT)
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // tile t + 1's 12 pieces may stay in flight
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    raw_barrier();  // tile t visible to every wave; every wave is done with tile t - 1 (stage (t + 2) % 3)
-    if (t + 2 < nT) io_issue(A, lds + ((t + 2) % NSTG) * STB, r0 + (int64_t)(t + 2) * TR, h, j, lane);
-    if (h == 0) {
-      // tile t stays in its stage until the DMA issued after the NEXT barrier, which this wave only passes after these
-      // reads.  Inline-asm LDS reads: a compiler-visible LDS read would be preceded by vmcnt(0) (the DMA in flight)
-      const uint32_t Gs = (uint32_t)(uintptr_t)(lds + (t % NSTG) * STB);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        uint32_t u[8][2];
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          const int row = 16 * ks + 8 * lh + jj;
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const int n = 64 * j + 32 * e + (lane & 31);
-            const uint32_t ad = Gs + row * 512 + 16 * ((n >> 3) ^ swz(row)) + 2 * (n & 7);
-            asm volatile("ds_read_u16 %0, %1" : "=v"(u[jj][e]) : "v"(ad) : "memory");
-          }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj)
-#pragma unroll
-          for (int e = 0; e < 2; ++e) bs[e] += __uint_as_float(u[jj][e] << 16);
-      }
-    }
+// io wave j: rows 16 j .. 16 j + 15 of every tile, HBM -> registers (one tile per register set, 12 x 16 B per lane:
+// 8 G pieces of 2 rows, 4 X-half pieces of 4 rows, each wave-instruction 1 KiB contiguous) -> swizzled LDS stage
+// Named members, not arrays: an array member of a set held across loop iterations stays a stack object (scratch),
+// with every load waited on before its scratch store.
+typedef unsigned int io_u32x4 __attribute__((ext_vector_type(4)));  // a vector value (uint4 copies become memcpy)
+struct IoSet {
+  io_u32x4 v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11;  // 0..7: G pieces, 8..11: X-half pieces
+  template <int I>
+  __device__ __forceinline__ io_u32x4& at() {
+    if constexpr (I == 0) return v0;
+    else if constexpr (I == 1) return v1;
+    else if constexpr (I == 2) return v2;
+    else if constexpr (I == 3) return v3;
+    else if constexpr (I == 4) return v4;
+    else if constexpr (I == 5) return v5;
+    else if constexpr (I == 6) return v6;
+    else if constexpr (I == 7) return v7;
+    else if constexpr (I == 8) return v8;
+    else if constexpr (I == 9) return v9;
+    else if constexpr (I == 10) return v10;
+    else return v11;
   }
-  if (h == 0) {
+};
+__device__ __forceinline__ void io_load(IoSet& S, const LayerArgs& A, int64_t m0, int h, int j, int lane) {
+  const nerf_bf16* g = A.G + (m0 + 16 * j + (lane >> 5)) * 256 + 8 * (lane & 31);
+  const nerf_bf16* x = A.X + (m0 + 16 * j + (lane >> 4)) * (int64_t)A.ldx + 128 * h + 8 * (lane & 15);
+  static_for<0, 8>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    S.template at<i>() = *reinterpret_cast<const io_u32x4*>(g + 2 * i * 256);
+  });
+  static_for<0, 4>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    S.template at<8 + i>() = *reinterpret_cast<const io_u32x4*>(x + 4 * i * (int64_t)A.ldx);
+  });
+}
+__device__ __forceinline__ void io_store(IoSet& S, char* st, int j, int lane) {
+  static_for<0, 8>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    const int r = 16 * j + 2 * i + (lane >> 5), c = lane & 31;
+    *reinterpret_cast<io_u32x4*>(st + r * 512 + 16 * (c ^ swz(r))) = S.template at<i>();
+  });
+  static_for<0, 4>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    const int r = 16 * j + 4 * i + (lane >> 4), c = lane & 15;
+    *reinterpret_cast<io_u32x4*>(st + GBY + r * 256 + 16 * (c ^ swz(r))) = S.template at<8 + i>();
+  });
+}
+
+// io wave j also accumulates (workgroup h = 0 only) the bias gradient Pb[n] = sum_m G[m][n] from the G pieces it has in
+// registers before they go to LDS: lane (r1, cc) = (lane >> 5, lane & 31) sums rows 16 j + 2 i + r1 of every tile for
+// columns 8 cc .. 8 cc + 7; at the end the two row parities are added (shuffle), the four io waves' partials meet in
+// LDS and io wave 0 adds them in wave order: a fixed order (bitwise reproducible), but not the layered kernel's.
+__device__ __forceinline__ void bias_acc(const IoSet& R, float (&bs)[8]) {
+  static_for<0, 8>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    const io_u32x4 v = const_cast<IoSet&>(R).template at<i>();
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const float v = bs[e] + __shfl_xor(bs[e], 32, 64);
-      if (lh == 0) A.Pb[(int64_t)s * A.slab + 64 * j + 32 * e + (lane & 31)] = v;
+    for (int d = 0; d < 4; ++d) {
+      bs[2 * d] += __uint_as_float(v[d] << 16);
+      bs[2 * d + 1] += __uint_as_float(v[d] & 0xffff0000u);
     }
+  });
+}
+
+// Two named register sets (an array of sets held across loop iterations is left in scratch): tile k lives in set k % 2.
+// Step t stores tile t + 1 into the stage tile t - 1 held, then reloads that set with tile t + 3, so tiles t + 2 and
+// t + 3 are in flight while tile t is computed.  Inside the loop every step stores and loads unconditionally (past the
+// end: the last tile again, into a stage nobody reads), so the compiler's vmcnt bookkeeping sees one fixed pattern —
+// with conditional loads it fell back to draining (vmcnt(0)) before every store.
+__device__ __forceinline__ void io_step(IoSet& R, const LayerArgs& A, char* lds, int h, int j, int t, int nT,
+                                        int64_t r0, int lane, float (&bs)[8]) {
+  raw_barrier();  // T_t: tile t in stage t % 2 is complete; every wave is done with tile t - 1
+  if (h == 0 && t + 1 < nT) bias_acc(R, bs);
+  io_store(R, lds + ((t + 1) % NSTG) * STB, j, lane);
+  const int tl = t + 3 < nT ? t + 3 : nT - 1;
+  io_load(R, A, r0 + (int64_t)tl * TR, h, j, lane);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile t + 1's LDS writes are done before T_{t+1}
+}
+
+__device__ __forceinline__ void bwd_io(const LayerArgs& A, char* lds, int h, int j, int nT, int64_t r0, int lane,
+                                       float (&bs)[8]) {
+  if (nT == 0) return;
+  IoSet R0, R1;
+  io_load(R0, A, r0, h, j, lane);
+  io_load(R1, A, r0 + (int64_t)(nT > 1 ? 1 : 0) * TR, h, j, lane);
+  if (h == 0) bias_acc(R0, bs);
+  io_store(R0, lds, j, lane);
+  io_load(R0, A, r0 + (int64_t)(nT > 2 ? 2 : nT - 1) * TR, h, j, lane);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  int t = 0;
+  for (; t + 1 < nT; t += 2) {
+    io_step(R1, A, lds, h, j, t, nT, r0, lane, bs);
+    io_step(R0, A, lds, h, j, t + 1, nT, r0, lane, bs);
   }
+  if (t < nT) io_step(R1, A, lds, h, j, t, nT, r0, lane, bs);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's redundant loads land before the wave retires
 }
 
 __global__ __launch_bounds__(768, 3) void bwd_layer_bf16_kernel(LayerArgs A) {
-  __shared__ __attribute__((aligned(1024))) char lds[NSTG * STB];
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
   const int b = blockIdx.x;
   const int h = (b >> 3) & 1;
   const int s = (b >> 4) * 8 + (b & 7);
@@ -365,10 +401,33 @@ __global__ __launch_bounds__(768, 3) void bwd_layer_bf16_kernel(LayerArgs A) {
   const int nT = r1 > r0 ? (int)((r1 - r0) / TR) : 0;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  load_wt(A, lds, h, (int)threadIdx.x);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // W^T in LDS before T_0 (the loop's first barrier)
+  float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (w >= 8)
-    bwd_io(A, lds, s, h, w - 8, nT, r0, lane);
+    bwd_io(A, lds, h, w - 8, nT, r0, lane, bs);
   else
     bwd_compute(A, lds, s, h, w, nT, r0, lane);
+  if (h == 0) {  // bias gradient: parities by shuffle, the io waves' partials through LDS (stage 0 is free now)
+    raw_barrier();
+    float* part = reinterpret_cast<float*>(lds);
+    if (w >= 8) {
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        const float v = bs[d] + __shfl_xor(bs[d], 32, 64);
+        if (lane < 32) part[(w - 8) * 256 + 8 * lane + d] = v;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (w == 8) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = 64 * e + lane;
+        A.Pb[(int64_t)s * A.slab + n] = ((part[n] + part[256 + n]) + part[512 + n]) + part[768 + n];
+      }
+    }
+  }
 }
 
 }  // namespace nerf_bwd
