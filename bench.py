@@ -17,6 +17,9 @@ Prints ONE JSON line on rank 0 (contract in the task statement), with
                   backward, so its wall durations are not per-kernel times and it is not eligible;
                   --no-overlap makes it eligible).  Durations are HIP events the library records on the
                   launch stream inside every timed step; achieved = algorithmic FLOP per launch / mean.
+                  With --precision bf16 the MLP is one fused forward launch plus one fused backward launch
+                  per trunk layer (HBM-bound): the kernel with the largest total time per step is reported
+                  against the HBM peak, with algorithmic bytes per launch (roofline_bf16).
   cpu_baseline  — the CPU oracle (a restatement of the reference's PyTorch path, pinned to its golden
                   vectors) running the same train step (4096 rays, 64+128, 2 nets), median of >= 5 steps
                   on this host (rank 0, N=1).
@@ -181,7 +184,58 @@ def _batch(rb, a, step, rank, world, n_local):
     return rb.batch(n_local, seed=shard_seed(step, rank, world))  # disjoint per-rank streams
 
 
+def _traffic(bf16, key):
+    tpath = os.path.join(ROOT, "profiles", "traffic_bf16.json" if bf16 else "traffic.json")
+    if os.path.exists(tpath):
+        try:
+            return json.load(open(tpath)).get(key)
+        except Exception:
+            return None
+    return None
+
+
+def roofline_bf16(tm):
+    """bf16 (configs[2]): the MLP runs as ONE fused forward launch (mlp_bf16_fused.hpp; events 0 -> 1 bracket it) and,
+    per trunk layer, ONE fused backward launch (mlp_bf16_bwd.hpp: input + weight gradient; events 4i -> 4i+1).
+    Both are HBM-bound; the reported kernel is the class with the largest TOTAL time per step (launch mean x
+    launches per step), the other is listed beside it.
+    Algorithmic bytes per sample row:
+      fused_bwd_layer  G (dZ_i) 512 B read + X_i 512 B read + dZ_{i-1} 512 B written = 1,536 B
+                       (+ the split-M weight-gradient slabs, S x 256 KiB per launch, listed as slab_bytes)
+      fused_fwd        encoding + colour-input prefill 256 B read; saved activations 7 x 512 + trunk.3 512 B,
+                       ReLU masks 256 B, colour input 128 B, colour layer 0 256 B + mask 16 B, sigma /
+                       colour-out pre-activations 20 B, rgb_sigma 16 B written = 5,044 B"""
+    M = tm["M"]
+    mean = lambda xs: sum(xs) / len(xs)
+    bwd_ms = mean([st[i] for st in tm["wgrad"] for i in K256])
+    fwd_ms = mean([st[0] for st in tm["fwd"]])
+    S = min(256, max(1, (M + 255) // 256 * 256 // 2048))
+    cls = {
+        "fused_bwd_layer": {"kernel": "bwd_layer_bf16 (fused input + weight gradient of one 256x256 trunk layer)",
+                            "mean_launch_ms": bwd_ms, "launches": len(K256), "bytes": 1536.0 * M,
+                            "slab_bytes": S * 256 * 256 * 4.0, "flop": 2 * 2.0 * M * 256 * 256},
+        "fused_fwd": {"kernel": "mlp_fwd_fused_bf16 (whole MLP forward, one persistent launch)",
+                      "mean_launch_ms": fwd_ms, "launches": 1, "bytes": 5044.0 * M, "flop": 2.0 * MAC_PER_EVAL * M},
+    }
+    for k, c in cls.items():
+        ms = c["mean_launch_ms"]
+        c["achieved_gbs"] = round(c["bytes"] / (ms * 1e-3) / 1e9, 1)
+        c["hbm_frac"] = round(c["bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        c["mfma_tflops"] = round(c["flop"] / (ms * 1e-3) / 1e12, 1)
+        c["mfma_frac_bf16"] = round(c["flop"] / (ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4)
+        c["ms_per_step"] = round(ms * c["launches"], 4)
+        c["mean_launch_ms"] = round(ms, 4)
+    dom = max(cls, key=lambda k: cls[k]["ms_per_step"])
+    d = cls[dom]
+    return {"bound": "hbm", "kernel": f"{d['kernel']}, fine net M={M}", "achieved": d["achieved_gbs"],
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": d["hbm_frac"], "bytes_per_launch": d["bytes"],
+            "traffic": _traffic(True, dom), "class": dom, "mean_launch_ms": d["mean_launch_ms"],
+            "classes": cls, "rule": "largest total time per step (mean launch x launches) among the fused MLP kernels"}
+
+
 def roofline(tm, bf16, overlap):
+    if bf16 and os.environ.get("NERF_BF16_FUSED", "1") != "0" and os.environ.get("NERF_BF16_FUSED_BWD", "1") != "0":
+        return roofline_bf16(tm)
     M = tm["M"]
     mean = lambda xs: sum(xs) / len(xs)
     flop256 = 2.0 * M * 256 * 256
@@ -190,21 +244,6 @@ def roofline(tm, bf16, overlap):
         "wgrad": mean([st[i] for st in tm["wgrad"] for i in K256]),
         "dgrad": mean([st[i - 1] for st in tm["dgrad"] for i in K256]),
     }
-    fused = None
-    if bf16 and cls["fwd"] < 0.02 * cls["dgrad"]:
-        # the bf16 forward is ONE fused launch (mlp_bf16_fused.hpp): events 0 -> 1 bracket it, the per-layer
-        # events are empty.  Algorithmic work per sample row: 2 x 500,864 MAC of MFMA; HBM: reads the encoding +
-        # colour-input prefill (256 B), writes the saved activations for the backward (7 trunk outputs + the
-        # trunk.3 output 4,096 B, ReLU masks 256 B, colour input 128 B, colour layer 0 256 B + mask 16 B, sigma /
-        # colour-out pre-activations 20 B) and rgb_sigma (16 B) = 5,044 B.
-        fms = mean([st[0] for st in tm["fwd"]])
-        fby = 5044.0 * M
-        fused = {"kernel": "mlp_fwd_fused_bf16 (whole MLP forward, one persistent launch)", "mean_launch_ms": round(fms, 4),
-                 "mfma_tflops": round(2.0 * MAC_PER_EVAL * M / (fms * 1e-3) / 1e12, 1),
-                 "mfma_frac_bf16": round(2.0 * MAC_PER_EVAL * M / (fms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4),
-                 "hbm_gbs": round(fby / (fms * 1e-3) / 1e9, 1), "hbm_frac": round(fby / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                 "bytes_per_launch": fby}
-        del cls["fwd"]
     eligible = [k for k in cls if not (overlap and k == "fwd")]
     dom = max(eligible, key=lambda k: cls[k])
     names = {"fwd": "gemm_nt fwd (bias+ReLU)", "wgrad": "gemm_wgrad (split-M, 128x128 tiles)",
@@ -212,7 +251,7 @@ def roofline(tm, bf16, overlap):
     ms = cls[dom]
     ach = flop256 / (ms * 1e-3) / 1e12
     kern = f"{names[dom]}, fine net M={M}: trunk 256x256 layers {K256}"
-    if bf16:
+    if bf16:  # the layered bf16 path (NERF_BF16_FUSED=0 / NERF_BF16_FUSED_BWD=0 A/B runs)
         names = {k: v.replace("gemm_nt", "gemm_nt_bf16").replace("gemm_wgrad", "gemm_wgrad_bf16") for k, v in names.items()}
         kern = f"{names[dom]}, fine net M={M}: trunk 256x256 layers {K256}"
         # bf16 layers are HBM-bound: algorithmic bytes per launch per sample row = bf16 rows in (256 * 2 B) +
@@ -226,16 +265,7 @@ def roofline(tm, bf16, overlap):
     else:
         roof = {"bound": "mfma", "kernel": kern, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "flop_per_launch": flop256}
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic_bf16.json" if bf16 else "traffic.json")
-    if os.path.exists(tpath):
-        try:
-            traffic = json.load(open(tpath)).get(dom)
-        except Exception:
-            traffic = None
-    if fused:
-        roof["fused_fwd"] = fused
-    roof.update({"traffic": traffic, "class": dom, "mean_launch_ms": round(ms, 4),
+    roof.update({"traffic": _traffic(bf16, dom), "class": dom, "mean_launch_ms": round(ms, 4),
                  "classes_ms": {k: round(v, 4) for k, v in cls.items()},
                  "classes_frac": {k: round(flop256 / (v * 1e-3) / 1e12 / (BF16_MFMA_PEAK_TFLOPS if bf16 else
                                                                        FP32_MFMA_PEAK_TFLOPS), 4)

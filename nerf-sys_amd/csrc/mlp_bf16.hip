@@ -15,6 +15,8 @@
 #include "gemm_bf16.hpp"
 #include "mlp_bf16_fused.hpp"
 #include "mlp_bf16_bwd.hpp"
+#include "mlp_bf16_tail.hpp"
+#include "mlp_tail.hpp"
 #include "mlp_common.hpp"
 
 #include <stdlib.h>
@@ -30,11 +32,22 @@ struct WSB {
   float *O16, *O3;
   uint32_t *MB[8], *MC0;
   nerf_bf16 *dA, *dB, *dO16, *dO3, *dC0, *WTb, *WTf;
-  float *dCIN, *partial;
+  float *dCIN, *partial, *partial2;
   int S;
   int64_t rps;
   int64_t bytes;
 };
+
+// split-M partial slabs of the weight gradient: one per >= 1024 rows, at most NERF_BF16_MAX_SPLITS (128) — the fused
+// backward runs two workgroups per split, so 128 splits fill the 256 CUs in one round (256 splits took two rounds and
+// doubled the slab traffic: 526 MB of partials per fine-net backward).  The env override is read per call (A/B runs;
+// the workspace query and the kernels must see the same value).
+int bf16_splits(int64_t Mp) {
+  int mx = 128;
+  if (const char* e = getenv("NERF_BF16_MAX_SPLITS")) mx = atoi(e) > 0 ? atoi(e) : 128;
+  int64_t sp = Mp / 1024;
+  return (int)(sp < 1 ? 1 : (sp > mx ? mx : sp));
+}
 
 WSB carve_b(void* base, int64_t M, int training) {
   WSB w{};
@@ -71,15 +84,10 @@ WSB carve_b(void* base, int64_t M, int training) {
     w.dCIN = (float*)take(Mp * 32 * 4);
     w.WTb = (nerf_bf16*)take(WTB_ELEMS * 2);
     w.WTf = (nerf_bf16*)take(7 * nerf_bwd::WT_LAYER * 2);
-#ifndef NERF_BF16_SPLIT_ROWS
-#define NERF_BF16_SPLIT_ROWS 2048
-#endif
-    {
-      int64_t sp = Mp / NERF_BF16_SPLIT_ROWS;
-      w.S = (int)(sp < 1 ? 1 : (sp > 256 ? 256 : sp));
-    }
+    w.S = bf16_splits(Mp);
     w.rps = round_up(nerf_cdiv(Mp, w.S), 64);  // whole slabs for every wgrad MR
     w.partial = (float*)take((int64_t)w.S * L.total * 4);
+    w.partial2 = (float*)take((int64_t)w.S * (L.total - L.off[16]) * 4);  // second-half tail sums (fused backward)
   }
   w.bytes = (int64_t)(p - (char*)base);
   return w;
@@ -375,6 +383,66 @@ int fused_forward(const float* w, const float* x_d, int64_t M, float* rgb_sigma,
   return nerf_launch_status();
 }
 
+// The fused bf16 backward: ONE tail launch (mlp_bf16_tail.hpp: head-output derivatives, colour branch, head dgrad +
+// wgrad -> dZ7), ONE launch per 256-wide trunk layer 7..1 (mlp_bf16_bwd.hpp: input + weight gradient), the narrow
+// wgrads of trunk.0 and of trunk.4's encoding columns, then one deterministic split reduce (the tail's second-half
+// sums added after the slab terms).
+int fused_backward(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, const WSB& W,
+                   hipEvent_t* ev, hipStream_t st) {
+  const Layout& L = layout();
+  const int64_t Mp = W.Mp;
+  if (W.rps % nerf_bwd::TR) return NERF_E_ARG;
+  const int S8 = (W.S + 7) / 8 * 8;
+  nerf_tail::TailArgs T{};
+  T.w = w; T.g = d_rgb_sigma; T.O3 = W.O3; T.O16 = W.O16; T.Y7 = W.Y[7]; T.C0 = W.C0; T.CIN = W.CIN;
+  T.dZ7 = W.dA; T.partial = W.partial; T.partial2 = W.partial2;
+  T.slab = L.total; T.off16 = L.off[16]; T.cslab = L.total - L.off[16];
+  T.off17 = L.off[17]; T.off18 = L.off[18]; T.off19 = L.off[19]; T.off20 = L.off[20]; T.off21 = L.off[21];
+  T.rps = W.rps; T.M = M; T.Mp = Mp; T.S = W.S;
+  if (ev) (void)hipEventRecord(ev[2], st);
+  nerf_tail::bwd_tail_bf16_kernel<<<2 * S8, 768, 0, st>>>(T);
+  if (ev) (void)hipEventRecord(ev[3], st);
+  nerf_bf16* dcur = W.dA;
+  nerf_bf16* dnext = W.dB;
+  nerf_bwd::WTSrc src{};
+  for (int i = 1; i < 8; ++i) {
+    src.off[i - 1] = L.off[2 * i];
+    src.ld[i - 1] = KPAD[i];
+  }
+  nerf_bwd::wt_pack_kernel<<<(unsigned)nerf_cdiv(7 * nerf_bwd::WT_LAYER / 8, 256), 256, 0, st>>>(w, W.WTf, src);
+  for (int i = 7; i >= 1; --i) {
+    nerf_bwd::LayerArgs A{};
+    A.G = dcur;
+    A.X = (i == 4) ? W.X3E : W.Y[i - 1];
+    A.ldx = (i == 4 || i - 1 == 3) ? 320 : 256;
+    A.WT = W.WTf + (int64_t)(i - 1) * nerf_bwd::WT_LAYER;
+    A.D = dnext;
+    A.P = W.partial + L.off[2 * i];
+    A.Pb = W.partial + L.off[2 * i + 1];
+    A.ldp = L.cols[2 * i];
+    A.slab = L.total;
+    A.rps = W.rps;
+    A.Mp = Mp;
+    A.S = W.S;
+    if (ev) (void)hipEventRecord(ev[4 * i], st);
+    nerf_bwd::bwd_layer_bf16_kernel<<<2 * S8, 768, 0, st>>>(A);
+    if (ev) {
+      (void)hipEventRecord(ev[4 * i + 1], st);
+      (void)hipEventRecord(ev[4 * i + 2], st);
+      (void)hipEventRecord(ev[4 * i + 3], st);
+    }
+    if (i == 4) TRY(narrowb(dcur, 256, W.X3E + 256, 320, A.P + 256, A.ldp, nullptr, L.total, W, 256, st));
+    nerf_bf16* t = dcur; dcur = dnext; dnext = t;
+  }
+  if (ev) (void)hipEventRecord(ev[0], st);
+  TRY(wgradb(dcur, 256, W.X3E + 256, 320, 0, W, 256, KPAD[0], st));
+  if (ev) (void)hipEventRecord(ev[1], st);
+  const int64_t n4 = L.total / 4;
+  reduce_splits2_kernel<<<(unsigned)nerf_cdiv(n4, 256), 256, 0, st>>>(W.partial, L.total, W.S, d_w, n4, accumulate,
+                                                                      W.partial2, L.total - L.off[16], L.off[16] / 4);
+  return nerf_launch_status();
+}
+
 extern "C" int64_t nerf_mlp_workspace_bytes_bf16(int64_t M, int training) {
   if (M < 0) return -1;
   return carve_b(nullptr, M, training).bytes + 256;
@@ -432,6 +500,7 @@ extern "C" int nerf_mlp_bwd_bf16(const float* w, int64_t M, const float* d_rgb_s
   const int64_t Mp = W.Mp;
   auto Wt = [&](int t) { return w + L.off[t]; };
 
+  if (fused_bwd_enabled()) return fused_backward(w, M, d_rgb_sigma, d_w, accumulate, W, ev, st);
   // bf16 transposed weights for the input-gradient GEMMs (the bf16 forward copy W.Wb is reused for nothing
   // here: the backward GEMMs contract over the output dimension)
   nerf_bf16* T = W.WTb;
@@ -463,48 +532,6 @@ extern "C" int nerf_mlp_bwd_bf16(const float* w, int64_t M, const float* d_rgb_s
   TRY((ntb<EPI_MASK, 1>(W.dO16, 32, Wht, 32, nullptr, dcur, 256, W.MB[7], nullptr, Mp, 256, 32, st)));
   if (ev) (void)hipEventRecord(ev[3], st);
   TRY(wgradb(W.dO16, 32, W.Y[7], 256, 16, W, 32, 256, st));
-  if (fused_bwd_enabled()) {
-    // trunk.7 .. trunk.1: one fused launch per layer (mlp_bf16_bwd.hpp); trunk.0 and the encoding columns of
-    // trunk.4 (no input gradient) stay on the narrow wgrad kernel
-    nerf_bwd::WTSrc src{};
-    for (int i = 1; i < 8; ++i) {
-      src.off[i - 1] = L.off[2 * i];
-      src.ld[i - 1] = KPAD[i];
-    }
-    nerf_bwd::wt_pack_kernel<<<(unsigned)nerf_cdiv(7 * nerf_bwd::WT_LAYER / 8, 256), 256, 0, st>>>(w, W.WTf, src);
-    const int S8 = (W.S + 7) / 8 * 8;
-    for (int i = 7; i >= 1; --i) {
-      nerf_bwd::LayerArgs A{};
-      A.G = dcur;
-      A.X = (i == 4) ? W.X3E : W.Y[i - 1];
-      A.ldx = (i == 4 || i - 1 == 3) ? 320 : 256;
-      A.WT = W.WTf + (int64_t)(i - 1) * nerf_bwd::WT_LAYER;
-      A.D = dnext;
-      A.P = W.partial + L.off[2 * i];
-      A.Pb = W.partial + L.off[2 * i + 1];
-      A.ldp = L.cols[2 * i];
-      A.slab = L.total;
-      A.rps = W.rps;
-      A.Mp = Mp;
-      A.S = W.S;
-      if (A.rps % nerf_bwd::TR) return NERF_E_ARG;
-      if (ev) (void)hipEventRecord(ev[4 * i], st);
-      nerf_bwd::bwd_layer_bf16_kernel<<<2 * S8, 768, 0, st>>>(A);
-      if (ev) {
-        (void)hipEventRecord(ev[4 * i + 1], st);
-        (void)hipEventRecord(ev[4 * i + 2], st);
-        (void)hipEventRecord(ev[4 * i + 3], st);
-      }
-      if (i == 4) TRY(narrowb(dcur, 256, W.X3E + 256, 320, A.P + 256, A.ldp, nullptr, L.total, W, 256, st));
-      nerf_bf16* t = dcur; dcur = dnext; dnext = t;
-    }
-    if (ev) (void)hipEventRecord(ev[0], st);
-    TRY(wgradb(dcur, 256, W.X3E + 256, 320, 0, W, 256, KPAD[0], st));
-    if (ev) (void)hipEventRecord(ev[1], st);
-    const int64_t n4 = L.total / 4;
-    reduce_splits_kernel<<<(unsigned)nerf_cdiv(n4, 256), 256, 0, st>>>(W.partial, L.total, W.S, d_w, n4, accumulate);
-    return nerf_launch_status();
-  }
   // trunk
   for (int i = 7; i >= 0; --i) {
     const nerf_bf16* X = (i == 0) ? W.X3E + 256 : (i == 4 ? W.X3E : W.Y[i - 1]);

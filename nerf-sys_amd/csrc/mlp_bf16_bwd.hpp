@@ -191,6 +191,9 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, char* lds, int s
   // it covers through "+v" so no MFMA can be hoisted above it, and sched_barrier fences keep the stages in order.
   for (int t = 0; t < nT; ++t) {
     raw_barrier();  // T_t: tile t is in stage t % 2; every wave is done with tile t - 1
+#ifdef NERF_EXP_BWD_NOCOMP  // timing experiment: the io stream alone (results are garbage)
+    if (t >= 0) continue;
+#endif
     const uint32_t Lb = lbase + (uint32_t)((t % NSTG) * STB);
     uint32_t gat[2][4], xat[2];
 #pragma unroll
@@ -276,7 +279,11 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, char* lds, int s
       // this lane now holds columns 16 pr + 8 lh .. + 7 of the block
       const uint4 xv = __builtin_bit_cast(uint4, xm[pr]);
       const uint4 o = make_uint4(relu_mask2(x.x, xv.x), relu_mask2(x.y, xv.y), relu_mask2(y.x, xv.z), relu_mask2(y.y, xv.w));
+#ifndef NERF_EXP_BWD_NOSTORE
       *reinterpret_cast<uint4*>(Dt + 16 * pr) = o;
+#else
+      if (o.x == 0x12345678u && o.y == 0x9abcdef0u) *reinterpret_cast<uint4*>(Dt + 16 * pr) = o;
+#endif
     }
     SCHED_FENCE();
   }
@@ -315,6 +322,9 @@ struct IoSet {
   }
 };
 __device__ __forceinline__ void io_load(IoSet& S, const LayerArgs& A, int64_t m0, int h, int j, int lane) {
+#ifdef NERF_EXP_BWD_NOIO  // timing experiment: compute-side throughput alone (results are garbage)
+  if (m0 >= 0) return;
+#endif
   const nerf_bf16* g = A.G + (m0 + 16 * j + (lane >> 5)) * 256 + 8 * (lane & 31);
   const nerf_bf16* x = A.X + (m0 + 16 * j + (lane >> 4)) * (int64_t)A.ldx + 128 * h + 8 * (lane & 15);
   static_for<0, 8>([&](auto I) {

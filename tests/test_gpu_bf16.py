@@ -136,10 +136,11 @@ def test_fused_forward_matches_layered(K, wpk, monkeypatch):
 @pytest.mark.parametrize("M", [1, 5000, 40001, 786432])
 def test_fused_backward_matches_layered(K, wpk, monkeypatch, M):
     """The fused per-layer bf16 backward (mlp_bf16_bwd.hpp: input + weight gradient of a trunk layer in one launch,
-    ReLU mask from the saved input) against the layered dgrad / wgrad launches (NERF_BF16_FUSED_BWD=0): the same
-    bf16 operands, the same MFMA k order and the same split-M slabs, so every weight gradient is BITWISE equal; the
-    trunk.1-7 bias gradients are the same fp32 column sums in another fixed order (rows summed by the io waves that
-    stage them), equal to 2e-6 of their scale, and bitwise reproducible run to run.
+    ReLU mask from the saved input; the head / colour "tail" in one launch, mlp_bf16_tail.hpp) against the layered
+    launches (NERF_BF16_FUSED_BWD=0): the same bf16 operands, rounding points and MFMA k order, so dZ7 and every trunk
+    weight gradient are BITWISE equal; the trunk biases (column sums by the io waves that stage the rows) and the
+    head / colour sums (each split in two row halves) are the same fp32 terms in another fixed order: within 1e-5 of
+    their scale, and bitwise reproducible run to run.
     Sizes: one row; a ragged tile; 19 splits (not a multiple of the 8-split block pairing: idle pairs exit); the
     C2 fine-net size (256 splits of 3,072 rows, 512 workgroups)."""
     from nerf_amd.vanilla import PackedLayout
@@ -156,11 +157,10 @@ def test_fused_backward_matches_layered(K, wpk, monkeypatch, M):
     assert torch.isfinite(res["1"]).all()
     assert torch.equal(res["1"], res["1b"]), "fused backward not reproducible"
     a, b = PackedLayout.get().unpack(res["1"]), PackedLayout.get().unpack(res["0"])
-    fused_bias = {f"trunk.{i}.linear.bias" for i in range(1, 8)}
     for n in b:
-        if n in fused_bias:
+        if n.startswith("trunk.") and n.endswith(".weight"):
+            assert torch.equal(a[n], b[n]), f"{n}: fused != layered at M={M}, max {float((a[n] - b[n]).abs().max()):.3e}"
+        else:  # trunk biases (io-wave column sums), head / colour tensors (split-half sums): same terms, other order
             scale = max(float(b[n].abs().max()), 1e-30)
             err = float((a[n] - b[n]).abs().max())
-            assert err <= 2e-6 * scale, f"{n}: fused vs layered bias {err:.3e} (scale {scale:.3e}) at M={M}"
-        else:
-            assert torch.equal(a[n], b[n]), f"{n}: fused != layered at M={M}, max {float((a[n] - b[n]).abs().max()):.3e}"
+            assert err <= 1e-5 * scale, f"{n}: fused vs layered {err:.3e} (scale {scale:.3e}) at M={M}"
