@@ -29,6 +29,16 @@ __device__ __forceinline__ uint32_t nerf_pack_bf16x2(float a, float b) {
   const nerf_bf16 x = (nerf_bf16)a, y = (nerf_bf16)b;  // v_cvt_pk_bf16_f32, round to nearest even
   return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
 }
+// sin / cos of the frequency encoding for the bf16 path, whose encoding is rounded to bf16 (8-bit mantissa): the
+// argument is reduced to [-1/2, 1/2] revolutions and fed to v_sin_f32 / v_cos_f32 (absolute error ~ |x| 6e-8 rad from
+// the fp32 product, 5e-5 rad at the top band of |x| = 1.5, far below the 2e-3 bf16 rounding of the result).  The fp32
+// path keeps the libm sincosf (pinned to the reference's torch.sin / torch.cos at 1e-5).
+__device__ __forceinline__ void pe_sincos_bf16(float x, float* s, float* c) {
+  const float r = x * 0.15915494309189535f;
+  const float f = r - rintf(r);
+  *s = __builtin_amdgcn_sinf(f);
+  *c = __builtin_amdgcn_cosf(f);
+}
 __device__ __forceinline__ float nerf_bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float nerf_bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 

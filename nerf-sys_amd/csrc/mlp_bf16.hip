@@ -24,6 +24,8 @@
 namespace {
 using namespace nerf_mlp;
 
+// narrow slab of the fused backward: trunk.0 W [256][64] | trunk.4 W[:, 256:320] [256][64] | trunk.0 b [256]
+constexpr int64_t NPS = 2 * 256 * 64 + 256;
 constexpr int64_t WTB_ELEMS = 7 * 65536 + 256 * 32 + 128 * 32 + 32 * 128;
 
 struct WSB {
@@ -32,9 +34,9 @@ struct WSB {
   float *O16, *O3;
   uint32_t *MB[8], *MC0;
   nerf_bf16 *dA, *dB, *dO16, *dO3, *dC0, *WTb, *WTf;
-  float *dCIN, *partial, *partial2;
-  int S;
-  int64_t rps;
+  float *dCIN, *partial, *partial2, *np;
+  int S, S2;
+  int64_t rps, rps2;
   int64_t bytes;
 };
 
@@ -88,6 +90,15 @@ WSB carve_b(void* base, int64_t M, int training) {
     w.rps = round_up(nerf_cdiv(Mp, w.S), 64);  // whole slabs for every wgrad MR
     w.partial = (float*)take((int64_t)w.S * L.total * 4);
     w.partial2 = (float*)take((int64_t)w.S * (L.total - L.off[16]) * 4);  // second-half tail sums (fused backward)
+    // the narrow weight gradients of the fused backward (trunk.0, trunk.4's encoding columns) over S2 = 4 S sub-splits
+    {  // NERF_BF16_NARROW_MUL (A/B runs): sub-splits per split
+      int mul = 2;
+      if (const char* e = getenv("NERF_BF16_NARROW_MUL")) mul = atoi(e) > 0 ? atoi(e) : 2;
+      int64_t s2 = (int64_t)mul * w.S, cap = Mp / 256;
+      w.S2 = (int)(s2 > cap ? (cap < 1 ? 1 : cap) : s2);
+      w.rps2 = round_up(nerf_cdiv(Mp, w.S2), 64);
+    }
+    w.np = (float*)take((int64_t)w.S2 * NPS * 4);
   }
   w.bytes = (int64_t)(p - (char*)base);
   return w;
@@ -150,7 +161,7 @@ __global__ void pe_xyz_bf16_kernel(const float* __restrict__ xd, int64_t M, int6
 #pragma unroll
       for (int l = 0; l < 10; ++l) {
         float s, c;
-        sincosf(x[k] * band, &s, &c);
+        pe_sincos_bf16(x[k] * band, &s, &c);
         v[3 + k * 20 + l] = c;
         v[3 + k * 20 + 10 + l] = s;
         band *= 2.0f;
@@ -185,7 +196,7 @@ __global__ void build_cin_bf16_kernel(const float* __restrict__ xd, const float*
 #pragma unroll
       for (int l = 0; l < 4; ++l) {
         float s, c;
-        sincosf(d[k] * band, &s, &c);
+        pe_sincos_bf16(d[k] * band, &s, &c);
         v[18 + k * 8 + l] = c;
         v[18 + k * 8 + 4 + l] = s;
         band *= 2.0f;
@@ -374,13 +385,51 @@ int fused_forward(const float* w, const float* x_d, int64_t M, float* rgb_sigma,
   A.ntiles = (int)(Mp / BMF);  // Mp is a multiple of 256: whole 128-row tiles
   const int grid = A.ntiles < n_cu ? A.ntiles : n_cu;  // persistent, one workgroup per CU (LDS ~87 KB)
   if (ev) (void)hipEventRecord(ev[0], st);
-  if (training)
-    mlp_fwd_fused_bf16_kernel<true><<<grid, 512, 0, st>>>(A);
+  if (training && !fused_bwd_enabled())  // the layered backward reads ReLU bitmasks
+    mlp_fwd_fused_bf16_kernel<true, true><<<grid, 512, 0, st>>>(A);
+  else if (training)
+    mlp_fwd_fused_bf16_kernel<true, false><<<grid, 512, 0, st>>>(A);
   else
-    mlp_fwd_fused_bf16_kernel<false><<<grid, 512, 0, st>>>(A);
+    mlp_fwd_fused_bf16_kernel<false, false><<<grid, 512, 0, st>>>(A);
   if (ev)
     for (int i = 1; i < 16; ++i) (void)hipEventRecord(ev[i], st);  // ev[0] -> ev[1] brackets the fused launch
   return nerf_launch_status();
+}
+
+// Final reduce of the fused backward (fixed order, bitwise reproducible): element e of the packed gradient =
+//   trunk.0 W / b and trunk.4 W[:, 256:320]  sum over the S2 narrow sub-slabs (np);
+//   everything else                          sum over the S split slabs, plus (e >= off16: head / colour) the S
+//                                            second-half tail slabs after them.
+__global__ void reduce_fused_bf16_kernel(const float* __restrict__ partial, int64_t slab, int S,
+                                         const float* __restrict__ partial2, int64_t slab2, int64_t off16,
+                                         const float* __restrict__ np, int S2, float* __restrict__ dst, int64_t n4,
+                                         int accumulate, int64_t off0, int64_t off1, int64_t off8) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const int64_t e = 4 * i;
+  float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  int64_t nofs = -1;  // offset in the narrow slab, or -1
+  if (e >= off0 && e < off0 + 256 * 64) nofs = e - off0;
+  else if (e >= off1 && e < off1 + 256) nofs = 32768 + (e - off1);
+  else if (e >= off8 && e < off8 + 256 * 320 && (e - off8) % 320 >= 256) {
+    const int64_t n = (e - off8) / 320, k = (e - off8) % 320 - 256;
+    nofs = 16384 + n * 64 + k;
+  }
+  auto add = [&](const float* base, int64_t stride, int count) {
+    const float4* p = reinterpret_cast<const float4*>(base);
+#pragma unroll 16
+    for (int s = 0; s < count; ++s) {
+      const float4 v = p[s * (stride / 4)];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  };
+  if (nofs >= 0) {
+    add(np + nofs, NPS, S2);
+  } else {
+    add(partial + e, slab, S);
+    if (e >= off16) add(partial2 + (e - off16), slab2, S);
+  }
+  reinterpret_cast<float4*>(dst)[i] = a;
 }
 
 // The fused bf16 backward: ONE tail launch (mlp_bf16_tail.hpp: head-output derivatives, colour branch, head dgrad +
@@ -404,12 +453,11 @@ int fused_backward(const float* w, int64_t M, const float* d_rgb_sigma, float* d
   if (ev) (void)hipEventRecord(ev[3], st);
   nerf_bf16* dcur = W.dA;
   nerf_bf16* dnext = W.dB;
-  nerf_bwd::WTSrc src{};
-  for (int i = 1; i < 8; ++i) {
-    src.off[i - 1] = L.off[2 * i];
-    src.ld[i - 1] = KPAD[i];
+  {  // W_i^T images (bf16 [k][n], first 256 input columns) through 32 x 32 LDS tiles: coalesced on both sides
+    TJobsB jobs{};
+    for (int i = 1; i < 8; ++i) jobs.j[i - 1] = TJobB{w + L.off[2 * i], W.WTf + (int64_t)(i - 1) * nerf_bwd::WT_LAYER, 256, 256, KPAD[i]};
+    transpose_bf16_kernel<<<dim3(8, 8, 7), 256, 0, st>>>(jobs);
   }
-  nerf_bwd::wt_pack_kernel<<<(unsigned)nerf_cdiv(7 * nerf_bwd::WT_LAYER / 8, 256), 256, 0, st>>>(w, W.WTf, src);
   for (int i = 7; i >= 1; --i) {
     nerf_bwd::LayerArgs A{};
     A.G = dcur;
@@ -431,15 +479,19 @@ int fused_backward(const float* w, int64_t M, const float* d_rgb_sigma, float* d
       (void)hipEventRecord(ev[4 * i + 2], st);
       (void)hipEventRecord(ev[4 * i + 3], st);
     }
-    if (i == 4) TRY(narrowb(dcur, 256, W.X3E + 256, 320, A.P + 256, A.ldp, nullptr, L.total, W, 256, st));
+    if (i == 4)  // the encoding columns of trunk.4 (no input gradient): narrow wgrad over the S2 sub-splits
+      gemm_wgrad_bf16_kernel<128, 64, 2, 64><<<2 * W.S2, 256, 0, st>>>(dcur, 256, W.X3E + 256, 320, W.np + 16384, 64,
+                                                                      nullptr, NPS, W.rps2, Mp, 1, 2);
     nerf_bf16* t = dcur; dcur = dnext; dnext = t;
   }
   if (ev) (void)hipEventRecord(ev[0], st);
-  TRY(wgradb(dcur, 256, W.X3E + 256, 320, 0, W, 256, KPAD[0], st));
+  gemm_wgrad_bf16_kernel<128, 64, 2, 64><<<2 * W.S2, 256, 0, st>>>(dcur, 256, W.X3E + 256, 320, W.np, 64, W.np + 32768,
+                                                                  NPS, W.rps2, Mp, 1, 2);
   if (ev) (void)hipEventRecord(ev[1], st);
   const int64_t n4 = L.total / 4;
-  reduce_splits2_kernel<<<(unsigned)nerf_cdiv(n4, 256), 256, 0, st>>>(W.partial, L.total, W.S, d_w, n4, accumulate,
-                                                                      W.partial2, L.total - L.off[16], L.off[16] / 4);
+  reduce_fused_bf16_kernel<<<(unsigned)nerf_cdiv(n4, 256), 256, 0, st>>>(
+      W.partial, L.total, W.S, W.partial2, L.total - L.off[16], L.off[16], W.np, W.S2, d_w, n4, accumulate, L.off[0],
+      L.off[1], L.off[8]);
   return nerf_launch_status();
 }
 

@@ -59,25 +59,8 @@ constexpr int WT_LAYER = 256 * 256;     // bf16 elements of one layer's W^T imag
 __device__ __forceinline__ int swz(int r) { return 4 * (r & 3) + ((r >> 2) & 3); }
 
 // W_i^T of trunk layers i = 1..7 (image i - 1), row-major bf16: WT[k][n] = W_i[n][k] for k < 256 (trunk.4: its first
-// 256 input columns, the trunk.3 output; the encoding columns need no input gradient).
-struct WTSrc {
-  int64_t off[7];  // fp32 offset of W_i (i = 1..7) in the packed layout
-  int ld[7];       // its row pitch (KPAD[i])
-};
-__global__ void wt_pack_kernel(const float* __restrict__ w, nerf_bf16* __restrict__ wt, WTSrc S) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 8 consecutive n of one k
-  if (c >= 7 * WT_LAYER / 8) return;
-  const int img = (int)(c / (WT_LAYER / 8));
-  const int r = (int)(c - (int64_t)img * (WT_LAYER / 8));
-  const int k = r >> 5, n0 = 8 * (r & 31);
-  const float* src = w + S.off[img] + (int64_t)n0 * S.ld[img] + k;
-  float v[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = src[(int64_t)j * S.ld[img]];
-  *reinterpret_cast<uint4*>(wt + c * 8) = make_uint4(nerf_pack_bf16x2(v[0], v[1]), nerf_pack_bf16x2(v[2], v[3]),
-                                                     nerf_pack_bf16x2(v[4], v[5]), nerf_pack_bf16x2(v[6], v[7]));
-}
-
+// 256 input columns, the trunk.3 output; the encoding columns need no input gradient) — mlp_bf16.hip builds it with the
+// tiled transpose kernel.
 struct LayerArgs {
   const nerf_bf16* G;    // dZ_i [Mp][256]
   const nerf_bf16* X;    // X_i, row pitch ldx (cols 0..255 used)

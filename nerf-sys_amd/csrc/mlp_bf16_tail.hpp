@@ -60,17 +60,16 @@ struct TailArgs {
   int S;
 };
 
-// transposing-read fragment (A = G^T or B = X^T of a weight gradient): 16-row k-step ks, 32-column block cb of a tile
-// whose chunk addresses come from AD(row, chunk); lane geometry as gemm_wgrad_bf16
+// transposing-read fragments (A = G^T or B = X^T of a weight gradient; lane geometry as gemm_wgrad_bf16) by inline asm:
+// two per-lane base addresses (rows +0 / +4 of k-step 0) and the k-step as an immediate offset (the intrinsic got no
+// offset folding: one address VGPR per read, which spilled here); the caller waits lgkmcnt(0) and passes the
+// fragments through "+v" before the MFMAs
 template <typename AD>
-__device__ __forceinline__ nerf_bf16x8 trf(const char* L, AD ad, int ks, int cb, int lane) {
+__device__ __forceinline__ void tr_bases(uint32_t base, AD ad, int cb, int lane, uint32_t& b0, uint32_t& b1) {
   const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int r = 16 * ks + 8 * (grp >> 1) + q, c = 4 * cb + 2 * (grp & 1) + (p >> 1);
-  typedef __attribute__((address_space(3))) nerf_s16x4 lds_s16x4;
-  const nerf_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(L + ad(r, c) + 8 * (p & 1)));
-  const nerf_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(L + ad(r + 4, c) + 8 * (p & 1)));
-  const short v8 __attribute__((ext_vector_type(8))) = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(nerf_bf16x8, v8);
+  const int r = 8 * (grp >> 1) + q, c = 4 * cb + 2 * (grp & 1) + (p >> 1);
+  b0 = base + (uint32_t)(ad(r, c) + 8 * (p & 1));
+  b1 = base + (uint32_t)(ad(r + 4, c) + 8 * (p & 1));
 }
 __device__ __forceinline__ nerf_bf16x8 ld16(const char* p) { return *reinterpret_cast<const nerf_bf16x8*>(p); }
 
@@ -119,10 +118,20 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
 #pragma unroll
   for (int r = 0; r < 16; ++r) ac1[r] = ac0[r] = ahd[r] = 0.f;
   float b1 = 0.f, b0 = 0.f, bh = 0.f;
+  // transposing-read bases (k-step 0): work tiles absolute, stage tiles relative to the stage (+ Lo per tile)
+  const uint32_t lb = (uint32_t)(uintptr_t)lds;
+  uint32_t t3a0, t3a1, tca0, tca1, tda0, tda1, tia0, tia1, t16a0, t16a1, tya0, tya1;
+  tr_bases(lb, a3, 0, lane, t3a0, t3a1);
+  tr_bases(lb, ac, w & 3, lane, tca0, tca1);
+  tr_bases(lb, adc, w >> 1, lane, tda0, tda1);
+  tr_bases(lb, ai, w & 1, lane, tia0, tia1);
+  tr_bases(lb, a16, 0, lane, t16a0, t16a1);
+  tr_bases(lb, ay, w, lane, tya0, tya1);
 
   for (int t = 0; t < nT; ++t) {
     raw_barrier();  // T_t
     const char* L = lds + (t % NSTG) * STB;
+    const uint32_t Lo = (uint32_t)((t % NSTG) * STB);
     // ---- P0: head-output derivatives of the tile's rows (wave 0, lane = row)
     if (w == 0) {
       const int64_t m = r0 + (int64_t)t * TR + lane;
@@ -159,14 +168,21 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
       }
     }
     if (w < 4) {
+      nerf_bf16x8 ga[4], gb[4];
+      static_for<0, 4>([&](auto KS) {
+        constexpr int ks = decltype(KS)::value;
+        ga[ks] = nerf_bwd::tr_frag_asm<1024 * ks>(t3a0, t3a1);
+        gb[ks] = nerf_bwd::tr_frag_asm<4096 * ks>(tca0 + Lo, tca1 + Lo);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ga[0]), "+v"(ga[1]), "+v"(ga[2]), "+v"(ga[3]), "+v"(gb[0]), "+v"(gb[1]),
+                   "+v"(gb[2]), "+v"(gb[3])::"memory");
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const nerf_bf16x8 ga = trf(lds, a3, ks, 0, lane);
         if (w == 0) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) b1 += (float)ga[j];
+          for (int j = 0; j < 8; ++j) b1 += (float)ga[ks][j];
         }
-        ac1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, trf(L, ac, ks, w, lane), ac1, 0, 0, 0);
+        ac1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ks], gb[ks], ac1, 0, 0, 0);
       }
     }
     wait_lds();
@@ -191,15 +207,21 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
       *reinterpret_cast<uint4*>(lds + a16(row, lh)) = v;
     }
     {
-      const int nb = w >> 1, kb = w & 1;
+      nerf_bf16x8 ga[4], gb[4];
+      static_for<0, 4>([&](auto KS) {
+        constexpr int ks = decltype(KS)::value;
+        ga[ks] = nerf_bwd::tr_frag_asm<4096 * ks>(tda0, tda1);
+        gb[ks] = nerf_bwd::tr_frag_asm<2048 * ks>(tia0 + Lo, tia1 + Lo);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ga[0]), "+v"(ga[1]), "+v"(ga[2]), "+v"(ga[3]), "+v"(gb[0]), "+v"(gb[1]),
+                   "+v"(gb[2]), "+v"(gb[3])::"memory");
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const nerf_bf16x8 ga = trf(lds, adc, ks, nb, lane);
-        if (kb == 0) {
+        if ((w & 1) == 0) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) b0 += (float)ga[j];
+          for (int j = 0; j < 8; ++j) b0 += (float)ga[ks][j];
         }
-        ac0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, trf(L, ai, ks, kb, lane), ac0, 0, 0, 0);
+        ac0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ks], gb[ks], ac0, 0, 0, 0);
       }
     }
     wait_lds();
@@ -221,14 +243,21 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
         for (int pr = 0; pr < 2; ++pr)
           *reinterpret_cast<uint4*>(dst + 16 * pr) = mask4(o[pr], *reinterpret_cast<const uint4*>(L + ay(row, 4 * w + 2 * pr + lh)));
       }
+      nerf_bf16x8 ga[4], gb[4];
+      static_for<0, 4>([&](auto KS) {
+        constexpr int ks = decltype(KS)::value;
+        ga[ks] = nerf_bwd::tr_frag_asm<1024 * ks>(t16a0, t16a1);
+        gb[ks] = nerf_bwd::tr_frag_asm<8192 * ks>(tya0 + Lo, tya1 + Lo);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ga[0]), "+v"(ga[1]), "+v"(ga[2]), "+v"(ga[3]), "+v"(gb[0]), "+v"(gb[1]),
+                   "+v"(gb[2]), "+v"(gb[3])::"memory");
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const nerf_bf16x8 ga = trf(lds, a16, ks, 0, lane);
         if (w == 0) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) bh += (float)ga[j];
+          for (int j = 0; j < 8; ++j) bh += (float)ga[ks][j];
         }
-        ahd = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, trf(L, ay, ks, w, lane), ahd, 0, 0, 0);
+        ahd = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ks], gb[ks], ahd, 0, 0, 0);
       }
     }
   }
@@ -283,10 +312,12 @@ __device__ __forceinline__ void tail_load(TailSet& S, const TailArgs& A, int64_t
   static_for<0, 8>([&](auto I) { S.template at<decltype(I)::value>() = *reinterpret_cast<const u32x4*>(y + 512 * decltype(I)::value); });
   static_for<0, 4>([&](auto I) { S.template at<8 + decltype(I)::value>() = *reinterpret_cast<const u32x4*>(c + 512 * decltype(I)::value); });
   static_for<0, 2>([&](auto I) { S.template at<12 + decltype(I)::value>() = *reinterpret_cast<const u32x4*>(x + 512 * decltype(I)::value); });
+  // one unconditional 16-B load per lane for every io wave (a conditional load left the compiler unable to count the
+  // set's loads: it drained vmcnt(0) before the stores); g is [M][4]: rows past M read row M - 1 and are zeroed
   const int64_t m = m0 + lane;
-  if (j == 0) S.v14 = m < A.M ? *reinterpret_cast<const u32x4*>(A.g + m * 4) : u32x4{0u, 0u, 0u, 0u};
-  if (j == 1) S.v14 = *reinterpret_cast<const u32x4*>(A.O3 + m * 32);
-  if (j == 2) S.v14 = u32x4{__float_as_uint(A.O16[m * 32]), 0u, 0u, 0u};
+  const float* pv = j == 0 ? A.g + (m < A.M ? m : A.M - 1) * 4 : (j == 1 ? A.O3 : A.O16) + m * 32;
+  S.v14 = *reinterpret_cast<const u32x4*>(pv);
+  if (j == 0 && m >= A.M) S.v14 = u32x4{0u, 0u, 0u, 0u};
 }
 __device__ __forceinline__ void tail_store(TailSet& S, char* st, int j, int lane) {
   static_for<0, 8>([&](auto I) {

@@ -137,10 +137,11 @@ def test_fused_forward_matches_layered(K, wpk, monkeypatch):
 def test_fused_backward_matches_layered(K, wpk, monkeypatch, M):
     """The fused per-layer bf16 backward (mlp_bf16_bwd.hpp: input + weight gradient of a trunk layer in one launch,
     ReLU mask from the saved input; the head / colour "tail" in one launch, mlp_bf16_tail.hpp) against the layered
-    launches (NERF_BF16_FUSED_BWD=0): the same bf16 operands, rounding points and MFMA k order, so dZ7 and every trunk
-    weight gradient are BITWISE equal; the trunk biases (column sums by the io waves that stage the rows) and the
-    head / colour sums (each split in two row halves) are the same fp32 terms in another fixed order: within 1e-5 of
-    their scale, and bitwise reproducible run to run.
+    launches (NERF_BF16_FUSED_BWD=0): the same bf16 operands, rounding points and MFMA k order, so dZ7 and the
+    256-wide trunk weight gradients are BITWISE equal; the trunk biases (column sums by the io waves that stage the
+    rows), the head / colour sums (each split in two row halves) and the narrow trunk.0 / trunk.4-encoding sums (4x
+    finer sub-splits) are the same fp32 terms in another fixed order: within 1e-5 of their scale, and bitwise
+    reproducible run to run.
     Sizes: one row; a ragged tile; 19 splits (not a multiple of the 8-split block pairing: idle pairs exit); the
     C2 fine-net size (256 splits of 3,072 rows, 512 workgroups)."""
     from nerf_amd.vanilla import PackedLayout
@@ -148,6 +149,7 @@ def test_fused_backward_matches_layered(K, wpk, monkeypatch, M):
     g = torch.Generator().manual_seed(23)
     gup = (torch.randn(M, 4, generator=g) * 1e-3).to(DEV)
     ws = K.mlp_workspace(M, True, DEV, "bf16")
+    monkeypatch.setenv("NERF_BF16_FUSED_BWD", "0")  # a forward for the layered backward also writes its ReLU bitmasks
     K.mlp_fwd(wpk, x, ws, True, precision="bf16")
     res = {}
     for mode in ("0", "1", "1b"):
@@ -157,10 +159,15 @@ def test_fused_backward_matches_layered(K, wpk, monkeypatch, M):
     assert torch.isfinite(res["1"]).all()
     assert torch.equal(res["1"], res["1b"]), "fused backward not reproducible"
     a, b = PackedLayout.get().unpack(res["1"]), PackedLayout.get().unpack(res["0"])
+    exact = {f"trunk.{i}.linear.weight" for i in (1, 2, 3, 5, 6, 7)}
     for n in b:
-        if n.startswith("trunk.") and n.endswith(".weight"):
-            assert torch.equal(a[n], b[n]), f"{n}: fused != layered at M={M}, max {float((a[n] - b[n]).abs().max()):.3e}"
-        else:  # trunk biases (io-wave column sums), head / colour tensors (split-half sums): same terms, other order
-            scale = max(float(b[n].abs().max()), 1e-30)
-            err = float((a[n] - b[n]).abs().max())
+        got, ref = a[n], b[n]
+        if n == "trunk.4.linear.weight":  # the trunk.3 columns: fused; the encoding columns: narrow sub-split wgrad
+            assert torch.equal(got[:, :256], ref[:, :256]), f"{n}[:, :256]: fused != layered at M={M}"
+            got, ref = got[:, 256:], ref[:, 256:]
+        if n in exact:
+            assert torch.equal(got, ref), f"{n}: fused != layered at M={M}, max {float((got - ref).abs().max()):.3e}"
+        else:  # same fp32 terms, another fixed summation order (io-wave column sums, split halves, sub-splits)
+            scale = max(float(ref.abs().max()), 1e-30)
+            err = float((got - ref).abs().max())
             assert err <= 1e-5 * scale, f"{n}: fused vs layered {err:.3e} (scale {scale:.3e}) at M={M}"
