@@ -203,8 +203,9 @@ def roofline_bf16(tm):
       fused_bwd_layer  G (dZ_i) 512 B read + X_i 512 B read + dZ_{i-1} 512 B written = 1,536 B
                        (+ the split-M weight-gradient slabs, S x 256 KiB per launch, listed as slab_bytes)
       fused_fwd        encoding + colour-input prefill 256 B read; saved activations 7 x 512 + trunk.3 512 B,
-                       ReLU masks 256 B, colour input 128 B, colour layer 0 256 B + mask 16 B, sigma /
-                       colour-out pre-activations 20 B, rgb_sigma 16 B written = 5,044 B"""
+                       colour input 128 B, colour layer 0 256 B, sigma / colour-out pre-activations 20 B,
+                       rgb_sigma 16 B written = 4,772 B (the fused backward takes its ReLU masks from the saved
+                       activations: no bitmask words are written)"""
     M = tm["M"]
     mean = lambda xs: sum(xs) / len(xs)
     bwd_ms = mean([st[i] for st in tm["wgrad"] for i in K256])
@@ -215,7 +216,7 @@ def roofline_bf16(tm):
                             "mean_launch_ms": bwd_ms, "launches": len(K256), "bytes": 1536.0 * M,
                             "slab_bytes": S * 256 * 256 * 4.0, "flop": 2 * 2.0 * M * 256 * 256},
         "fused_fwd": {"kernel": "mlp_fwd_fused_bf16 (whole MLP forward, one persistent launch)",
-                      "mean_launch_ms": fwd_ms, "launches": 1, "bytes": 5044.0 * M, "flop": 2.0 * MAC_PER_EVAL * M},
+                      "mean_launch_ms": fwd_ms, "launches": 1, "bytes": 4772.0 * M, "flop": 2.0 * MAC_PER_EVAL * M},
     }
     for k, c in cls.items():
         ms = c["mean_launch_ms"]

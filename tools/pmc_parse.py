@@ -18,7 +18,12 @@ CLASSES = {
     "dgrad": ("gemm_nt_kernel<128, 128, 2, 2,", 0),
     "wgrad": ("gemm_wgrad_kernel<128, 128, 2,", 0),
 }
-if len(sys.argv) > 2 and sys.argv[2] == "bf16":  # bf16 MLP (configs[2]) kernel names
+if len(sys.argv) > 2 and sys.argv[2] == "bf16fused":  # the fused bf16 MLP (bench.py roofline_bf16 classes)
+    CLASSES = {
+        "fused_bwd_layer": ("bwd_layer_bf16_kernel", 0),
+        "fused_fwd": ("mlp_fwd_fused_bf16_kernel<true", 0),
+    }
+elif len(sys.argv) > 2 and sys.argv[2] == "bf16":  # layered bf16 MLP (configs[2]) kernel names
     CLASSES = {
         "fwd": ("gemm_nt_bf16_wsr_kernel<256, 128, 1, 1,", 0),
         "dgrad": ("gemm_nt_bf16_wsr_kernel<256, 128, 2, 1,", 0),
