@@ -61,6 +61,8 @@ __device__ __forceinline__ int swz(int r) { return 4 * (r & 3) + ((r >> 2) & 3);
 // W_i^T of trunk layers i = 1..7 (image i - 1), row-major bf16: WT[k][n] = W_i[n][k] for k < 256 (trunk.4: its first
 // 256 input columns, the trunk.3 output; the encoding columns need no input gradient) — mlp_bf16.hip builds it with the
 // tiled transpose kernel.
+typedef unsigned int io_u32x4 __attribute__((ext_vector_type(4)));  // a vector value (uint4 copies become memcpy)
+
 struct LayerArgs {
   const nerf_bf16* G;    // dZ_i [Mp][256]
   const nerf_bf16* X;    // X_i, row pitch ldx (cols 0..255 used)
@@ -174,9 +176,6 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, char* lds, int s
   // it covers through "+v" so no MFMA can be hoisted above it, and sched_barrier fences keep the stages in order.
   for (int t = 0; t < nT; ++t) {
     raw_barrier();  // T_t: tile t is in stage t % 2; every wave is done with tile t - 1
-#ifdef NERF_EXP_BWD_NOCOMP  // timing experiment: the io stream alone (results are garbage)
-    if (t >= 0) continue;
-#endif
     const uint32_t Lb = lbase + (uint32_t)((t % NSTG) * STB);
     uint32_t gat[2][4], xat[2];
 #pragma unroll
@@ -262,10 +261,10 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, char* lds, int s
       // this lane now holds columns 16 pr + 8 lh .. + 7 of the block
       const uint4 xv = __builtin_bit_cast(uint4, xm[pr]);
       const uint4 o = make_uint4(relu_mask2(x.x, xv.x), relu_mask2(x.y, xv.y), relu_mask2(y.x, xv.z), relu_mask2(y.y, xv.w));
-#ifndef NERF_EXP_BWD_NOSTORE
-      *reinterpret_cast<uint4*>(Dt + 16 * pr) = o;
+#ifdef NERF_EXP_BWD_NT
+      __builtin_nontemporal_store(io_u32x4{o.x, o.y, o.z, o.w}, reinterpret_cast<io_u32x4*>(Dt + 16 * pr));
 #else
-      if (o.x == 0x12345678u && o.y == 0x9abcdef0u) *reinterpret_cast<uint4*>(Dt + 16 * pr) = o;
+      *reinterpret_cast<uint4*>(Dt + 16 * pr) = o;
 #endif
     }
     SCHED_FENCE();
@@ -285,7 +284,6 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, char* lds, int s
 // 8 G pieces of 2 rows, 4 X-half pieces of 4 rows, each wave-instruction 1 KiB contiguous) -> swizzled LDS stage
 // Named members, not arrays: an array member of a set held across loop iterations stays a stack object (scratch),
 // with every load waited on before its scratch store.
-typedef unsigned int io_u32x4 __attribute__((ext_vector_type(4)));  // a vector value (uint4 copies become memcpy)
 struct IoSet {
   io_u32x4 v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11;  // 0..7: G pieces, 8..11: X-half pieces
   template <int I>
@@ -305,9 +303,6 @@ struct IoSet {
   }
 };
 __device__ __forceinline__ void io_load(IoSet& S, const LayerArgs& A, int64_t m0, int h, int j, int lane) {
-#ifdef NERF_EXP_BWD_NOIO  // timing experiment: compute-side throughput alone (results are garbage)
-  if (m0 >= 0) return;
-#endif
   const nerf_bf16* g = A.G + (m0 + 16 * j + (lane >> 5)) * 256 + 8 * (lane & 31);
   const nerf_bf16* x = A.X + (m0 + 16 * j + (lane >> 4)) * (int64_t)A.ldx + 128 * h + 8 * (lane & 15);
   static_for<0, 8>([&](auto I) {

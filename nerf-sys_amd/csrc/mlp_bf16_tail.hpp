@@ -241,7 +241,14 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
         nerf_bf16* dst = A.dZ7 + (r0 + (int64_t)t * TR + row) * 256 + 32 * w + 8 * lh;
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr)
-          *reinterpret_cast<uint4*>(dst + 16 * pr) = mask4(o[pr], *reinterpret_cast<const uint4*>(L + ay(row, 4 * w + 2 * pr + lh)));
+        {
+          const uint4 v = mask4(o[pr], *reinterpret_cast<const uint4*>(L + ay(row, 4 * w + 2 * pr + lh)));
+#ifdef NERF_EXP_BWD_NT
+          __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(dst + 16 * pr));
+#else
+          *reinterpret_cast<uint4*>(dst + 16 * pr) = v;
+#endif
+        }
       }
       nerf_bf16x8 ga[4], gb[4];
       static_for<0, 4>([&](auto KS) {
