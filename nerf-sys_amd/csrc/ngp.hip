@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <set>
+#include <type_traits>
 
 #include "mlp_common.hpp"
 
@@ -32,10 +33,12 @@
 #pragma clang fp contract(off)
 
 typedef float ngp_f32x16 __attribute__((ext_vector_type(16)));
+typedef float ngp_f32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-constexpr int NGP_ROWS = 64;
+constexpr int NGP_ROWS = 64;   // forward / density tile (32x32 MFMA blocks)
+constexpr int NGP_BROWS = 32;  // backward tile (16x16 MFMA blocks; half the LDS, so two workgroups fit per CU)
 constexpr int NGP_MAX_LAYERS = 12;
 constexpr int NGP_MAX_SB = 32;
 
@@ -110,7 +113,8 @@ bool make_plan(const NerfNgpNet& n, bool save, NgpPlan& P) {
   P.total = o;
   // LDS plan (floats)
   int s = 0;
-  auto take = [&](int ld) { int b = s; s += NGP_ROWS * ld; return b; };
+  const int rows = save ? NGP_BROWS : NGP_ROWS;
+  auto take = [&](int ld) { int b = s; s += rows * ld; return b; };
   P.enc_ld = pad32(n.in_dim) + 4;
   P.enc_buf = take(P.enc_ld);
   P.cin_ld = P.cin_kpad + 4;
@@ -122,7 +126,7 @@ bool make_plan(const NerfNgpNet& n, bool save, NgpPlan& P) {
   if (save) {
     P.g0 = take(68);
     P.g1 = take(68);
-    P.dsig = s; s += NGP_ROWS;
+    P.dsig = s; s += NGP_BROWS;
     P.sraw = -1;
     P.bsum = -1;
   } else {
@@ -144,14 +148,15 @@ bool make_plan(const NerfNgpNet& n, bool save, NgpPlan& P) {
     prev_out = L.out_buf;
     prev_ld = L.out_ld;
   }
-  // bias-gradient partials last, only when they fit (deep nets: one wave per layer sums all rows in registers)
-  if (save && (int64_t)(s + 4 * P.nl * 64) * 4 <= 160 * 1024) { P.bsum = s; s += 4 * P.nl * 64; }
+  // bias-gradient partials last, only when two workgroups still fit per CU (deep nets: one wave per layer sums all
+  // rows in registers)
+  if (save && (int64_t)(s + 4 * P.nl * 64) * 4 <= 80 * 1024) { P.bsum = s; s += 4 * P.nl * 64; }
   P.smem_floats = s;
   if ((int64_t)s * 4 > 160 * 1024) return false;
-  // weight-gradient blocks, dealt to the 4 waves: slot sb = wave + 4 j.  In the backward a layer's wgrad blocks run
-  // in the same barrier interval as its input-gradient MFMAs (wave (rb, kb) busy iff kb*32 < Kpad, Npad/2 MFMAs), so
-  // each block goes to the wave with the least work in that interval (then the fewest slots used): the critical
-  // MFMA chain of the production net drops from 352 to 288 per tile versus a layer-major deal.
+  // weight-gradient blocks (32x32, 16 MFMAs of 64 cycles per 32-row tile), dealt to the 4 waves: slot sb = wave + 4 j.
+  // A layer's wgrad blocks run in the same barrier interval as its input-gradient MFMAs (16x16 blocks: every wave
+  // owns Kpad / 32 of them, Npad / 4 MFMAs of 32 cycles each), so each block goes to the wave with the least work in
+  // that interval (then the fewest slots used).  Costs in units of 32 cycles.
   int nblk = 0;
   for (int l = 0; l < P.nl; ++l) nblk += (P.ly[l].Npad / 32) * (P.ly[l].Kpad / 32);
   const int per_wave = (nblk + 3) / 4;
@@ -161,7 +166,7 @@ bool make_plan(const NerfNgpNet& n, bool save, NgpPlan& P) {
   for (int l = 0; l < P.nl; ++l) {
     const NgpLayer& L = P.ly[l];
     int cost[4];
-    for (int w = 0; w < 4; ++w) cost[w] = ((w >> 1) * 32 < L.Kpad) ? L.Npad / 2 : 0;
+    for (int w = 0; w < 4; ++w) cost[w] = (L.Kpad / 32) * (L.Npad / 4);
     for (int nb = 0; nb < L.Npad / 32; ++nb)
       for (int kb = 0; kb < L.Kpad / 32; ++kb) {
         int best = -1;
@@ -172,7 +177,7 @@ bool make_plan(const NerfNgpNet& n, bool save, NgpPlan& P) {
         const int sb = best + 4 * used[best];
         P.sb_layer[sb] = l; P.sb_nb[sb] = nb; P.sb_kb[sb] = kb;
         ++used[best];
-        cost[best] += 32;  // 64 rows / 2 per MFMA
+        cost[best] += 32;  // 16 MFMAs x 64 cycles
       }
   }
   P.nsb = 4 * per_wave;
@@ -550,19 +555,12 @@ __device__ __forceinline__ void load_enc(const NgpPlan& P, float* smem, const fl
   }
 }
 
-// cin = [geo (head cols 1..geo) | dir encoding | 0] for row r (one thread per row)
-__device__ __forceinline__ void build_cin_row(const NgpPlan& P, float* smem, const float* __restrict__ x_d, int64_t m,
-                                              int64_t M, int r) {
-  float* c = smem + P.cin_buf + r * P.cin_ld;
-  const float* h = smem + P.ly[P.head].out_buf + r * P.ly[P.head].out_ld;
-  if (P.sraw >= 0) smem[P.sraw + r] = h[0];
-  for (int k = 0; k < P.geo; ++k) c[k] = h[1 + k];
-  float v[27];
-  float x = 0.f, y = 0.f, z = 1.f;
-  if (m < M) { x = x_d[m * 6 + 3]; y = x_d[m * 6 + 4]; z = x_d[m * 6 + 5]; }
-  unit3(x, y, z, 1e-9f);  // MetaNGP._enc_dir (meta_ngp.py:176-179)
+// direction encoding of one row into v[0..dir_dim): MetaNGP._enc_dir (meta_ngp.py:176-179) then SHEncoder.forward
+// (encodings.py:133-151, normalises again) or the dir FrequencyEncoder (encodings.py:437-444)
+__device__ __forceinline__ void dir_encode(const NgpPlan& P, float x, float y, float z, float v[27]) {
+  unit3(x, y, z, 1e-9f);
   if (P.dir_mode == 0) {
-    unit3(x, y, z, 1e-9f);  // SHEncoder.forward normalises again (encodings.py:141)
+    unit3(x, y, z, 1e-9f);
     sh_eval(P.sh_levels - 1, x, y, z, v);
   } else {
     const float d[3] = {x, y, z};
@@ -580,6 +578,19 @@ __device__ __forceinline__ void build_cin_row(const NgpPlan& P, float* smem, con
       }
     }
   }
+}
+
+// cin = [geo (head cols 1..geo) | dir encoding | 0] for row r (one thread per row)
+__device__ __forceinline__ void build_cin_row(const NgpPlan& P, float* smem, const float* __restrict__ x_d, int64_t m,
+                                              int64_t M, int r) {
+  float* c = smem + P.cin_buf + r * P.cin_ld;
+  const float* h = smem + P.ly[P.head].out_buf + r * P.ly[P.head].out_ld;
+  if (P.sraw >= 0) smem[P.sraw + r] = h[0];
+  for (int k = 0; k < P.geo; ++k) c[k] = h[1 + k];
+  float v[27];
+  float x = 0.f, y = 0.f, z = 1.f;
+  if (m < M) { x = x_d[m * 6 + 3]; y = x_d[m * 6 + 4]; z = x_d[m * 6 + 5]; }
+  dir_encode(P, x, y, z, v);
   for (int k = 0; k < P.dir_dim; ++k) c[P.geo + k] = v[k];
   for (int k = P.geo + P.dir_dim; k < P.cin_kpad; ++k) c[k] = 0.f;
 }
@@ -647,134 +658,296 @@ __global__ __launch_bounds__(256) void ngp_density_kernel(NgpPlan P, const float
   }
 }
 
-// Gnext[r][k] = sum_n G[r][n] W[n][k]  (masked by X > 0 when the input is a ReLU output).  If dst_global the
-// result goes to d_enc rows m < M, columns < ncols instead of LDS.
-__device__ __forceinline__ void layer_dgrad(const NgpLayer& L, float* smem, const float* __restrict__ w, int G,
-                                            int Gn, int wave, int li, int lh, float* __restrict__ dst_global,
-                                            int ds, int ncols, int64_t m0, int64_t M) {
-  const int rb = wave & 1, kb = wave >> 1;
-  if (kb * 32 >= L.Kpad) return;
-  const float* Gr = smem + G + (rb * 32 + li) * 68 + 8 * lh;
-  const float* Wc = w + L.w_off + kb * 32 + li;  // column k = kb*32 + li, row n = 16 s + 8 lh + t
-  ngp_f32x16 acc = zero16();
-  const int ns = L.Npad / 16;
+// ---- backward: 32-row tiles, 16x16x4 f32 MFMA blocks for the recomputed forward and the input gradients, 32x32x2
+// blocks for the weight gradients.  Two workgroups share a CU (LDS ~68 KB each), so one workgroup's barrier and L2
+// waits hide behind the other's MFMAs.  A wave's weight operands of the NEXT layer step are loaded into registers
+// while the current step computes (the fragment stream of a tile: forward layers 0..nl-1, then input-gradient
+// layers nl-1..0, wrapping to the next tile), and the barriers are plain s_barriers behind an LDS wait, so the
+// prefetch stays in flight across them.
+
+// one wave's weight operands for one step: a[j] = 4 k-values of its 16-row A fragment for k-slab j (16 k), b = bias
+struct NgpFrag {
+  float4 a[4];
+  float4 b;
+};
+
+// 16x16 blocks of a [32 x N] output (N = 32 or 64): wave w owns column block w (both row blocks) when N = 64, else
+// the block (column w & 1, row w >> 1).
+__device__ __forceinline__ void blk16(int N, int wave, int& cb, int& rb0, int& nrb) {
+  if (N == 64) { cb = wave; rb0 = 0; nrb = 2; }
+  else { cb = wave & 1; rb0 = wave >> 1; nrb = 1; }
+}
+
+// Step i < nl: forward of layer i, A = W rows (n = 16 cb + c16), k = 16 j + 4 g + e.  Step i >= nl: input gradient
+// of layer 2 nl - 1 - i, A = W^T rows (k = 16 kb + c16) of the transposed image wt, n = 16 j + 4 g + e.  Both are
+// five unconditional float4 loads (slabs past the layer's width re-read slab 0; the input-gradient step re-reads a
+// bias it ignores): with a fixed count the compiler waits for the current fragment with vmcnt(5), not vmcnt(0).
+__device__ __forceinline__ void load_frag(const NgpPlan& P, const float* __restrict__ w, const float* __restrict__ wt,
+                                          int i, int wave, int lane, NgpFrag& f) {
+  const int g = lane >> 4, c16 = lane & 15;
+  const bool fw = i < P.nl;
+  const NgpLayer& L = P.ly[fw ? i : 2 * P.nl - 1 - i];
+  const int width = fw ? L.Npad : L.Kpad;   // output width of the step
+  const int depth = fw ? L.Kpad : L.Npad;   // reduction length
+  const int cb = width == 64 ? wave : (wave & 1);
+  const float* src = (fw ? w : wt) + L.w_off + (cb * 16 + c16) * depth + 4 * g;
+  const int ns = depth / 16;
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    if (s < ns) {
-      const float4 g0 = *reinterpret_cast<const float4*>(Gr + 16 * s);
-      const float4 g1 = *reinterpret_cast<const float4*>(Gr + 16 * s + 4);
-      const float* wc = Wc + (int64_t)(16 * s + 8 * lh) * L.Kpad;
-      float wv[8];
-#pragma unroll
-      for (int t = 0; t < 8; ++t) wv[t] = wc[(int64_t)t * L.Kpad];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[0], g0.x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[1], g0.y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[2], g0.z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[3], g0.w, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[4], g1.x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[5], g1.y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[6], g1.z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[7], g1.w, acc, 0, 0, 0);
-    }
-  }
-  const int r = rb * 32 + li;
-  const int k0 = kb * 32 + 4 * lh;
-  if (dst_global) {
-    const int64_t m = m0 + r;
-    if (m < M) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int k = k0 + 8 * q + e;
-          if (k < ncols) dst_global[m * ds + k] = acc[4 * q + e];
-        }
-    }
-    return;
-  }
-  const float* X = smem + L.in_buf + r * L.in_ld + k0;
-  float* Y = smem + Gn + r * 68 + k0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float v0 = acc[4 * q], v1 = acc[4 * q + 1], v2 = acc[4 * q + 2], v3 = acc[4 * q + 3];
-    if (L.in_relu) {
-      const float4 x = *reinterpret_cast<const float4*>(X + 8 * q);
-      v0 = x.x > 0.f ? v0 : 0.f; v1 = x.y > 0.f ? v1 : 0.f; v2 = x.z > 0.f ? v2 : 0.f; v3 = x.w > 0.f ? v3 : 0.f;
-    }
-    *reinterpret_cast<float4*>(Y + 8 * q) = make_float4(v0, v1, v2, v3);
+  for (int j = 0; j < 4; ++j) f.a[j] = *reinterpret_cast<const float4*>(src + 16 * (j < ns ? j : 0));
+  f.b = *reinterpret_cast<const float4*>(w + L.b_off + (fw ? cb * 16 : 0) + 4 * g);
+}
+
+// W^T image of every layer (Kpad x Npad at the layer's packed weight offset) for the input-gradient fragments
+__global__ __launch_bounds__(256) void ngp_wt_kernel(NgpPlan P, const float* __restrict__ w, float* __restrict__ wt) {
+  const NgpLayer& L = P.ly[blockIdx.x];
+  for (int i = threadIdx.x; i < L.Kpad * L.Npad; i += 256) {
+    const int k = i / L.Npad, n = i - k * L.Npad;
+    wt[L.w_off + i] = w[L.w_off + n * L.Kpad + k];
   }
 }
 
-// acc += G[:, nb-block]^T X[:, kb-block] over the tile's 64 rows; lane li <-> k = kb*32 + li, register
-// 4q+e <-> n = nb*32 + 8q + 4lh + e.
-__device__ __forceinline__ void wgrad_block(ngp_f32x16& acc, const NgpLayer& L, const float* smem, int G, int nb,
-                                            int kb, int li, int lh) {
-  const float* Gc = smem + G + nb * 32 + li;
-  const float* Xc = smem + L.in_buf + kb * 32 + li;
+// acc[b] (16x16) += A(16 x 4 KS) B_b for NRB row blocks whose B rows come from LDS (4 k-values per lane per 16-k
+// slab).  Compile-time KS / NRB: every LDS read is issued before the first MFMA, and the row blocks' accumulator
+// chains interleave (16x16x4 has 40 cycles of dependent latency against 32 of issue).
+template <int KS, int NRB>
+__device__ __forceinline__ void mfma16_tile(float4 (&acc)[2], const NgpFrag& f, const float* row0, int ld) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  float4 x[NRB][KS];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int b = 0; b < NRB; ++b)
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int r = 16 * s + 8 * lh + t;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Gc[r * 68], Xc[r * L.in_ld], acc, 0, 0, 0);
+    for (int j = 0; j < KS; ++j) x[b][j] = *reinterpret_cast<const float4*>(row0 + 16 * b * ld + 16 * j);
+  f32x4 c[NRB];
+#pragma unroll
+  for (int b = 0; b < NRB; ++b) c[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < KS; ++j) {
+    const float av[4] = {f.a[j].x, f.a[j].y, f.a[j].z, f.a[j].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int b = 0; b < NRB; ++b) {
+        const float xv = e == 0 ? x[b][j].x : e == 1 ? x[b][j].y : e == 2 ? x[b][j].z : x[b][j].w;
+        c[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], xv, c[b], 0, 0, 0);
+      }
+  }
+#pragma unroll
+  for (int b = 0; b < NRB; ++b) acc[b] = make_float4(c[b][0], c[b][1], c[b][2], c[b][3]);
+}
+
+// Y[32 x Npad] = act(X W^T + b): lane (g, c16) of a block holds Y[16 rb + c16][16 cb + 4 g .. + 3]
+template <int KS, int NRB>
+__device__ __forceinline__ void layer_fwd16_t(const NgpLayer& L, float* smem, const NgpFrag& f, int wave, int lane) {
+  const int g = lane >> 4, c16 = lane & 15;
+  const int cb = NRB == 2 ? wave : (wave & 1), rb0 = NRB == 2 ? 0 : (wave >> 1);
+  float4 acc[2];
+  mfma16_tile<KS, NRB>(acc, f, smem + L.in_buf + (16 * rb0 + c16) * L.in_ld + 4 * g, L.in_ld);
+#pragma unroll
+  for (int b = 0; b < NRB; ++b) {
+    float v0 = acc[b].x + f.b.x, v1 = acc[b].y + f.b.y, v2 = acc[b].z + f.b.z, v3 = acc[b].w + f.b.w;
+    if (L.relu) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
+    *reinterpret_cast<float4*>(smem + L.out_buf + (16 * (rb0 + b) + c16) * L.out_ld + cb * 16 + 4 * g) =
+        make_float4(v0, v1, v2, v3);
+  }
+}
+
+__device__ __forceinline__ void layer_fwd16(const NgpLayer& L, float* smem, const NgpFrag& f, int wave, int lane) {
+  // Kpad, Npad in {32, 64}: uniform dispatch to the four compile-time shapes
+  if (L.Kpad == 64) {
+    if (L.Npad == 64) layer_fwd16_t<4, 2>(L, smem, f, wave, lane);
+    else layer_fwd16_t<4, 1>(L, smem, f, wave, lane);
+  } else {
+    if (L.Npad == 64) layer_fwd16_t<2, 2>(L, smem, f, wave, lane);
+    else layer_fwd16_t<2, 1>(L, smem, f, wave, lane);
+  }
+}
+
+// Gnext[r][k] = sum_n G[r][n] W[n][k]  (masked by X > 0 when the input is a ReLU output).  If dst_global the
+// result goes to d_enc rows m < M, columns < ncols instead of LDS.
+template <int KS, int NRB>
+__device__ __forceinline__ void layer_dgrad16_t(const NgpLayer& L, float* smem, const NgpFrag& f, int G, int Gn,
+                                                int wave, int lane, float* __restrict__ dst_global, int ds, int ncols,
+                                                int64_t m0, int64_t M) {
+  const int g = lane >> 4, c16 = lane & 15;
+  const int kb = NRB == 2 ? wave : (wave & 1), rb0 = NRB == 2 ? 0 : (wave >> 1);
+  float4 acc[2];
+  mfma16_tile<KS, NRB>(acc, f, smem + G + (16 * rb0 + c16) * 68 + 4 * g, 68);
+  const int k0 = kb * 16 + 4 * g;
+#pragma unroll
+  for (int b = 0; b < NRB; ++b) {
+    const int r = 16 * (rb0 + b) + c16;
+    float v0 = acc[b].x, v1 = acc[b].y, v2 = acc[b].z, v3 = acc[b].w;
+    if (dst_global) {
+      const int64_t m = m0 + r;
+      if (m < M) {
+        float* o = dst_global + m * ds + k0;
+        if (k0 < ncols) o[0] = v0;
+        if (k0 + 1 < ncols) o[1] = v1;
+        if (k0 + 2 < ncols) o[2] = v2;
+        if (k0 + 3 < ncols) o[3] = v3;
+      }
+    } else {
+      if (L.in_relu) {
+        const float4 x = *reinterpret_cast<const float4*>(smem + L.in_buf + r * L.in_ld + k0);
+        v0 = x.x > 0.f ? v0 : 0.f; v1 = x.y > 0.f ? v1 : 0.f; v2 = x.z > 0.f ? v2 : 0.f; v3 = x.w > 0.f ? v3 : 0.f;
+      }
+      *reinterpret_cast<float4*>(smem + Gn + r * 68 + k0) = make_float4(v0, v1, v2, v3);
     }
   }
+}
+
+__device__ __forceinline__ void layer_dgrad16(const NgpLayer& L, float* smem, const NgpFrag& f, int G, int Gn,
+                                              int wave, int lane, float* __restrict__ dst_global, int ds, int ncols,
+                                              int64_t m0, int64_t M) {
+  // reduction over Npad, output width Kpad
+  if (L.Npad == 64) {
+    if (L.Kpad == 64) layer_dgrad16_t<4, 2>(L, smem, f, G, Gn, wave, lane, dst_global, ds, ncols, m0, M);
+    else layer_dgrad16_t<4, 1>(L, smem, f, G, Gn, wave, lane, dst_global, ds, ncols, m0, M);
+  } else {
+    if (L.Kpad == 64) layer_dgrad16_t<2, 2>(L, smem, f, G, Gn, wave, lane, dst_global, ds, ncols, m0, M);
+    else layer_dgrad16_t<2, 1>(L, smem, f, G, Gn, wave, lane, dst_global, ds, ncols, m0, M);
+  }
+}
+
+// acc += G[:, nb-block]^T X[:, kb-block] over the tile's 32 rows; lane li <-> k = kb*32 + li, register
+// 4q+e <-> n = nb*32 + 8q + 4lh + e.  Operands of 8 MFMAs are read ahead of them.
+__device__ __forceinline__ void wgrad_block(ngp_f32x16& acc, const NgpLayer& L, const float* smem, int G, int nb,
+                                            int kb, int li, int lh) {
+  const float* Gc = smem + G + nb * 32 + li + 8 * lh * 68;
+  const float* Xc = smem + L.in_buf + kb * 32 + li + 8 * lh * L.in_ld;
+#pragma unroll
+  for (int s = 0; s < NGP_BROWS / 16; ++s) {
+    float gv[8], xv[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      gv[t] = Gc[(16 * s + t) * 68];
+      xv[t] = Xc[(16 * s + t) * L.in_ld];
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(gv[t], xv[t], acc, 0, 0, 0);
+  }
+}
+
+// LDS writes of every wave visible, then s_barrier — without the release fence of __syncthreads, which would also
+// wait for the weight prefetch in flight
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 template <int NSB>
-__global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpPlan P, const float* __restrict__ w,
-                                                      const float* __restrict__ enc, int es,
-                                                      const float* __restrict__ x_d, int64_t M,
-                                                      const float* __restrict__ gout, float* __restrict__ d_enc,
-                                                      float* __restrict__ partial, int64_t ntiles) {
+__global__ __launch_bounds__(256, 2) void ngp_bwd_kernel(NgpPlan P, const float* __restrict__ w,
+                                                         const float* __restrict__ enc, int es,
+                                                         const float* __restrict__ x_d, int64_t M,
+                                                         const float* __restrict__ gout, float* __restrict__ d_enc,
+                                                         float* __restrict__ partial,
+                                                         const float* __restrict__ wt, int64_t ntiles) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* dsig = smem + P.dsig;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 31, lh = lane >> 5;
+  // wave index in an SGPR: the plan's per-wave tables (sb_layer, ...) are then scalar kernarg loads, not vector
+  // loads that the compiler would wait for with vmcnt(0) (draining the weight prefetch)
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, li = lane & 31,
+            lh = lane >> 5;
   ngp_f32x16 accw[NSB];
 #pragma unroll
   for (int j = 0; j < NSB; ++j) accw[j] = zero16();
-  // bias gradients: wave w sums rows 16w..16w+15 of every tile into its own LDS partial (column = lane); without
+  // bias gradients: wave w sums rows 8w..8w+7 of every tile into its own LDS partial (column = lane); without
   // room for the partials (P.bsum < 0) wave l&3 sums all rows of layer l into bacc[l>>2]
   float* bsum = smem + (P.bsum >= 0 ? P.bsum : 0) + wave * P.nl * 64;
   if (P.bsum >= 0)
     for (int l = 0; l < P.nl; ++l) bsum[l * 64 + lane] = 0.f;
   float bacc[3] = {0.f, 0.f, 0.f};
+  const int nsteps = 2 * P.nl;
+  // fragment ping-pong: step s computes with (s even ? fa : fb) and prefetches step s + 1 into the other (2 nl steps
+  // per tile, so the parity carries over to the next tile); no register copies, which would wait for the prefetch
+  NgpFrag fa, fb;
+  load_frag(P, w, wt, 0, wave, lane, fa);
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t m0 = tile * NGP_ROWS;
-    forward_tile(P, smem, w, enc, es, x_d, m0, M, wave, li, lh);
-    // output gradients: rgb through the sigmoid, sigma through trunc_exp (trunc_exp.py:54-57)
-    const NgpLayer& Lo = P.ly[P.nl - 1];
-    const NgpLayer& Lh = P.ly[P.head];
-    float gc[3] = {0.f, 0.f, 0.f};
-    if (threadIdx.x < NGP_ROWS) {
-      const int r = threadIdx.x;
-      const int64_t m = m0 + r;
-      float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (m < M) g = reinterpret_cast<const float4*>(gout)[m];
-      const float* o = smem + Lo.out_buf + r * Lo.out_ld;
-      const float gg[3] = {g.x, g.y, g.z};
+    const int64_t m0 = tile * NGP_BROWS;
+    // ---- tile inputs, spread over the workgroup: thread (r = tid / 8, p = tid % 8) owns row r's columns
+    // p, p + 8, ... of the enc tile and of the direction encoding (cin columns geo..), and keeps the row's output
+    // gradient.  Loads are unconditional (rows clamped to M - 1, masked after), so none of them drains the weight
+    // prefetch with vmcnt(0).
+    const int pr = tid >> 3, pp = tid & 7;
+    {
+      const int64_t m = m0 + pr;
+      const int64_t mc = m < M ? m : M - 1;
+      const int kp = P.enc_ld - 4;
+      const float* src = enc + mc * es;
+      float* erow = smem + P.enc_buf + pr * P.enc_ld;
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        if (P.sigmoid) {
-          const float s = nerf_mlp::sigmoidf_(o[c]);
-          gc[c] = gg[c] * (s * (1.0f - s));
-        } else {
-          gc[c] = gg[c];
-        }
+      for (int i = 0; i < 8; ++i) {
+        const int c = pp + 8 * i;
+        const float v = src[c < P.in_dim ? c : 0];
+        if (c < kp) erow[c] = (m < M && c < P.in_dim) ? v : 0.f;
       }
-      const float sr = smem[Lh.out_buf + r * Lh.out_ld];
-      dsig[r] = g.w * expf(fminf(fmaxf(sr, -nerf_mlp::EXP_MAX), nerf_mlp::EXP_MAX));
+      const float* dr = x_d + mc * 6 + 3;
+      const float dx = dr[0], dy = dr[1], dz = dr[2];
+      float v[27];
+      dir_encode(P, m < M ? dx : 0.f, m < M ? dy : 0.f, m < M ? dz : 1.f, v);
+      float* crow = smem + P.cin_buf + pr * P.cin_ld;
+#pragma unroll
+      for (int k = 0; k < 27; ++k)
+        if (k < P.dir_dim && (k & 7) == pp) crow[P.geo + k] = v[k];
+      for (int c = P.geo + P.dir_dim + pp; c < P.cin_kpad; c += 8) crow[c] = 0.f;
     }
-    __syncthreads();  // the raw head/out tiles alias the gradient tiles
-    if (threadIdx.x < NGP_ROWS) {
-      float* gr = smem + P.g0 + threadIdx.x * 68;
-      gr[0] = gc[0]; gr[1] = gc[1]; gr[2] = gc[2];
-      for (int c = 3; c < 32; ++c) gr[c] = 0.f;
-    }
-    __syncthreads();
+    lds_barrier();
     int G = P.g0, Gn = P.g1;
-    for (int l = P.nl - 1; l >= 0; --l) {
+    // step s < nl: forward of layer s; the last forward step also forms the output gradients.  Step s >= nl: layer
+    // l = 2 nl - 1 - s in reverse (weight gradient, bias partials, input gradient).
+    auto step = [&](int s, const NgpFrag& use, NgpFrag& pre) {
+      // lane-derived values recomputed per step from an opaque copy: otherwise the compiler hoists every per-lane
+      // LDS address of every layer shape out of the tile loop and holds them all in VGPRs (spilling past 256)
+      int lane = tid & 63;
+      asm volatile("" : "+v"(lane));
+      const int li = lane & 31, lh = lane >> 5, pr = 8 * wave + (lane >> 3), pp = lane & 7;
+      // the row's output gradient, issued before the weight prefetch so that waiting for it leaves that in flight
+      float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (s == P.nl - 1) gv = reinterpret_cast<const float4*>(gout)[m0 + pr < M ? m0 + pr : M - 1];
+      load_frag(P, w, wt, s + 1 == nsteps ? 0 : s + 1, wave, lane, pre);
+      if (s < P.nl) {
+        layer_fwd16(P.ly[s], smem, use, wave, lane);
+        lds_barrier();
+        if (s == P.head) {  // cin columns 0..geo-1 = head output columns 1..geo
+          const float* hrow = smem + P.ly[P.head].out_buf + pr * P.ly[P.head].out_ld;
+          float* crow = smem + P.cin_buf + pr * P.cin_ld;
+          for (int c = pp; c < P.geo; c += 8) crow[c] = hrow[1 + c];
+          lds_barrier();
+        }
+        if (s == P.nl - 1) {
+          // output gradients: rgb through the sigmoid, sigma through trunc_exp (trunc_exp.py:54-57); thread p = 0 of
+          // each row (8 rows per wave, so all four waves share the work)
+          const NgpLayer& Lo = P.ly[P.nl - 1];
+          const NgpLayer& Lh = P.ly[P.head];
+          float4 gq = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (m0 + pr >= M) gv = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (pp == 0) {
+            const float* o = smem + Lo.out_buf + pr * Lo.out_ld;
+            const float gg[3] = {gv.x, gv.y, gv.z};
+            float gc[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              if (P.sigmoid) {
+                const float sg = nerf_mlp::sigmoidf_(o[c]);
+                gc[c] = gg[c] * (sg * (1.0f - sg));
+              } else {
+                gc[c] = gg[c];
+              }
+            }
+            gq = make_float4(gc[0], gc[1], gc[2], 0.f);
+            const float sr = smem[Lh.out_buf + pr * Lh.out_ld];
+            dsig[pr] = gv.w * expf(fminf(fmaxf(sr, -nerf_mlp::EXP_MAX), nerf_mlp::EXP_MAX));
+          }
+          lds_barrier();  // the raw head/out tiles alias the gradient tiles
+          *reinterpret_cast<float4*>(smem + P.g0 + pr * 68 + 4 * pp) = gq;
+          lds_barrier();
+          G = P.g0; Gn = P.g1;
+        }
+        return;
+      }
+      const int l = 2 * P.nl - 1 - s;
       const NgpLayer& L = P.ly[l];
       // weight gradient blocks of this layer owned by this wave
 #pragma unroll
@@ -783,34 +956,41 @@ __global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpPlan P, const float* __
         if (sb < P.nsb && P.sb_layer[sb] == l) wgrad_block(accw[j], L, smem, G, P.sb_nb[sb], P.sb_kb[sb], li, lh);
       }
       if (P.bsum >= 0 && lane < L.Npad) {
-        const float* gc = smem + G + (16 * wave) * 68 + lane;
-        float s = 0.f;
+        const float* gcol = smem + G + (8 * wave) * 68 + lane;
+        float sum = 0.f;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s += gc[r * 68];
-        bsum[l * 64 + lane] += s;
+        for (int r = 0; r < 8; ++r) sum += gcol[r * 68];
+        bsum[l * 64 + lane] += sum;
       } else if (P.bsum < 0 && (l & 3) == wave && lane < L.Npad) {
-        float s = 0.f;
-        for (int r = 0; r < NGP_ROWS; ++r) s += smem[G + r * 68 + lane];
-        bacc[l >> 2] += s;
+        float sum = 0.f;
+        for (int r = 0; r < NGP_BROWS; ++r) sum += smem[G + r * 68 + lane];
+        bacc[l >> 2] += sum;
       }
       // input gradient
       const bool to_enc = (l == 0);
-      layer_dgrad(L, smem, w, G, Gn, wave, li, lh, to_enc ? d_enc : nullptr, es, P.in_dim, m0, M);
-      __syncthreads();
+      layer_dgrad16(L, smem, use, G, Gn, wave, lane, to_enc ? d_enc : nullptr, es, P.in_dim, m0, M);
+      lds_barrier();
       if (l == P.head + 1) {
-        // Gn holds d cin: the head's gradient is [d sigma_raw, d geo, 0...]
-        if (threadIdx.x < NGP_ROWS) {
-          const int r = threadIdx.x;
-          const float* dc = smem + Gn + r * 68;
-          float* gh = smem + G + r * 68;
-          gh[0] = dsig[r];
-          for (int c = 0; c < P.geo; ++c) gh[1 + c] = dc[c];
-          for (int c = 1 + P.geo; c < 32; ++c) gh[c] = 0.f;
+        // Gn holds d cin: the head's gradient is [d sigma_raw, d geo, 0...] (thread (r, p): columns 4p..4p+3)
+        {
+          const float* dc = smem + Gn + pr * 68;
+          float hv[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int c = 4 * pp + e;
+            hv[e] = c == 0 ? dsig[pr] : (c <= P.geo ? dc[c - 1] : 0.f);
+          }
+          *reinterpret_cast<float4*>(smem + G + pr * 68 + 4 * pp) = make_float4(hv[0], hv[1], hv[2], hv[3]);
         }
-        __syncthreads();
+        lds_barrier();
       } else {
         const int t = G; G = Gn; Gn = t;
       }
+    };
+    // pairs of steps with fixed operands (2 nl steps per tile): no selects or copies between the two fragments
+    for (int s = 0; s < nsteps; s += 2) {
+      step(s, fa, fb);
+      step(s + 1, fb, fa);
     }
   }
   // slab of this workgroup: every packed float is written exactly once
@@ -844,6 +1024,299 @@ __global__ __launch_bounds__(256) void ngp_bwd_kernel(NgpPlan P, const float* __
     for (int j = 0; j < 3; ++j) {
       const int l = wave + 4 * j;
       if (l < P.nl && lane < P.ly[l].Npad) slab[P.ly[l].b_off + lane] = bacc[j];
+    }
+  }
+}
+
+// ---- the production expert's backward.  MetaNGP's defaults (nerf_runner.py:103-121; meta_ngp.py:21-105): hash
+// encoding <= 32 wide, sigma trunk 2 x 64, head 1 + 15, SH degree-4 directions (16), colour 2 x 64, rgb.  The same
+// algorithm as ngp_bwd_kernel with every shape, LDS offset and weight-gradient block fixed at compile time: the whole
+// tile is straight-line code (no plan lookups, no branches on the layer shape, no conditional accumulator updates),
+// the head / rgb layers compute only their live 16 columns, and the weight gradients use balanced 16x16 blocks (each
+// wave owns a quarter of every layer's live blocks, so no wave idles through a layer's barrier interval).
+namespace ngp_prod {
+constexpr int NL = 6, HEAD = 2;
+constexpr int KP[NL] = {32, 64, 64, 32, 64, 64};    // padded fan-in
+constexpr int NP[NL] = {64, 64, 32, 64, 64, 32};    // padded fan-out (packed layout)
+constexpr int NE[NL] = {64, 64, 16, 64, 64, 16};    // live fan-out: head 1 + 15, rgb 3 -> 16
+constexpr int RELU[NL] = {1, 1, 0, 1, 1, 0};
+constexpr int INRELU[NL] = {0, 1, 1, 0, 1, 1};
+constexpr int WOFF[NL] = {0, 2112, 6272, 8352, 10464, 14624};
+constexpr int BOFF[NL] = {2048, 6208, 8320, 10400, 14560, 16672};
+constexpr int TOTAL = 16704;
+// LDS (floats; the backward plan of make_plan for this shape, checked on the host)
+constexpr int ENC = 0, CIN = 1152, G0 = 2304, G1 = 4480, DSIG = 6656, BSUM = 15392, SMEM = 16928;
+constexpr int OUTB[NL] = {6688, 8864, G0, 11040, 13216, G1};
+constexpr int INB[NL] = {ENC, 6688, 8864, CIN, 11040, 13216};
+constexpr int INLD[NL] = {36, 68, 68, 36, 68, 68};
+constexpr int GEO = 15, DIRD = 16;
+// gradient tile read (G) and written (GN) by the input-gradient step of layer l (g0 holds the output gradients)
+constexpr int GB[NL] = {G0, G1, G0, G0, G1, G0};
+constexpr int GNB[NL] = {-1, G0, G1, G1, G0, G1};
+// weight-gradient 16x16 blocks: layer l has (NE/16) x (KP/16) live blocks, block i = wave + 4 q -> (i / (KP/16),
+// i % (KP/16)); NBW[l] blocks per wave in accumulator slots SLOT0[l]..
+constexpr int NBW[NL] = {2, 4, 1, 2, 4, 1};
+constexpr int SLOT0[NL] = {0, 2, 6, 7, 9, 13};
+constexpr int NSLOT = 14;
+
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+
+// weights of step s (forward layer s < NL, else the input gradient of layer 2 NL - 1 - s): a fixed, per-step load
+// count, so the compiler's waits for the current fragment are exact
+template <int S>
+__device__ __forceinline__ void load_frag(const float* __restrict__ w, const float* __restrict__ wt, int wave, int lane,
+                                          NgpFrag& f) {
+  constexpr bool fw = S < NL;
+  constexpr int l = fw ? S : 2 * NL - 1 - S;
+  constexpr int width = fw ? NE[l] : KP[l], depth = fw ? KP[l] : NE[l], pitch = fw ? KP[l] : NP[l];
+  const int g = lane >> 4, c16 = lane & 15;
+  const int cb = width == 64 ? wave : width == 32 ? (wave & 1) : 0;
+  const float* src = (fw ? w : wt) + WOFF[l] + (cb * 16 + c16) * pitch + 4 * g;
+#pragma unroll
+  for (int j = 0; j < depth / 16; ++j) f.a[j] = *reinterpret_cast<const float4*>(src + 16 * j);
+  if constexpr (fw) f.b = *reinterpret_cast<const float4*>(w + BOFF[l] + cb * 16 + 4 * g);
+}
+
+template <int l>
+__device__ __forceinline__ void fwd(float* smem, const NgpFrag& f, int wave, int lane) {
+  constexpr int NRB = NE[l] == 64 ? 2 : 1;
+  if (NE[l] == 16 && wave >= 2) return;  // 16 live columns: one column block, waves 0-1 take its row blocks
+  const int g = lane >> 4, c16 = lane & 15;
+  const int cb = NE[l] == 64 ? wave : 0, rb0 = NE[l] == 64 ? 0 : wave;
+  float4 acc[2];
+  mfma16_tile<KP[l] / 16, NRB>(acc, f, smem + INB[l] + (16 * rb0 + c16) * INLD[l] + 4 * g, INLD[l]);
+#pragma unroll
+  for (int b = 0; b < NRB; ++b) {
+    float v0 = acc[b].x + f.b.x, v1 = acc[b].y + f.b.y, v2 = acc[b].z + f.b.z, v3 = acc[b].w + f.b.w;
+    if (RELU[l]) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
+    *reinterpret_cast<float4*>(smem + OUTB[l] + (16 * (rb0 + b) + c16) * 68 + cb * 16 + 4 * g) =
+        make_float4(v0, v1, v2, v3);
+  }
+}
+
+template <int l>
+__device__ __forceinline__ void dgrad(float* smem, const NgpFrag& f, int wave, int lane, float* __restrict__ d_enc,
+                                      int es, int in_dim, int64_t m0, int64_t M) {
+  constexpr int NRB = KP[l] == 64 ? 2 : 1;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int kb = KP[l] == 64 ? wave : (wave & 1), rb0 = KP[l] == 64 ? 0 : (wave >> 1);
+  float4 acc[2];
+  mfma16_tile<NE[l] / 16, NRB>(acc, f, smem + GB[l] + (16 * rb0 + c16) * 68 + 4 * g, 68);
+  const int k0 = kb * 16 + 4 * g;
+#pragma unroll
+  for (int b = 0; b < NRB; ++b) {
+    const int r = 16 * (rb0 + b) + c16;
+    float v0 = acc[b].x, v1 = acc[b].y, v2 = acc[b].z, v3 = acc[b].w;
+    if constexpr (l == 0) {
+      const int64_t m = m0 + r;
+      if (m < M) {
+        float* o = d_enc + m * es + k0;
+        if (k0 < in_dim) o[0] = v0;
+        if (k0 + 1 < in_dim) o[1] = v1;
+        if (k0 + 2 < in_dim) o[2] = v2;
+        if (k0 + 3 < in_dim) o[3] = v3;
+      }
+    } else {
+      if (INRELU[l]) {
+        const float4 x = *reinterpret_cast<const float4*>(smem + INB[l] + r * INLD[l] + k0);
+        v0 = x.x > 0.f ? v0 : 0.f; v1 = x.y > 0.f ? v1 : 0.f; v2 = x.z > 0.f ? v2 : 0.f; v3 = x.w > 0.f ? v3 : 0.f;
+      }
+      *reinterpret_cast<float4*>(smem + GNB[l] + r * 68 + k0) = make_float4(v0, v1, v2, v3);
+    }
+  }
+}
+
+// acc[slot] (16x16: n = 16 nb + 4 g + e, k = 16 kb + c16) += sum over the tile's 32 rows of G[r][n] X[r][k];
+// MFMA s reduces rows 8 g + s (lane group g), the wave's blocks of the layer interleaved
+template <int l>
+__device__ __forceinline__ void wgrad(ngp_f32x4 (&acc)[NSLOT], const float* smem, int wave, int lane) {
+  constexpr int KB = KP[l] / 16;
+  const int g = lane >> 4, c16 = lane & 15;
+  float gv[NBW[l]][8], xv[NBW[l]][8];
+#pragma unroll
+  for (int q = 0; q < NBW[l]; ++q) {
+    const int i = wave + 4 * q, nb = i / KB, kb = i % KB;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      gv[q][s] = smem[GB[l] + (8 * g + s) * 68 + nb * 16 + c16];
+      xv[q][s] = smem[INB[l] + (8 * g + s) * INLD[l] + kb * 16 + c16];
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+#pragma unroll
+    for (int q = 0; q < NBW[l]; ++q)
+      acc[SLOT0[l] + q] = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[q][s], xv[q][s], acc[SLOT0[l] + q], 0, 0, 0);
+}
+
+// one tile's inputs for thread (row pr, part pp): enc columns pp + 8 i and the ray direction; rows clamped to M - 1
+struct TileIn {
+  float e[4];
+  float d[3];
+};
+
+__device__ __forceinline__ void load_tile_in(const float* __restrict__ enc, int es, int in_dim,
+                                             const float* __restrict__ x_d, int64_t M, int64_t tile, int pr, int pp,
+                                             TileIn& t) {
+  const int64_t m = tile * NGP_BROWS + pr;
+  const int64_t mc = m < M ? m : M - 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = pp + 8 * i;
+    t.e[i] = enc[mc * es + (c < in_dim ? c : 0)];
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) t.d[c] = x_d[mc * 6 + 3 + c];
+}
+
+}  // namespace ngp_prod
+
+template <int SIGMOID>
+__global__ __launch_bounds__(256, 2) void ngp_bwd_prod_kernel(const float* __restrict__ w, const float* __restrict__ wt,
+                                                              const float* __restrict__ enc, int es, int in_dim,
+                                                              const float* __restrict__ x_d, int64_t M,
+                                                              const float* __restrict__ gout,
+                                                              float* __restrict__ d_enc, float* __restrict__ partial,
+                                                              int64_t ntiles) {
+  using namespace ngp_prod;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  ngp_f32x4 acc[NSLOT];
+#pragma unroll
+  for (int j = 0; j < NSLOT; ++j) acc[j] = ngp_f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[NL];  // bias gradient of column `lane`, this wave's rows 8 wave .. 8 wave + 7 of every tile
+#pragma unroll
+  for (int l = 0; l < NL; ++l) bacc[l] = 0.f;
+  NgpFrag fa, fb;
+  load_frag<0>(w, wt, wave, tid & 63, fa);
+  TileIn nx;
+  load_tile_in(enc, es, in_dim, x_d, M, blockIdx.x, tid >> 3, tid & 7, nx);
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t m0 = tile * NGP_BROWS;
+    // ---- tile inputs (prefetched during the previous tile's backward) -> enc tile, cin direction columns
+    {
+      int lane = tid & 63;
+      asm volatile("" : "+v"(lane));
+      const int pr = 8 * wave + (lane >> 3), pp = lane & 7;
+      const bool ok = m0 + pr < M;
+      float* erow = smem + ENC + pr * 36;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = pp + 8 * i;
+        erow[c] = (ok && c < in_dim) ? nx.e[i] : 0.f;
+      }
+      float v[27];
+      float x = ok ? nx.d[0] : 0.f, y = ok ? nx.d[1] : 0.f, z = ok ? nx.d[2] : 1.f;
+      unit3(x, y, z, 1e-9f);  // MetaNGP._enc_dir (meta_ngp.py:176-179)
+      unit3(x, y, z, 1e-9f);  // SHEncoder.forward normalises again (encodings.py:141)
+      sh_eval(3, x, y, z, v);
+      float v0 = v[0], v8 = v[8];  // components pp and 8 + pp (selects: a runtime index would put v in scratch)
+#pragma unroll
+      for (int k = 1; k < 8; ++k)
+        if (pp == k) { v0 = v[k]; v8 = v[8 + k]; }
+      float* crow = smem + CIN + pr * 36;
+      crow[GEO + pp] = v0;
+      crow[GEO + 8 + pp] = v8;
+      if (pp == 0) crow[GEO + DIRD] = 0.f;
+    }
+    lds_barrier();
+    sfor<0, 2 * NL>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      NgpFrag& use = (s & 1) ? fb : fa;
+      NgpFrag& pre = (s & 1) ? fa : fb;
+      int lane = tid & 63;
+      asm volatile("" : "+v"(lane));
+      const int pr = 8 * wave + (lane >> 3), pp = lane & 7;
+      float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (s == NL - 1) gv = reinterpret_cast<const float4*>(gout)[m0 + pr < M ? m0 + pr : M - 1];
+      if constexpr (s == NL) load_tile_in(enc, es, in_dim, x_d, M, tile + gridDim.x, pr, pp, nx);
+      load_frag<(s + 1) % (2 * NL)>(w, wt, wave, lane, pre);
+      if constexpr (s < NL) {
+        fwd<s>(smem, use, wave, lane);
+        lds_barrier();
+        if constexpr (s == HEAD) {  // cin columns 0..14 = head output columns 1..15
+          const float* hrow = smem + G0 + pr * 68;
+          float* crow = smem + CIN + pr * 36;
+          crow[pp] = hrow[1 + pp];
+          if (pp < GEO - 8) crow[8 + pp] = hrow[9 + pp];
+          lds_barrier();
+        }
+        if constexpr (s == NL - 1) {
+          // output gradients: rgb through the sigmoid, sigma through trunc_exp (trunc_exp.py:54-57)
+          float4 gq = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (m0 + pr >= M) gv = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (pp == 0) {
+            const float* o = smem + G1 + pr * 68;
+            if (SIGMOID) {
+              const float s0 = nerf_mlp::sigmoidf_(o[0]), s1 = nerf_mlp::sigmoidf_(o[1]),
+                          s2 = nerf_mlp::sigmoidf_(o[2]);
+              gq = make_float4(gv.x * (s0 * (1.0f - s0)), gv.y * (s1 * (1.0f - s1)), gv.z * (s2 * (1.0f - s2)), 0.f);
+            } else {
+              gq = make_float4(gv.x, gv.y, gv.z, 0.f);
+            }
+            const float sr = smem[G0 + pr * 68];
+            smem[DSIG + pr] = gv.w * expf(fminf(fmaxf(sr, -nerf_mlp::EXP_MAX), nerf_mlp::EXP_MAX));
+          }
+          lds_barrier();  // the raw head / rgb tiles alias the gradient tiles
+          *reinterpret_cast<float4*>(smem + G0 + pr * 68 + 4 * pp) = gq;
+          lds_barrier();
+        }
+      } else {
+        constexpr int l = 2 * NL - 1 - s;
+        wgrad<l>(acc, smem, wave, lane);
+        if (lane < NP[l]) {
+          const float* gcol = smem + GB[l] + (8 * wave) * 68 + lane;
+          float sum = 0.f;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) sum += gcol[r * 68];
+          bacc[l] += sum;
+        }
+        dgrad<l>(smem, use, wave, lane, d_enc, es, in_dim, m0, M);
+        lds_barrier();
+        if constexpr (l == HEAD + 1) {
+          // GNB holds d cin: the head's gradient is [d sigma_raw, d geo, 0...] (thread (r, p): columns 4p..4p+3)
+          const float* dc = smem + GNB[l] + pr * 68;
+          float hv[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int c = 4 * pp + e;
+            hv[e] = c == 0 ? smem[DSIG + pr] : (c <= GEO ? dc[c - 1] : 0.f);
+          }
+          *reinterpret_cast<float4*>(smem + GB[HEAD] + pr * 68 + 4 * pp) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+          lds_barrier();
+        }
+      }
+    });
+  }
+  // ---- this workgroup's slab: every packed float written exactly once
+  const int lane = tid & 63, g = lane >> 4, c16 = lane & 15;
+  float* slab = partial + (int64_t)blockIdx.x * TOTAL;
+  sfor<0, NL>([&](auto Lc) {
+    constexpr int l = decltype(Lc)::value;
+    constexpr int KB = KP[l] / 16;
+#pragma unroll
+    for (int q = 0; q < NBW[l]; ++q) {
+      const int i = wave + 4 * q, nb = i / KB, kb = i % KB;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) slab[WOFF[l] + (nb * 16 + 4 * g + e) * KP[l] + kb * 16 + c16] = acc[SLOT0[l] + q][e];
+    }
+    if constexpr (NE[l] < NP[l])  // dead rows of the head / rgb weights
+      for (int i = tid; i < (NP[l] - NE[l]) * KP[l]; i += 256) slab[WOFF[l] + NE[l] * KP[l] + i] = 0.f;
+    smem[BSUM + (wave * NL + l) * 64 + lane] = bacc[l];
+  });
+  __syncthreads();
+  for (int l = wave; l < NL; l += 4) {
+    if (lane < NP[l]) {
+      const float* b = smem + BSUM + l * 64 + lane;
+      constexpr int ws = NL * 64;
+      slab[BOFF[l] + lane] = (b[0] + b[ws]) + (b[2 * ws] + b[3 * ws]);
     }
   }
 }
@@ -903,13 +1376,35 @@ void allow_lds(K kernel) {
 }
 
 int bwd_grid(int64_t M) {
-  const int64_t ntiles = nerf_cdiv(M, NGP_ROWS);
+  const int64_t ntiles = nerf_cdiv(M, NGP_BROWS);
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) {
     int v = 0;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ncu = v;
   }
+  ncu *= 2;  // two workgroups per CU
   return (int)(ntiles < ncu ? (ntiles < 1 ? 1 : ntiles) : ncu);
+}
+
+// the plan is the production expert's (ngp_bwd_prod_kernel's compile-time shape and LDS layout);
+// NERF_NGP_PROD=0 keeps the generic kernel (A/B measurements, tests)
+bool is_prod_plan(const NgpPlan& P) {
+  const char* e = getenv("NERF_NGP_PROD");  // read per call: tests switch it between launches
+  const bool on = !(e && e[0] == '0');
+  using namespace ngp_prod;
+  if (!on || P.nl != NL || P.head != HEAD || P.total != TOTAL || P.dir_mode != 0 || P.sh_levels != 4 ||
+      P.geo != GEO || P.dir_dim != DIRD || P.in_dim > 32 || P.enc_buf != ENC || P.enc_ld != 36 ||
+      P.cin_buf != CIN || P.cin_ld != 36 || P.g0 != G0 || P.g1 != G1 || P.dsig != DSIG || P.bsum != BSUM ||
+      P.smem_floats != SMEM)
+    return false;
+  for (int l = 0; l < NL; ++l) {
+    const NgpLayer& L = P.ly[l];
+    if (L.Kpad != KP[l] || L.Npad != NP[l] || L.w_off != WOFF[l] || L.b_off != BOFF[l] || L.relu != RELU[l] ||
+        L.in_relu != INRELU[l] || L.in_buf != INB[l] || L.in_ld != INLD[l] || L.out_buf != OUTB[l] ||
+        (L.out_ld != 68))
+      return false;
+  }
+  return true;
 }
 
 bool hash_args(const NerfHashGrid* g, const float* aabb_host_unused, HashArgs& a) {
@@ -1030,7 +1525,7 @@ extern "C" int64_t nerf_ngp_layout(const NerfNgpNet* net, int64_t* table, int32_
 extern "C" int64_t nerf_ngp_workspace_bytes(const NerfNgpNet* net, int64_t M) {
   NgpPlan P;
   if (!net || M < 0 || !make_plan(*net, true, P)) return NERF_E_ARG;
-  return (int64_t)bwd_grid(M) * P.total * 4 + 256;
+  return ((int64_t)bwd_grid(M) + 1) * P.total * 4 + 256;  // slabs + the W^T image
 }
 
 extern "C" int nerf_ngp_fwd(const NerfNgpNet* net, const float* w, const float* enc, int enc_stride,
@@ -1071,20 +1566,38 @@ extern "C" int nerf_ngp_bwd(const NerfNgpNet* net, const float* w, const float* 
   if (!w || !enc || !x_d || !d_rgb_sigma || !d_enc || !ws) return NERF_E_ARG;
   if (!nerf_aligned16(w) || !nerf_aligned16(d_rgb_sigma) || !nerf_aligned16(ws)) return NERF_E_ALIGN;
   const int grid = bwd_grid(M);
-  if (ws_bytes < (int64_t)grid * P.total * 4) return NERF_E_WORKSPACE;
-  const int64_t ntiles = nerf_cdiv(M, NGP_ROWS);
+  if (ws_bytes < ((int64_t)grid + 1) * P.total * 4) return NERF_E_WORKSPACE;
+  const int64_t ntiles = nerf_cdiv(M, NGP_BROWS);
   const int nsbw = (P.nsb + 3) / 4;
   const size_t sm = (size_t)P.smem_floats * 4;
   float* partial = reinterpret_cast<float*>(ws);
+  float* wt = partial + (int64_t)grid * P.total;
+  ngp_wt_kernel<<<P.nl, 256, 0, st>>>(P, w, wt);
+  if (is_prod_plan(P)) {
+    const size_t smp = (size_t)ngp_prod::SMEM * 4;
+    if (P.sigmoid) {
+      allow_lds(ngp_bwd_prod_kernel<1>);
+      ngp_bwd_prod_kernel<1><<<grid, 256, smp, st>>>(w, wt, enc, enc_stride, P.in_dim, x_d, M, d_rgb_sigma, d_enc,
+                                                      partial, ntiles);
+    } else {
+      allow_lds(ngp_bwd_prod_kernel<0>);
+      ngp_bwd_prod_kernel<0><<<grid, 256, smp, st>>>(w, wt, enc, enc_stride, P.in_dim, x_d, M, d_rgb_sigma, d_enc,
+                                                      partial, ntiles);
+    }
+  } else {
   allow_lds(ngp_bwd_kernel<4>);
   allow_lds(ngp_bwd_kernel<6>);
   allow_lds(ngp_bwd_kernel<8>);
   if (nsbw <= 4)
-    ngp_bwd_kernel<4><<<grid, 256, sm, st>>>(P, w, enc, enc_stride, x_d, M, d_rgb_sigma, d_enc, partial, ntiles);
+    ngp_bwd_kernel<4><<<grid, 256, sm, st>>>(P, w, enc, enc_stride, x_d, M, d_rgb_sigma, d_enc, partial, wt,
+                                                 ntiles);
   else if (nsbw <= 6)
-    ngp_bwd_kernel<6><<<grid, 256, sm, st>>>(P, w, enc, enc_stride, x_d, M, d_rgb_sigma, d_enc, partial, ntiles);
+    ngp_bwd_kernel<6><<<grid, 256, sm, st>>>(P, w, enc, enc_stride, x_d, M, d_rgb_sigma, d_enc, partial, wt,
+                                                 ntiles);
   else
-    ngp_bwd_kernel<8><<<grid, 256, sm, st>>>(P, w, enc, enc_stride, x_d, M, d_rgb_sigma, d_enc, partial, ntiles);
+    ngp_bwd_kernel<8><<<grid, 256, sm, st>>>(P, w, enc, enc_stride, x_d, M, d_rgb_sigma, d_enc, partial, wt,
+                                                 ntiles);
+  }
   const unsigned rblocks = (unsigned)nerf_cdiv(P.total / 4, RED_COLS4);
   if (nerf_aligned16(d_w))
     ngp_reduce_kernel<true><<<rblocks, 256, 0, st>>>(partial, P.total, grid, d_w, accumulate);
