@@ -1083,19 +1083,19 @@ __device__ __forceinline__ void load_frag(const float* __restrict__ w, const flo
   if constexpr (fw) f.b = *reinterpret_cast<const float4*>(w + BOFF[l] + cb * 16 + 4 * g);
 }
 
-template <int l>
+template <int l, int IN = INB[l], int IN_LD = INLD[l], int OUT = OUTB[l]>
 __device__ __forceinline__ void fwd(float* smem, const NgpFrag& f, int wave, int lane) {
   constexpr int NRB = NE[l] == 64 ? 2 : 1;
   if (NE[l] == 16 && wave >= 2) return;  // 16 live columns: one column block, waves 0-1 take its row blocks
   const int g = lane >> 4, c16 = lane & 15;
   const int cb = NE[l] == 64 ? wave : 0, rb0 = NE[l] == 64 ? 0 : wave;
   float4 acc[2];
-  mfma16_tile<KP[l] / 16, NRB>(acc, f, smem + INB[l] + (16 * rb0 + c16) * INLD[l] + 4 * g, INLD[l]);
+  mfma16_tile<KP[l] / 16, NRB>(acc, f, smem + IN + (16 * rb0 + c16) * IN_LD + 4 * g, IN_LD);
 #pragma unroll
   for (int b = 0; b < NRB; ++b) {
     float v0 = acc[b].x + f.b.x, v1 = acc[b].y + f.b.y, v2 = acc[b].z + f.b.z, v3 = acc[b].w + f.b.w;
     if (RELU[l]) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
-    *reinterpret_cast<float4*>(smem + OUTB[l] + (16 * (rb0 + b) + c16) * 68 + cb * 16 + 4 * g) =
+    *reinterpret_cast<float4*>(smem + OUT + (16 * (rb0 + b) + c16) * 68 + cb * 16 + 4 * g) =
         make_float4(v0, v1, v2, v3);
   }
 }
@@ -1321,6 +1321,94 @@ __global__ __launch_bounds__(256, 2) void ngp_bwd_prod_kernel(const float* __res
   }
 }
 
+// The production expert's forward (MODE 0: rgb + sigma, nerf_ngp_fwd) and density (MODE 1: sigma trunk + head only,
+// nerf_ngp_density): one 32-row tile per workgroup, the same compile-time layer code as the backward's recompute,
+// activations ping-ponging through two LDS tiles (27 KB per workgroup: six workgroups per CU hide the weight loads).
+namespace ngp_prod {
+constexpr int F_ENC = 0, F_CIN = 1152, F_PA = 2304, F_PB = 4480, F_SRAW = 6656, F_SMEM = 6688;
+}
+
+template <int MODE, int SIGMOID>
+__global__ __launch_bounds__(256) void ngp_fwd_prod_kernel(const float* __restrict__ w, const float* __restrict__ enc,
+                                                           int es, int in_dim, const float* __restrict__ x_d,
+                                                           int64_t M, float* __restrict__ out) {
+  using namespace ngp_prod;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int pr = tid >> 3, pp = tid & 7;
+  const int64_t m0 = (int64_t)blockIdx.x * NGP_BROWS, m = m0 + pr, mc = m < M ? m : M - 1;
+  const bool ok = m < M;
+  NgpFrag fa, fb;
+  load_frag<0>(w, nullptr, wave, lane, fa);
+  {
+    float* erow = smem + F_ENC + pr * 36;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = pp + 8 * i;
+      const float v = enc[mc * es + (c < in_dim ? c : 0)];
+      erow[c] = (ok && c < in_dim) ? v : 0.f;
+    }
+    if constexpr (MODE == 0) {
+      const float* dr = x_d + mc * 6 + 3;
+      float x = ok ? dr[0] : 0.f, y = ok ? dr[1] : 0.f, z = ok ? dr[2] : 1.f;
+      float v[27];
+      unit3(x, y, z, 1e-9f);  // MetaNGP._enc_dir (meta_ngp.py:176-179)
+      unit3(x, y, z, 1e-9f);  // SHEncoder.forward normalises again (encodings.py:141)
+      sh_eval(3, x, y, z, v);
+      float v0 = v[0], v8 = v[8];
+#pragma unroll
+      for (int k = 1; k < 8; ++k)
+        if (pp == k) { v0 = v[k]; v8 = v[8 + k]; }
+      float* crow = smem + F_CIN + pr * 36;
+      crow[GEO + pp] = v0;
+      crow[GEO + 8 + pp] = v8;
+      if (pp == 0) crow[GEO + DIRD] = 0.f;
+    }
+  }
+  lds_barrier();
+  load_frag<1>(w, nullptr, wave, lane, fb);
+  fwd<0, F_ENC, 36, F_PA>(smem, fa, wave, lane);
+  lds_barrier();
+  load_frag<2>(w, nullptr, wave, lane, fa);
+  fwd<1, F_PA, 68, F_PB>(smem, fb, wave, lane);
+  lds_barrier();
+  if constexpr (MODE == 0) load_frag<3>(w, nullptr, wave, lane, fb);
+  fwd<2, F_PB, 68, F_PA>(smem, fa, wave, lane);
+  lds_barrier();
+  if constexpr (MODE == 1) {
+    if (pp == 0 && ok) {
+      const float sr = smem[F_PA + pr * 68];
+      out[m] = expf(fminf(fmaxf(sr, -nerf_mlp::EXP_MAX), nerf_mlp::EXP_MAX));
+    }
+    return;
+  } else {
+    {  // cin columns 0..14 = head output columns 1..15; sigma_raw aside (PA is reused by colour layer 1)
+      const float* hrow = smem + F_PA + pr * 68;
+      float* crow = smem + F_CIN + pr * 36;
+      crow[pp] = hrow[1 + pp];
+      if (pp < GEO - 8) crow[8 + pp] = hrow[9 + pp];
+      if (pp == 0) smem[F_SRAW + pr] = hrow[0];
+    }
+    lds_barrier();
+    load_frag<4>(w, nullptr, wave, lane, fa);
+    fwd<3, F_CIN, 36, F_PB>(smem, fb, wave, lane);
+    lds_barrier();
+    load_frag<5>(w, nullptr, wave, lane, fb);
+    fwd<4, F_PB, 68, F_PA>(smem, fa, wave, lane);
+    lds_barrier();
+    fwd<5, F_PA, 68, F_PB>(smem, fb, wave, lane);
+    lds_barrier();
+    if (pp == 0 && ok) {
+      const float* o = smem + F_PB + pr * 68;
+      float c0 = o[0], c1 = o[1], c2 = o[2];
+      if (SIGMOID) { c0 = nerf_mlp::sigmoidf_(c0); c1 = nerf_mlp::sigmoidf_(c1); c2 = nerf_mlp::sigmoidf_(c2); }
+      const float sg = expf(fminf(fmaxf(smem[F_SRAW + pr], -nerf_mlp::EXP_MAX), nerf_mlp::EXP_MAX));
+      reinterpret_cast<float4*>(out)[m] = make_float4(c0, c1, c2, sg);
+    }
+  }
+}
+
+
 // dw = sum over the workgroup slabs.  A block owns 64 consecutive columns (16 float4) and 16 slab groups: thread
 // (g, c) sums slabs g, g+16, ... of its column in order, then column c's 16 group sums are added in order g = 0..15
 // (deterministic).  One thread per column over all slabs ran at 0.3 TB/s (256 dependent adds per thread).
@@ -1535,6 +1623,16 @@ extern "C" int nerf_ngp_fwd(const NerfNgpNet* net, const float* w, const float* 
   if (M == 0) return NERF_OK;
   if (!w || !enc || !x_d || !rgb_sigma) return NERF_E_ARG;
   if (!nerf_aligned16(w) || !nerf_aligned16(rgb_sigma)) return NERF_E_ALIGN;
+  NgpPlan Pb;  // the production shape runs the compile-time kernel (its check is on the backward plan's layout)
+  if (make_plan(*net, true, Pb) && is_prod_plan(Pb)) {
+    const unsigned blocks = (unsigned)nerf_cdiv(M, NGP_BROWS);
+    const size_t smp = (size_t)ngp_prod::F_SMEM * 4;
+    if (P.sigmoid)
+      ngp_fwd_prod_kernel<0, 1><<<blocks, 256, smp, st>>>(w, enc, enc_stride, P.in_dim, x_d, M, rgb_sigma);
+    else
+      ngp_fwd_prod_kernel<0, 0><<<blocks, 256, smp, st>>>(w, enc, enc_stride, P.in_dim, x_d, M, rgb_sigma);
+    return nerf_launch_status();
+  }
   const size_t sm = (size_t)P.smem_floats * 4;
   allow_lds(ngp_fwd_kernel);
   ngp_fwd_kernel<<<(unsigned)nerf_cdiv(M, NGP_ROWS), 256, sm, st>>>(P, w, enc, enc_stride, x_d, M, rgb_sigma);
@@ -1548,6 +1646,12 @@ extern "C" int nerf_ngp_density(const NerfNgpNet* net, const float* w, const flo
   if (M == 0) return NERF_OK;
   if (!w || !enc || !sigma) return NERF_E_ARG;
   if (!nerf_aligned16(w)) return NERF_E_ALIGN;
+  NgpPlan Pb;
+  if (make_plan(*net, true, Pb) && is_prod_plan(Pb)) {
+    ngp_fwd_prod_kernel<1, 0><<<(unsigned)nerf_cdiv(M, NGP_BROWS), 256, (size_t)ngp_prod::F_SMEM * 4, st>>>(
+        w, enc, enc_stride, P.in_dim, nullptr, M, sigma);
+    return nerf_launch_status();
+  }
   const size_t sm = (size_t)P.smem_floats * 4;
   allow_lds(ngp_density_kernel);
   ngp_density_kernel<<<(unsigned)nerf_cdiv(M, NGP_ROWS), 256, sm, st>>>(P, w, enc, enc_stride, M, sigma);

@@ -20,6 +20,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "nerf-sys_amd"))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 import torch  # noqa: E402
 
@@ -132,6 +133,22 @@ def main():
           "hash_bwd": M * (12 + L * F * 4 + 2 * 8 * L * F * 4)}
     dom = max(("hash_fwd", "hash_bwd"), key=lambda k: ms[k])
     ach = by[dom] / (ms[dom] * 1e-3) / 1e9
+    # the table-gradient scatter is bound by the memory-side float-atomic unit, not by HBM bytes: count the 64-B
+    # atomic requests hash_bwd issues for one step's sample positions (tools/hash_requests.py)
+    from nerf_amd import ngp_trainer as NT
+    from hash_requests import ATOMIC_REQ_PEAK, count_requests
+    seen = {}
+    orig = NT.G.hash_encode_bwd
+
+    def spy(grid, x, *args, **kw):
+        seen.setdefault("x", x.detach().clone())
+        return orig(grid, x, *args, **kw)
+    NT.G.hash_encode_bwd = spy
+    one(a.warmup + 2 * a.steps)
+    NT.G.hash_encode_bwd = orig
+    nreq = count_requests(seen["x"], list(model.xyz_encoder.grid.resolutions)[:L],
+                          hc["log2_hashmap_size"], model._aabb_host, model._eps)
+    req_s = nreq / (ms["hash_bwd"] * 1e-3)
     out = {
         "metric": "rays/sec (train step), Instant-NGP expert (SURVEY §8f row 1), 800x800 Lego-style, "
                   f"{a.samples} stratified samples",
@@ -145,6 +162,9 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "bytes_per_launch": by[dom],
                      "mean_launch_ms": round(ms[dom], 4)},
+        "atomic_roofline": {"bound": "float-atomic requests", "kernel": "hash_bwd", "requests_per_launch": nreq,
+                            "achieved": round(req_s / 1e9, 2), "peak": round(ATOMIC_REQ_PEAK / 1e9, 2),
+                            "unit": "G 64-B requests/s", "frac": round(req_s / ATOMIC_REQ_PEAK, 4)},
         "final_loss": round(float(loss.item()), 6),
     }
     out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(a.cpu_seconds, a.samples)
