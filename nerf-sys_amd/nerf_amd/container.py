@@ -219,8 +219,17 @@ def _march_experts(model, rays, sub_params, render_step_size, alpha_thre, cone_a
                 a, b = bounds[k], bounds[k + 1]
                 if b > a:
                     sig[a:b] = ex.density(xd[a:b, :3], params=sub_params[k]).view(-1)
-            occ_mean = torch.stack([ex.occ_grid.occs.mean() for ex in subs]).float()
-            thr = torch.minimum(occ_mean, torch.tensor(athr, dtype=torch.float32, device=dev)).contiguous()
+            # per-expert thresholds min(alpha_thre, mean occupancy): recomputed only when a grid or alpha_thre
+            # changed (the grids update every 16 steps), not with 4 reductions and a host->device copy every step
+            key = (tuple((ex.occ_grid.gen, ex.occ_grid.occs._version, ex.occ_grid.occs.data_ptr()) for ex in subs),
+                   tuple(athr))
+            cache = model.__dict__.setdefault("_vis_thr", {})
+            thr = cache.get(key)
+            if thr is None:
+                occ_mean = torch.stack([ex.occ_grid.occs.mean() for ex in subs]).float()
+                thr = torch.minimum(occ_mean, torch.tensor(athr, dtype=torch.float32, device=dev)).contiguous()
+                cache.clear()
+                cache[key] = thr
             keep = torch.empty(M, dtype=torch.int32, device=dev)
             check(L.nerf_packed_visibility_groups(ptr(t0), ptr(t1), ptr(sig), ptr(offs), K * N, N, 1e-4,
                                                   float(max(athr)), ptr(thr), ptr(keep), stream()),
@@ -242,6 +251,13 @@ def render_container_occ(model, rays, *, params=None, bg_color_default="white", 
     occupancy marching, per-ray union of the experts' segments (GPU; a per-ray Python loop in the reference),
     routing at the segment midpoints, experts evaluated only where their weight > 1e-8, sigma / rgb blended
     before ONE packed integration.  Returns rgb (N,3), depth (N,), weights (M,1), acc (N,)."""
+    from .ngp import pack_scope
+    with pack_scope():
+        return _render_container_occ(model, rays, params, bg_color_default, chunk, render_step_size, alpha_thre,
+                                     cone_angle)
+
+
+def _render_container_occ(model, rays, params, bg_color_default, chunk, render_step_size, alpha_thre, cone_angle):
     from . import kernels as K_
     from .occupancy import exclusive_scan, render_packed
     from .ray_rendering import _get_bg_rgb

@@ -20,6 +20,7 @@ occupancy renderer once ``occ_ready``.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import math
 import warnings
@@ -321,9 +322,17 @@ class NgpLayout:
         return _PackFn.apply(self, *tensors)
 
     def pack_raw(self, tensors):
+        if _PACK_SCOPE["depth"]:
+            key = (id(self), tuple((t.data_ptr(), t._version) for t in tensors))
+            hit = _PACK_SCOPE["cache"].get(key)
+            if hit is not None:
+                return hit.view(-1)  # a fresh tensor object: each autograd use gets its own node
         flat = torch.cat([x.detach().reshape(-1).to(torch.float32) for x in tensors])
-        return torch.zeros(self.total, dtype=torch.float32, device=flat.device).index_copy(
+        out = torch.zeros(self.total, dtype=torch.float32, device=flat.device).index_copy(
             0, self.device_index(flat.device), flat)
+        if _PACK_SCOPE["depth"]:
+            _PACK_SCOPE["cache"][key] = out
+        return out
 
     def flat_grad_target(self, tensors):
         """(flat gradient buffer, element positions) when every tensor's .grad is a contiguous view of ONE
@@ -341,6 +350,23 @@ class NgpLayout:
             self._dev[key] = torch.cat([torch.arange((g.data_ptr() - b0) // 4, (g.data_ptr() - b0) // 4 + g.numel())
                                         for g in gs]).to(base.device)
         return base, self._dev[key]
+
+
+_PACK_SCOPE = {"depth": 0, "cache": {}}
+
+
+@contextlib.contextmanager
+def pack_scope():
+    """Within one render call the experts' parameters cannot change, so the visibility pass (sigma only) and the
+    forward pack each expert's MLP once (keyed on the tensors' storage and version counters); the cache is dropped
+    when the outermost scope exits."""
+    _PACK_SCOPE["depth"] += 1
+    try:
+        yield
+    finally:
+        _PACK_SCOPE["depth"] -= 1
+        if _PACK_SCOPE["depth"] == 0:
+            _PACK_SCOPE["cache"].clear()
 
 
 class _PackFn(torch.autograd.Function):

@@ -132,6 +132,7 @@ class OccGridEstimator(nn.Module):
         for i, v in enumerate(roi.tolist()):
             g.roi[i] = float(v)
         self.grid = g
+        self.gen = 0  # bumped whenever a HIP kernel rewrites occs (torch's version counter does not see those)
 
     def _seed(self):
         return int(torch.randint(0, 2 ** 62, (1,)).item())
@@ -218,6 +219,7 @@ class OccGridEstimator(nn.Module):
         check(lib().nerf_occ_cell_points(_addr(self.grid), ptr(cells), n, ctypes.c_uint64(self._seed()), ptr(x),
                                          stream()), "nerf_occ_cell_points")
         val = occ_eval_fn(x).reshape(-1).contiguous().float()
+        self.gen += 1
         check(lib().nerf_occ_update(ptr(self.occs), ptr(cells), ptr(val), n, float(ema_decay), stream()),
               "nerf_occ_update")
         check(lib().nerf_occ_threshold(ptr(self.occs), self.occs.numel(), float(occ_thre), ptr(self._thre), stream()),
@@ -238,3 +240,4 @@ class OccGridEstimator(nn.Module):
         c2w = torch.as_tensor(c2w, dtype=torch.float32, device=self.occs.device)[:, :3, :4].contiguous()
         check(lib().nerf_occ_mark_invisible(_addr(self.grid), ptr(K), ptr(c2w), c2w.shape[0], int(width), int(height),
                                             float(near_plane), ptr(self.occs), stream()), "nerf_occ_mark_invisible")
+        self.gen += 1
