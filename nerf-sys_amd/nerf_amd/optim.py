@@ -17,10 +17,21 @@ import torch
 from . import kernels as K
 from .dp import allreduce_flat
 
+_SHARD_ALIGN = 64  # floats: every rank's shard starts 256-B aligned (float4 Adam path)
+
 
 class FlatAdam:
+    """world_size > 1 shards the optimiser (``shard=True``, the default there): the flat gradient is
+    reduce-scattered (each rank receives the rank-mean of ONE 1/N slice), each rank runs the clip and Adam on its
+    slice only (m / v are slice-sized), and the updated parameter slices are all-gathered into every rank's flat
+    buffer.  The bytes on the wire equal one all-reduce of the gradient; the optimiser's HBM traffic and m / v memory
+    drop N-fold (at N = 8 the production container's 134 M-element Adam, 0.75 ms per step on one GPU, becomes ~0.1
+    ms).  A touched-rows exchange of the hash tables does not pay at these batch sizes: one 4096-ray step touches
+    ~61 % of an expert's 2^20-entry levels (tools/hash_requests.py), and an (index, value) pair costs
+    more bytes than the dense value at that density.  shard=False keeps the replicated update (one all-reduce)."""
+
     def __init__(self, groups: List[Dict], betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 grad_clip=1.0, world_size: int = 1):
+                 grad_clip=1.0, world_size: int = 1, shard=None):
         if len(groups) > 8:
             raise ValueError("at most 8 parameter groups (nerf_adam segments)")
         params = [p for g in groups for p in g["params"]]
@@ -28,10 +39,26 @@ class FlatAdam:
             raise ValueError("a parameter appears in two groups")
         dev = params[0].device
         n = sum(p.numel() for p in params)
-        self.flat = torch.empty(n, dtype=torch.float32, device=dev)
-        self.grad = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.m = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.v = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.world_size = int(world_size)
+        self.shard = (self.world_size > 1) if shard is None else (bool(shard) and self.world_size > 1)
+        if self.shard:
+            import torch.distributed as dist
+            self.rank = dist.get_rank()
+            S = -(-n // (self.world_size * _SHARD_ALIGN)) * _SHARD_ALIGN
+            self.shard_size, self.shard_off = S, self.rank * S
+            npad = S * self.world_size
+            # gloo moves CUDA tensors for all_reduce only: the 1-GPU multi-process tests emulate the two collectives
+            self._emulate = dist.get_backend() == "gloo" and dev.type == "cuda"
+        else:
+            npad = n
+        self.n = n
+        self.flat = torch.zeros(npad, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(npad, dtype=torch.float32, device=dev)
+        ns = self.shard_size if self.shard else n
+        self.m = torch.zeros(ns, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(ns, dtype=torch.float32, device=dev)
+        if self.shard:
+            self.gshard = torch.empty(ns, dtype=torch.float32, device=dev)
         self.partials = torch.empty(256, dtype=torch.float32, device=dev)
         self.seg_off, self.seg_lr = [0], []
         o = 0
@@ -50,7 +77,6 @@ class FlatAdam:
                 self.seg_lr.append(float(g["lr"]))
         self.params = params
         self.betas, self.eps, self.wd, self.grad_clip = betas, eps, weight_decay, grad_clip
-        self.world_size = int(world_size)
         self.step_count = 0
 
     def zero_grad(self):
@@ -67,9 +93,41 @@ class FlatAdam:
             allreduce_flat(self.grad, self.world_size)
             self.grad.mul_(1.0 / self.world_size)
 
+    def _step_sharded(self):
+        import torch.distributed as dist
+        S, off, W = self.shard_size, self.shard_off, self.world_size
+        if self._emulate:
+            full = self.grad.clone()
+            dist.all_reduce(full)
+            self.gshard.copy_(full[off:off + S])
+        else:
+            dist.reduce_scatter_tensor(self.gshard, self.grad)
+        self.gshard.mul_(1.0 / W)
+        if self.grad_clip is not None and self.grad_clip > 0:
+            # the global norm: per-block partial sums of this slice, summed over ranks block by block
+            K.grad_sqnorm(self.gshard, self.partials)
+            dist.all_reduce(self.partials)
+            parts, mx = self.partials, float(self.grad_clip)
+        else:
+            parts, mx = None, 0.0
+        pshard = self.flat[off:off + S]
+        seg = [min(max(o - off, 0), S) for o in self.seg_off]
+        K.adam(pshard, self.gshard, self.m, self.v, seg, self.seg_lr, self.step_count, self.betas, self.eps,
+               self.wd, parts, mx)
+        if self._emulate:
+            full = torch.zeros_like(self.flat)
+            full[off:off + S].copy_(pshard)
+            dist.all_reduce(full)  # every other rank's slice is 0 here: the sum is exact
+            self.flat.copy_(full)
+        else:
+            dist.all_gather_into_tensor(self.flat, pshard)  # in place: pshard is this rank's slice of flat
+
     def step(self):
-        self.allreduce_grads()
         self.step_count += 1
+        if self.shard:
+            self._step_sharded()
+            return
+        self.allreduce_grads()
         if self.grad_clip is not None and self.grad_clip > 0:
             K.grad_sqnorm(self.grad, self.partials)
             parts, mx = self.partials, float(self.grad_clip)
