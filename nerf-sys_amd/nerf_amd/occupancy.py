@@ -214,6 +214,10 @@ class OccGridEstimator(nn.Module):
             cells = torch.empty(self.levels * 2 * n, dtype=torch.int32, device=dev)
             check(L.nerf_occ_sample_cells(ptr(occ_list), ptr(pos), self.levels, cpl, n, ctypes.c_uint64(self._seed()),
                                           ptr(cells), stream()), "nerf_occ_sample_cells")
+            # evaluate the drawn cells in cell order: neighbouring points then share hash-grid vertices at the
+            # coarse levels, so the density's gathers hit the caches (the draws are a set; a duplicated cell's
+            # update stays the last-writer-wins of the reference's index assignment)
+            cells = torch.sort(cells).values
         n = cells.numel()
         x = torch.empty((n, 3), dtype=torch.float32, device=dev)
         check(lib().nerf_occ_cell_points(_addr(self.grid), ptr(cells), n, ctypes.c_uint64(self._seed()), ptr(x),
