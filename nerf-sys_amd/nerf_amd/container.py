@@ -164,7 +164,7 @@ class _BlendFn(torch.autograd.Function):
 MARCH_STAGE_CAP = 512  # staged segments per (expert, ray) pair: K*N*512*8 B (67 MB at 4 x 4096 pairs)
 
 
-def _march_experts(model, rays, sub_params, render_step_size, alpha_thre, cone_angle):
+def _march_experts(model, rays, sub_params, render_step_size, alpha_thre, cone_angle, before_sync=None):
     """Every expert's occupancy marching (MetaNGP.occupancy_marching, meta_ngp.py:384-443, on the rays that hit its
     box, ray_rendering.py:397-422) in ONE launch pair: count -> scan -> ONE host read of the K+1 expert boundaries
     -> write.  In training, the visibility filter (nerfacc render_visibility_from_density with alpha_thre =
@@ -199,6 +199,8 @@ def _march_experts(model, rays, sub_params, render_step_size, alpha_thre, cone_a
     check(L.nerf_occ_march_multi_staged(*args, ptr(counts), ptr(stage), MARCH_STAGE_CAP, None, None, None, None,
                                         stream()), "nerf_occ_march_multi_staged(count)")
     offs = exclusive_scan(counts)
+    if before_sync is not None:
+        before_sync()
     bounds = offs[::N].cpu().tolist()                  # the one host read: K+1 expert boundaries
     M = bounds[-1]
     if M == 0:
@@ -270,12 +272,21 @@ def _render_container_occ(model, rays, params, bg_color_default, chunk, render_s
                   else [None] * K)
     if K > 8:
         raise ValueError("occupancy marching / segment union support at most 8 experts")
+    early = {}
+
+    def before_sync():
+        # host work that needs no marched sizes, issued while the march's count pass runs on the GPU (before the
+        # host read of the packed sizes): each expert's packed MLP (cached for this render) and the background
+        for k, sub in enumerate(model.submodules):
+            if hasattr(sub, "packed"):
+                sub.packed(sub_params[k])
+        early["bg"] = _get_bg_rgb(model, d, params, rays, N, bg_color_default)
+
     ri_all, t0_all, t1_all, offs_all = _march_experts(model, rays, sub_params, render_step_size, alpha_thre,
-                                                      cone_angle)
+                                                      cone_angle, before_sync=before_sync)
     if offs_all is None:
         acc = rays.new_zeros(N)
-        bg_rgb = _get_bg_rgb(model, d, params, rays, N, bg_color_default)
-        return bg_rgb, acc.clone(), torch.zeros(1, 1, device=dev, dtype=rays.dtype), acc
+        return early["bg"], acc.clone(), torch.zeros(1, 1, device=dev, dtype=rays.dtype), acc
     # expert k's segments: offsets[k*N : (k+1)*N + 1] index the shared t0 / t1 arrays
     t0s = (ctypes.c_void_p * K)(*([t0_all.data_ptr()] * K))
     t1s = (ctypes.c_void_p * K)(*([t1_all.data_ptr()] * K))
@@ -308,8 +319,7 @@ def _render_container_occ(model, rays, params, bg_color_default, chunk, render_s
     M, offs = host[0], host[1:]
     if M == 0:
         acc = rays.new_zeros(N)
-        bg_rgb = _get_bg_rgb(model, d, params, rays, N, bg_color_default)
-        return bg_rgb, acc.clone(), torch.zeros(1, 1, device=dev, dtype=rays.dtype), acc
+        return early["bg"], acc.clone(), torch.zeros(1, 1, device=dev, dtype=rays.dtype), acc
     ri, t0, t1, xm, W = ri[:M], t0[:M], t1[:M], xm[:M], W[:M]
     ks, sels, ys = [], [], []
     for k, sub in enumerate(model.submodules):
@@ -323,8 +333,7 @@ def _render_container_occ(model, rays, params, bg_color_default, chunk, render_s
         sels.append(sel)
         ys.append(yk)
     rs = _BlendFn.apply(W, M, sels, ks, *ys)
-    bg = _get_bg_rgb(model, d, params, rays, N, bg_color_default)
-    rgb, depth, w, acc = render_packed(rs, t0, t1, moff, bg)
+    rgb, depth, w, acc = render_packed(rs, t0, t1, moff, early["bg"])
     return rgb, depth, w[:, None], acc
 
 
