@@ -28,6 +28,7 @@ extern "C" {
 #define NERF_E_ALIGN (-2)    /* pointer not 16-byte aligned */
 #define NERF_E_ENUM (-3)     /* unknown enum value */
 #define NERF_E_WORKSPACE (-4)/* workspace too small */
+#define NERF_E_UNSUPPORTED (-5) /* valid arguments, but no kernel for this configuration (use the general path) */
 
 /* ------------------------------------------------------------------ rays */
 
@@ -225,6 +226,12 @@ int nerf_ngp_fwd(const NerfNgpNet* net, const float* w, const float* enc, int en
  * the colour branch is not evaluated. */
 int nerf_ngp_density(const NerfNgpNet* net, const float* w, const float* enc, int enc_stride, int64_t M,
                      float* sigma, hipStream_t stream);
+/* sigma from world points in ONE launch (hash-grid encoding into LDS + sigma trunk + head; bitwise the
+ * nerf_hash_encode + nerf_ngp_density pair) for the production expert shape (16 x 2 hash features, 2 x 64 sigma
+ * trunk, 1 + 15 head, SH degree 4 colour input — MetaNGP's defaults); NERF_E_UNSUPPORTED for other shapes. */
+int nerf_ngp_density_enc(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table, const float* w,
+                         const float* x, int64_t x_stride, int64_t M, const float* aabb, float enc_eps, float* sigma,
+                         hipStream_t stream);
 
 /* Backward of nerf_ngp_fwd (recomputes the forward on chip): d_enc (M rows, pitch enc_stride; cols
  * >= in_dim untouched) and d_w (packed layout; overwritten, or accumulated into if accumulate != 0). */

@@ -214,19 +214,13 @@ __device__ __forceinline__ void load_x01(const HashArgs& a, const float* __restr
 
 // corner weights in the reference's autograd product order: ((g*(1-wz))*(1-wy))*(1-wx) etc.  For the
 // forward the blend is c00 = f000*(1-wx) + f100*wx, ... (no fma contraction: bit-exact with torch).
+// the F features of one level at unit-cube point p (shared by hash_fwd_kernel and the fused density kernel)
 template <int F>
-__global__ void hash_fwd_kernel(HashArgs a, const float* __restrict__ table, const float* __restrict__ x, int64_t xs,
-                                int64_t M, float* __restrict__ out, int os) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t m = gid / a.L;
-  const int l = (int)(gid - m * a.L);
-  if (m >= M) return;
-  float p[3];
-  load_x01(a, x, xs, m, p);
+__device__ __forceinline__ void hash_level(const HashArgs& a, const float* __restrict__ table, const float p[3], int l,
+                                           float acc[F]) {
   const float r = (float)a.res[l];
   const uint32_t mask = (1u << a.log2T) - 1u;
   const float* tb = table + ((int64_t)l << a.log2T) * F;
-  float acc[F];
   if (a.interp == 0) {  // Nearest: torch.round = round half to even
     const int ix = (int)rintf(__fmul_rn(p[0], r)), iy = (int)rintf(__fmul_rn(p[1], r)), iz = (int)rintf(__fmul_rn(p[2], r));
     const float* e = tb + (int64_t)ngp_hash(ix, iy, iz, mask) * F;
@@ -272,6 +266,19 @@ __global__ void hash_fwd_kernel(HashArgs a, const float* __restrict__ table, con
       acc[q] = __fadd_rn(__fmul_rn(c0, uz), __fmul_rn(c1, w[2]));
     }
   }
+}
+
+template <int F>
+__global__ void hash_fwd_kernel(HashArgs a, const float* __restrict__ table, const float* __restrict__ x, int64_t xs,
+                                int64_t M, float* __restrict__ out, int os) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t m = gid / a.L;
+  const int l = (int)(gid - m * a.L);
+  if (m >= M) return;
+  float p[3];
+  load_x01(a, x, xs, m, p);
+  float acc[F];
+  hash_level<F>(a, table, p, l, acc);
   float* o = out + m * os + l * F;
   if (F == 2) {
     *reinterpret_cast<float2*>(o) = make_float2(acc[0], acc[F > 1 ? 1 : 0]);
@@ -1409,6 +1416,49 @@ __global__ __launch_bounds__(256) void ngp_fwd_prod_kernel(const float* __restri
 }
 
 
+// Density straight from world points for the production expert (occupancy-grid updates and the visibility filter's
+// sigma): the hash-grid encoding of the tile's 32 rows is computed into the LDS enc tile (thread t: (row, level)
+// pairs t and t + 256 — 16 levels x 2 features; the same arithmetic as hash_fwd_kernel, so the bits match the
+// two-launch path) and the sigma trunk + head run on it at once: no enc round trip through HBM, and one
+// workgroup's gathers overlap another's MFMAs (six per CU).
+__global__ __launch_bounds__(256) void ngp_density_enc_prod_kernel(HashArgs a, const float* __restrict__ table,
+                                                                   const float* __restrict__ w,
+                                                                   const float* __restrict__ x, int64_t xs,
+                                                                   int64_t M, float* __restrict__ sigma) {
+  using namespace ngp_prod;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int64_t m0 = (int64_t)blockIdx.x * NGP_BROWS;
+  NgpFrag fa, fb;
+  load_frag<0>(w, nullptr, wave, lane, fa);
+  load_frag<1>(w, nullptr, wave, lane, fb);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int pair = tid + 256 * u, r = pair >> 4, l = pair & 15;
+    const int64_t m = m0 + r;
+    float2 v = make_float2(0.f, 0.f);
+    if (m < M && l < a.L) {
+      float p[3], acc[2];
+      load_x01(a, x, xs, m, p);
+      hash_level<2>(a, table, p, l, acc);
+      v = make_float2(acc[0], acc[1]);
+    }
+    *reinterpret_cast<float2*>(smem + F_ENC + r * 36 + 2 * l) = v;
+  }
+  lds_barrier();
+  fwd<0, F_ENC, 36, F_PA>(smem, fa, wave, lane);
+  lds_barrier();
+  load_frag<2>(w, nullptr, wave, lane, fa);
+  fwd<1, F_PA, 68, F_PB>(smem, fb, wave, lane);
+  lds_barrier();
+  fwd<2, F_PB, 68, F_PA>(smem, fa, wave, lane);
+  lds_barrier();
+  if (tid < NGP_BROWS && m0 + tid < M) {
+    const float sr = smem[F_PA + tid * 68];
+    sigma[m0 + tid] = expf(fminf(fmaxf(sr, -nerf_mlp::EXP_MAX), nerf_mlp::EXP_MAX));
+  }
+}
+
 // dw = sum over the workgroup slabs.  A block owns 64 consecutive columns (16 float4) and 16 slab groups: thread
 // (g, c) sums slabs g, g+16, ... of its column in order, then column c's 16 group sums are added in order g = 0..15
 // (deterministic).  One thread per column over all slabs ran at 0.3 TB/s (256 dependent adds per thread).
@@ -1655,6 +1705,28 @@ extern "C" int nerf_ngp_density(const NerfNgpNet* net, const float* w, const flo
   const size_t sm = (size_t)P.smem_floats * 4;
   allow_lds(ngp_density_kernel);
   ngp_density_kernel<<<(unsigned)nerf_cdiv(M, NGP_ROWS), 256, sm, st>>>(P, w, enc, enc_stride, M, sigma);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_ngp_density_enc(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table,
+                                    const float* w, const float* x, int64_t x_stride, int64_t M, const float* aabb,
+                                    float enc_eps, float* sigma, hipStream_t st) {
+  NgpPlan P, Pb;
+  HashArgs a;
+  if (!net || !grid || M < 0 || x_stride < 3 || !make_plan(*net, false, P) || !hash_args(grid, nullptr, a))
+    return NERF_E_ARG;
+  if (a.F != 2 || a.L > 16 || a.L * a.F != net->in_dim || !make_plan(*net, true, Pb) || !is_prod_plan(Pb))
+    return NERF_E_UNSUPPORTED;
+  if (M == 0) return NERF_OK;
+  if (!table || !w || !x || !sigma) return NERF_E_ARG;
+  if (!nerf_aligned16(w) || !nerf_aligned16(table)) return NERF_E_ALIGN;
+  if (aabb) {
+    a.has_aabb = 1;
+    for (int c = 0; c < 3; ++c) { a.mn[c] = aabb[c]; a.ext[c] = aabb[3 + c] - aabb[c]; }
+    a.eps = enc_eps;
+  }
+  ngp_density_enc_prod_kernel<<<(unsigned)nerf_cdiv(M, NGP_BROWS), 256, (size_t)ngp_prod::F_SMEM * 4, st>>>(
+      a, table, w, x, x_stride, M, sigma);
   return nerf_launch_status();
 }
 

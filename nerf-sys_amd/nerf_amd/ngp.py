@@ -135,6 +135,25 @@ def ngp_fwd(net: NerfNgpNet, w_packed, enc, x_d, out=None):
     return out
 
 
+E_UNSUPPORTED = -5
+
+
+def ngp_density_enc(net: NerfNgpNet, grid: NerfHashGrid, table, w_packed, x, aabb=None, enc_eps=1e-6):
+    """nerf_ngp_density_enc: world points (M, >=3) -> sigma (M,) in one launch (encoding in LDS), or None when
+    the expert's shape has no fused kernel (the caller then runs hash_encode + ngp_density)."""
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    M = x.shape[0]
+    out = torch.empty(M, dtype=torch.float32, device=x.device)
+    ab = (ctypes.c_float * 6)(*[float(v) for v in aabb]) if aabb is not None else None
+    rc = lib().nerf_ngp_density_enc(_addr(net), _addr(grid), ptr(table), ptr(w_packed), ptr(x), x.stride(0), M, ab,
+                                    float(enc_eps), ptr(out), stream())
+    if rc == E_UNSUPPORTED:
+        return None
+    check(rc, "nerf_ngp_density_enc")
+    return out
+
+
 def ngp_density(net: NerfNgpNet, w_packed, enc):
     """nerf_ngp_density: enc (M, >=in_dim) -> sigma (M,) (trunk + sigma head only)."""
     M = enc.shape[0]
@@ -554,6 +573,12 @@ class InstantNGP(nn.Module):
         if not (torch.is_grad_enabled() and (w.requires_grad or self.xyz_encoder.hash_table.requires_grad)):
             # no graph needed (visibility filter, occupancy update): sigma branch only
             with torch.no_grad():
+                h = TIMING.start("density_enc", xf.shape[0])
+                sig = ngp_density_enc(self.net_struct, self.xyz_encoder.grid, self.xyz_encoder.hash_table.detach(),
+                                      w.detach(), xf, self._aabb_host, self._eps)
+                TIMING.stop(h)
+                if sig is not None:
+                    return sig.view(*shp, 1)
                 h = TIMING.start("hash_fwd", xf.shape[0])
                 enc = hash_encode(self.xyz_encoder.grid, self.xyz_encoder.hash_table.detach(), xf, self._aabb_host,
                                   self._eps)

@@ -388,3 +388,44 @@ def test_ngp_production_backward_kernel(N, levels, M, monkeypatch):
         tol = 1e-5 * max(1.0, r.abs().max().item())
         assert _err(gp[n].double(), r) <= tol, n
         assert _err(gp[n], gg[n]) <= tol, n
+
+
+@pytest.mark.parametrize("levels,M", [(16, 1), (16, 4097), (8, 50001)])
+def test_density_enc_fused_bitwise(N, levels, M):
+    """nerf_ngp_density_enc (hash encoding into LDS + sigma trunk/head in one launch) is bitwise the two-launch
+    nerf_hash_encode + nerf_ngp_density path, points inside and outside the box."""
+    from nerf_amd import ngp as G
+    from nerf_amd.ngp import InstantNGP
+    torch.manual_seed(9)
+    box = torch.tensor([[-1.5] * 3, [1.5] * 3])
+    net = InstantNGP(scene_box=box, hidden=64, sigma_depth=2, color_hidden=64, color_depth=2,
+                     dir_encoding="spherical",
+                     hash_enc_conf=dict(levels=levels, features_per_level=2, log2_hashmap_size=14, min_res=8,
+                                        max_res=512, interpolation="Linear")).to(DEV)
+    with torch.no_grad():
+        net.xyz_encoder.hash_table.uniform_(-0.5, 0.5)
+    g = torch.Generator().manual_seed(M)
+    x = (torch.rand(M, 3, generator=g) * 3.4 - 1.7).to(DEV)
+    w = net.packed().detach()
+    tab = net.xyz_encoder.hash_table.detach()
+    fused = G.ngp_density_enc(net.net_struct, net.xyz_encoder.grid, tab, w, x, net._aabb_host, net._eps)
+    assert fused is not None
+    enc = G.hash_encode(net.xyz_encoder.grid, tab, x, net._aabb_host, net._eps)
+    ref = G.ngp_density(net.net_struct, w, enc)
+    torch.cuda.synchronize()
+    assert torch.equal(fused.cpu(), ref.reshape(-1).cpu())
+
+
+def test_density_enc_unsupported_shape_falls_back(N):
+    from nerf_amd import ngp as G
+    from nerf_amd.ngp import InstantNGP
+    net = InstantNGP(scene_box=torch.tensor([[-1.0] * 3, [1.0] * 3]), hidden=32, sigma_depth=1, color_hidden=48,
+                     color_depth=3, dir_encoding="frequency",
+                     hash_enc_conf=dict(levels=8, features_per_level=2, log2_hashmap_size=12, min_res=8, max_res=128,
+                                        interpolation="Linear")).to(DEV)
+    x = torch.rand(100, 3, device=DEV)
+    assert G.ngp_density_enc(net.net_struct, net.xyz_encoder.grid, net.xyz_encoder.hash_table.detach(),
+                             net.packed().detach(), x, net._aabb_host, net._eps) is None
+    with torch.no_grad():
+        s = net.density(x)  # the two-launch path
+    assert s.shape == (100, 1) and torch.isfinite(s).all()
