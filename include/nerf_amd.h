@@ -229,6 +229,12 @@ int nerf_ngp_density(const NerfNgpNet* net, const float* w, const float* enc, in
 /* sigma from world points in ONE launch (hash-grid encoding into LDS + sigma trunk + head; bitwise the
  * nerf_hash_encode + nerf_ngp_density pair) for the production expert shape (16 x 2 hash features, 2 x 64 sigma
  * trunk, 1 + 15 head, SH degree 4 colour input — MetaNGP's defaults); NERF_E_UNSUPPORTED for other shapes. */
+/* the expert's forward in ONE launch for the production shape: hash encoding of x_d's positions into LDS (also
+ * written to enc [M][enc_stride] for nerf_ngp_bwd, bitwise nerf_hash_encode's) + the fused MLP -> rgb_sigma (bitwise
+ * nerf_ngp_fwd's); NERF_E_UNSUPPORTED for other shapes. */
+int nerf_ngp_fwd_enc(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table, const float* w,
+                     const float* x_d, int64_t M, const float* aabb, float enc_eps, float* enc, int enc_stride,
+                     float* rgb_sigma, hipStream_t stream);
 int nerf_ngp_density_enc(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table, const float* w,
                          const float* x, int64_t x_stride, int64_t M, const float* aabb, float enc_eps, float* sigma,
                          hipStream_t stream);

@@ -1335,10 +1335,15 @@ namespace ngp_prod {
 constexpr int F_ENC = 0, F_CIN = 1152, F_PA = 2304, F_PB = 4480, F_SRAW = 6656, F_SMEM = 6688;
 }
 
-template <int MODE, int SIGMOID>
+// HASH: the enc tile is computed from the sample positions (x_d cols 0..2) in the prologue — the hash_fwd_kernel
+// arithmetic, (row, level) pairs t and t + 256 — and also written to enc [M][es] for the backward (one launch for the
+// expert's encoding + MLP forward, the gathers of one workgroup overlapping another's MFMAs); else read from enc.
+template <int MODE, int SIGMOID, bool HASH = false>
 __global__ __launch_bounds__(256) void ngp_fwd_prod_kernel(const float* __restrict__ w, const float* __restrict__ enc,
                                                            int es, int in_dim, const float* __restrict__ x_d,
-                                                           int64_t M, float* __restrict__ out) {
+                                                           int64_t M, float* __restrict__ out, HashArgs ha = HashArgs{},
+                                                           const float* __restrict__ table = nullptr,
+                                                           float* __restrict__ enc_out = nullptr) {
   using namespace ngp_prod;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -1348,12 +1353,33 @@ __global__ __launch_bounds__(256) void ngp_fwd_prod_kernel(const float* __restri
   NgpFrag fa, fb;
   load_frag<0>(w, nullptr, wave, lane, fa);
   {
-    float* erow = smem + F_ENC + pr * 36;
+    if constexpr (HASH) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = pp + 8 * i;
-      const float v = enc[mc * es + (c < in_dim ? c : 0)];
-      erow[c] = (ok && c < in_dim) ? v : 0.f;
+      for (int u = 0; u < 2; ++u) {
+        const int pair = tid + 256 * u, r = pair >> 4, l = pair & 15;
+        const int64_t mr = m0 + r;
+        float2 v = make_float2(0.f, 0.f);
+        if (mr < M && l < ha.L) {
+          float p[3], acc[2];
+          load_x01(ha, x_d, 6, mr, p);
+          hash_level<2>(ha, table, p, l, acc);
+          v = make_float2(acc[0], acc[1]);
+          *reinterpret_cast<float2*>(enc_out + mr * es + 2 * l) = v;
+        }
+        *reinterpret_cast<float2*>(smem + F_ENC + r * 36 + 2 * l) = v;
+      }
+      for (int i = tid; i < NGP_BROWS * (es - 2 * ha.L); i += 256) {  // enc pad columns, as hash_fwd_kernel
+        const int r = i / (es - 2 * ha.L), c = 2 * ha.L + i % (es - 2 * ha.L);
+        if (m0 + r < M) enc_out[(m0 + r) * es + c] = 0.f;
+      }
+    } else {
+      float* erow = smem + F_ENC + pr * 36;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = pp + 8 * i;
+        const float v = enc[mc * es + (c < in_dim ? c : 0)];
+        erow[c] = (ok && c < in_dim) ? v : 0.f;
+      }
     }
     if constexpr (MODE == 0) {
       const float* dr = x_d + mc * 6 + 3;
@@ -1727,6 +1753,36 @@ extern "C" int nerf_ngp_density_enc(const NerfNgpNet* net, const NerfHashGrid* g
   }
   ngp_density_enc_prod_kernel<<<(unsigned)nerf_cdiv(M, NGP_BROWS), 256, (size_t)ngp_prod::F_SMEM * 4, st>>>(
       a, table, w, x, x_stride, M, sigma);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_ngp_fwd_enc(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table,
+                                const float* w, const float* x_d, int64_t M, const float* aabb, float enc_eps,
+                                float* enc, int enc_stride, float* rgb_sigma, hipStream_t st) {
+  NgpPlan P, Pb;
+  HashArgs a;
+  if (!net || !grid || M < 0 || !make_plan(*net, false, P) || !hash_args(grid, nullptr, a)) return NERF_E_ARG;
+  if (enc_stride < a.L * a.F) return NERF_E_ARG;
+  if (a.F != 2 || a.L > 16 || a.L * a.F != net->in_dim || !make_plan(*net, true, Pb) || !is_prod_plan(Pb))
+    return NERF_E_UNSUPPORTED;
+  if (M == 0) return NERF_OK;
+  if (!table || !w || !x_d || !enc || !rgb_sigma) return NERF_E_ARG;
+  if (!nerf_aligned16(w) || !nerf_aligned16(table) || !nerf_aligned16(rgb_sigma) || (enc_stride % 2) ||
+      !nerf_aligned16(enc))
+    return NERF_E_ALIGN;
+  if (aabb) {
+    a.has_aabb = 1;
+    for (int c = 0; c < 3; ++c) { a.mn[c] = aabb[c]; a.ext[c] = aabb[3 + c] - aabb[c]; }
+    a.eps = enc_eps;
+  }
+  const unsigned blocks = (unsigned)nerf_cdiv(M, NGP_BROWS);
+  const size_t smp = (size_t)ngp_prod::F_SMEM * 4;
+  if (P.sigmoid)
+    ngp_fwd_prod_kernel<0, 1, true><<<blocks, 256, smp, st>>>(w, nullptr, enc_stride, P.in_dim, x_d, M, rgb_sigma, a,
+                                                                table, enc);
+  else
+    ngp_fwd_prod_kernel<0, 0, true><<<blocks, 256, smp, st>>>(w, nullptr, enc_stride, P.in_dim, x_d, M, rgb_sigma, a,
+                                                                table, enc);
   return nerf_launch_status();
 }
 

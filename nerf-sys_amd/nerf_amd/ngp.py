@@ -138,6 +138,23 @@ def ngp_fwd(net: NerfNgpNet, w_packed, enc, x_d, out=None):
 E_UNSUPPORTED = -5
 
 
+def ngp_fwd_enc(net: NerfNgpNet, grid: NerfHashGrid, table, w_packed, x_d, aabb=None, enc_eps=1e-6):
+    """nerf_ngp_fwd_enc: x_d (M, 6) -> (rgb_sigma (M, 4), enc (M, L*F)) in one launch, or None when the expert's
+    shape has no fused kernel (the caller then runs hash_encode + ngp_fwd)."""
+    x_d = x_d.contiguous()
+    M = x_d.shape[0]
+    od = grid.levels * grid.features_per_level
+    enc = torch.empty((M, od), dtype=torch.float32, device=x_d.device)
+    out = torch.empty((M, 4), dtype=torch.float32, device=x_d.device)
+    ab = (ctypes.c_float * 6)(*[float(v) for v in aabb]) if aabb is not None else None
+    rc = lib().nerf_ngp_fwd_enc(_addr(net), _addr(grid), ptr(table), ptr(w_packed), ptr(x_d), M, ab, float(enc_eps),
+                                ptr(enc), od, ptr(out), stream())
+    if rc == E_UNSUPPORTED:
+        return None
+    check(rc, "nerf_ngp_fwd_enc")
+    return out, enc
+
+
 def ngp_density_enc(net: NerfNgpNet, grid: NerfHashGrid, table, w_packed, x, aabb=None, enc_eps=1e-6):
     """nerf_ngp_density_enc: world points (M, >=3) -> sigma (M,) in one launch (encoding in LDS), or None when
     the expert's shape has no fused kernel (the caller then runs hash_encode + ngp_density)."""
@@ -423,12 +440,21 @@ class _NgpFn(torch.autograd.Function):
     def forward(ctx, x_d, table, w_packed, model):
         x_d = x_d.contiguous().float()
         M = x_d.shape[0]
-        h = TIMING.start("hash_fwd", M)
-        enc = hash_encode(model.xyz_encoder.grid, table.detach(), x_d, model._aabb_host, model._eps)
-        TIMING.stop(h)
-        h = TIMING.start("mlp_fwd", M)
-        out = ngp_fwd(model.net_struct, w_packed, enc, x_d) if M else x_d.new_empty((0, 4))
-        TIMING.stop(h)
+        fused = None
+        if M:
+            h = TIMING.start("fwd_enc", M)
+            fused = ngp_fwd_enc(model.net_struct, model.xyz_encoder.grid, table.detach(), w_packed, x_d,
+                                model._aabb_host, model._eps)
+            TIMING.stop(h)
+        if fused is not None:
+            out, enc = fused
+        else:
+            h = TIMING.start("hash_fwd", M)
+            enc = hash_encode(model.xyz_encoder.grid, table.detach(), x_d, model._aabb_host, model._eps)
+            TIMING.stop(h)
+            h = TIMING.start("mlp_fwd", M)
+            out = ngp_fwd(model.net_struct, w_packed, enc, x_d) if M else x_d.new_empty((0, 4))
+            TIMING.stop(h)
         ctx.model = model
         ctx.rows = table.shape[0]
         ctx.table = table  # the parameter itself: FlatAdam-owned tables take their gradient in place

@@ -94,12 +94,18 @@ class NGPTrainer:
         self.gbuf.zero_()
         t = K.sample_stratified(rays, self.S, True, u_strat, seed)
         xd = K.build_xd(rays, t)
-        e = self._ev("hash_fwd")
-        enc = G.hash_encode(m.xyz_encoder.grid, self.table(), xd, m._aabb_host, m._eps)
+        e = self._ev("fwd_enc")  # hash encoding + MLP forward in one launch (production shape)
+        fused = G.ngp_fwd_enc(m.net_struct, m.xyz_encoder.grid, self.table(), self.w(), xd, m._aabb_host, m._eps)
         self._end(e)
-        e = self._ev("mlp_fwd")
-        rs = G.ngp_fwd(m.net_struct, self.w(), enc, xd)
-        self._end(e)
+        if fused is not None:
+            rs, enc = fused
+        else:
+            e = self._ev("hash_fwd")
+            enc = G.hash_encode(m.xyz_encoder.grid, self.table(), xd, m._aabb_host, m._eps)
+            self._end(e)
+            e = self._ev("mlp_fwd")
+            rs = G.ngp_fwd(m.net_struct, self.w(), enc, xd)
+            self._end(e)
         _, _, _, _, _, drgb = K.composite_fwd(rs, t, bg, 1.0, gt=gt, color_space=self.color_space,
                                               inv_count=inv_count, loss_sum=self.loss_buf)
         d_rs = K.composite_bwd(rs, t, bg, drgb)

@@ -429,3 +429,30 @@ def test_density_enc_unsupported_shape_falls_back(N):
     with torch.no_grad():
         s = net.density(x)  # the two-launch path
     assert s.shape == (100, 1) and torch.isfinite(s).all()
+
+
+@pytest.mark.parametrize("levels,M", [(16, 1), (16, 4097), (8, 50001)])
+def test_fwd_enc_fused_bitwise(N, levels, M):
+    """nerf_ngp_fwd_enc (encoding into LDS and to HBM + the fused MLP forward in one launch) is bitwise the
+    nerf_hash_encode + nerf_ngp_fwd pair: rgb_sigma and the enc the backward reads."""
+    from nerf_amd import ngp as G
+    from nerf_amd.ngp import InstantNGP
+    torch.manual_seed(10)
+    box = torch.tensor([[-1.5] * 3, [1.5] * 3])
+    net = InstantNGP(scene_box=box, hidden=64, sigma_depth=2, color_hidden=64, color_depth=2,
+                     dir_encoding="spherical",
+                     hash_enc_conf=dict(levels=levels, features_per_level=2, log2_hashmap_size=14, min_res=8,
+                                        max_res=512, interpolation="Linear")).to(DEV)
+    with torch.no_grad():
+        net.xyz_encoder.hash_table.uniform_(-0.5, 0.5)
+    g = torch.Generator().manual_seed(M + 1)
+    x_d = torch.cat([torch.rand(M, 3, generator=g) * 3.4 - 1.7,
+                     torch.nn.functional.normalize(torch.randn(M, 3, generator=g), dim=-1)], -1).to(DEV)
+    w = net.packed().detach()
+    tab = net.xyz_encoder.hash_table.detach()
+    out, enc = G.ngp_fwd_enc(net.net_struct, net.xyz_encoder.grid, tab, w, x_d, net._aabb_host, net._eps)
+    enc_ref = G.hash_encode(net.xyz_encoder.grid, tab, x_d, net._aabb_host, net._eps)
+    out_ref = G.ngp_fwd(net.net_struct, w, enc_ref, x_d)
+    torch.cuda.synchronize()
+    assert torch.equal(enc.cpu(), enc_ref.cpu())
+    assert torch.equal(out.cpu(), out_ref.cpu())

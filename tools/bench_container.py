@@ -195,7 +195,7 @@ def main():
     # bwd 12 + L*F*4 + 2*8*L*F*4 (atomic read-modify-write)
     L, F = 16, 2
     bps = {"hash_fwd": 12 + 8 * L * F * 4 + L * F * 4, "hash_bwd": 12 + L * F * 4 + 2 * 8 * L * F * 4}
-    hk = max(bps, key=lambda k: ms.get(k, 0.0))
+    hk = max((k for k in bps if k in per), key=lambda k: ms.get(k, 0.0))
     tot_ms = sum(t for t, _ in per[hk])
     ach = bps[hk] * rows[hk] / (tot_ms * 1e-3) / 1e9
     roof = {"bound": "hbm", "kernel": hk, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -215,7 +215,7 @@ def main():
         "mean_launch_ms": {k: round(v, 4) for k, v in launch.items()},
         "dominant": dom,
         "roofline": roof,
-        "samples_per_step": round(rows.get("mlp_fwd", 0) / a.steps),
+        "samples_per_step": round((rows.get("fwd_enc", 0) + rows.get("mlp_fwd", 0)) / a.steps),
         "final_loss": round(float(loss.item()), 6),
     }
     out["cpu_baseline"] = None if (a.no_cpu_baseline or world > 1) else cpu_baseline(a.cpu_seconds)

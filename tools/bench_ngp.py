@@ -131,7 +131,7 @@ def main():
     # bwd reads d_enc L*F fp32 and read-modify-writes 8 x L x F fp32 in the table gradient
     by = {"hash_fwd": M * (12 + 8 * L * F * 4 + L * F * 4),
           "hash_bwd": M * (12 + L * F * 4 + 2 * 8 * L * F * 4)}
-    dom = max(("hash_fwd", "hash_bwd"), key=lambda k: ms[k])
+    dom = max((k for k in ("hash_fwd", "hash_bwd") if k in ms), key=lambda k: ms[k])
     ach = by[dom] / (ms[dom] * 1e-3) / 1e9
     # the table-gradient scatter is bound by the memory-side float-atomic unit, not by HBM bytes: count the 64-B
     # atomic requests hash_bwd issues for one step's sample positions (tools/hash_requests.py)
