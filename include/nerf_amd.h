@@ -244,6 +244,13 @@ int nerf_ngp_density_enc(const NerfNgpNet* net, const NerfHashGrid* grid, const 
 int nerf_ngp_bwd(const NerfNgpNet* net, const float* w, const float* enc, int enc_stride, const float* x_d,
                  int64_t M, const float* d_rgb_sigma, float* d_enc, float* d_w, int accumulate, void* ws,
                  int64_t ws_bytes, hipStream_t stream);
+/* nerf_ngp_bwd + nerf_hash_encode_bwd(d_table += ...) in ONE launch for the production expert shape with a
+ * Linear / Smoothstep F = 2 grid (d_enc never leaves the chip; the table scatter runs beside the MLP backward);
+ * NERF_E_UNSUPPORTED otherwise.  d_table accumulates (atomics), d_w as nerf_ngp_bwd. */
+int nerf_ngp_bwd_hash(const NerfNgpNet* net, const NerfHashGrid* grid, const float* w, const float* enc,
+                      int enc_stride, const float* x_d, int64_t M, const float* d_rgb_sigma, const float* aabb,
+                      float enc_eps, float* d_table, float* d_w, int accumulate, void* ws, int64_t ws_bytes,
+                      hipStream_t stream);
 
 /* ------------------------------------------------------------------ MoE container */
 

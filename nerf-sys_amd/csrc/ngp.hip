@@ -1107,7 +1107,7 @@ __device__ __forceinline__ void fwd(float* smem, const NgpFrag& f, int wave, int
   }
 }
 
-template <int l>
+template <int l, bool ENC_TO_LDS = false>
 __device__ __forceinline__ void dgrad(float* smem, const NgpFrag& f, int wave, int lane, float* __restrict__ d_enc,
                                       int es, int in_dim, int64_t m0, int64_t M) {
   constexpr int NRB = KP[l] == 64 ? 2 : 1;
@@ -1120,7 +1120,9 @@ __device__ __forceinline__ void dgrad(float* smem, const NgpFrag& f, int wave, i
   for (int b = 0; b < NRB; ++b) {
     const int r = 16 * (rb0 + b) + c16;
     float v0 = acc[b].x, v1 = acc[b].y, v2 = acc[b].z, v3 = acc[b].w;
-    if constexpr (l == 0) {
+    if constexpr (l == 0 && ENC_TO_LDS) {  // d_enc tile -> the free gradient tile (G1) for the fused table scatter
+      *reinterpret_cast<float4*>(smem + G1 + r * 68 + k0) = make_float4(v0, v1, v2, v3);
+    } else if constexpr (l == 0) {
       const int64_t m = m0 + r;
       if (m < M) {
         float* o = d_enc + m * es + k0;
@@ -1184,13 +1186,18 @@ __device__ __forceinline__ void load_tile_in(const float* __restrict__ enc, int 
 
 }  // namespace ngp_prod
 
-template <int SIGMOID>
+// HB: the hash-table gradient is scattered from the kernel itself — d_enc of a tile goes to LDS (never to HBM) and
+// the four waves issue hash_bwd_f2_agg_kernel's run-aggregated atomics for it (wave w: samples 16 (w & 1) .. + 15 of
+// the tile, levels 8 (w >> 1) .. + 7; the same 16-consecutive-sample grouping, so the same request count), while the
+// other workgroup on the CU runs its MFMAs: the MLP backward hides under the memory-side atomic traffic.
+template <int SIGMOID, bool HB = false>
 __global__ __launch_bounds__(256, 2) void ngp_bwd_prod_kernel(const float* __restrict__ w, const float* __restrict__ wt,
                                                               const float* __restrict__ enc, int es, int in_dim,
                                                               const float* __restrict__ x_d, int64_t M,
                                                               const float* __restrict__ gout,
                                                               float* __restrict__ d_enc, float* __restrict__ partial,
-                                                              int64_t ntiles) {
+                                                              int64_t ntiles, HashArgs ha = HashArgs{},
+                                                              float* __restrict__ dtab = nullptr) {
   using namespace ngp_prod;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1285,8 +1292,62 @@ __global__ __launch_bounds__(256, 2) void ngp_bwd_prod_kernel(const float* __res
           for (int r = 0; r < 8; ++r) sum += gcol[r * 68];
           bacc[l] += sum;
         }
-        dgrad<l>(smem, use, wave, lane, d_enc, es, in_dim, m0, M);
+        dgrad<l, HB>(smem, use, wave, lane, d_enc, es, in_dim, m0, M);
         lds_barrier();
+        if constexpr (HB && l == 0) {
+          // table scatter of this tile (hash_bwd_f2_agg_kernel's lanes: q = (x-corner, feature), 16 samples)
+          const int q = lane & 3, grp = lane >> 2;
+          const int r = 16 * (wave & 1) + grp;
+          const int64_t m = m0 + r;
+          const bool valid = m < M;
+          float p[3] = {0.f, 0.f, 0.f};
+          if (valid) load_x01(ha, x_d, 6, m, p);
+          const uint32_t mask = (1u << ha.log2T) - 1u;
+          const int dx = q >> 1, f = q & 1;
+          const unsigned long long qmask = 0x1111111111111111ull << q;
+          const unsigned long long after = lane == 63 ? 0ull : ~((2ull << lane) - 1ull);
+          const float* drow = smem + G1 + r * 68;
+          // a fixed count of 32 atomic instructions per wave (8 levels x 4 corners, lanes masked): with a variable
+          // count the compiler would wait for the next tile's first weight fragments with vmcnt(0), behind them
+#pragma unroll
+          for (int li2 = 0; li2 < 8; ++li2) {
+            const int l2 = 8 * (wave >> 1) + li2;
+            const bool lvalid = valid && l2 < ha.L;
+            const float rr = (float)ha.res[l2 < ha.L ? l2 : 0];
+            float wv[3];
+            int i0[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              const float sc = __fmul_rn(p[c], rr);
+              const float fl = floorf(sc);
+              wv[c] = __fsub_rn(sc, fl);
+              i0[c] = (int)fl;
+              if (ha.interp == 2) wv[c] = __fmul_rn(__fmul_rn(wv[c], wv[c]), __fsub_rn(3.0f, __fmul_rn(2.0f, wv[c])));
+            }
+            const float u[3] = {__fsub_rn(1.0f, wv[0]), __fsub_rn(1.0f, wv[1]), __fsub_rn(1.0f, wv[2])};
+            const float wx = dx ? wv[0] : u[0];
+            const float gg = lvalid ? drow[2 * l2 + f] : 0.f;
+            float* tb = dtab + ((int64_t)l2 << ha.log2T) * 2;
+#pragma unroll
+            for (int yz = 0; yz < 4; ++yz) {
+              const int dy = yz >> 1, dz = yz & 1;
+              const float v = __fmul_rn(__fmul_rn(__fmul_rn(gg, dz ? wv[2] : u[2]), dy ? wv[1] : u[1]), wx);
+              const uint32_t idx = lvalid ? ngp_hash(i0[0] + dx, i0[1] + dy, i0[2] + dz, mask) * 2u + (uint32_t)f
+                                          : 0xFFFFFFFFu;
+              const uint32_t prev = __shfl_up(idx, 4, 64);
+              const bool head = grp == 0 || prev != idx;
+              const unsigned long long nxt = __ballot(head) & qmask & after;
+              const int run_end = nxt ? (int)__builtin_ctzll(nxt) - 4 : 60 + q;
+              float sum = v;
+#pragma unroll
+              for (int off = 4; off < 64; off <<= 1) {
+                const float o = __shfl_down(sum, off, 64);
+                if (lane + off <= run_end) sum += o;
+              }
+              if (head && lvalid) unsafeAtomicAdd(tb + idx, sum);
+            }
+          }
+        }
         if constexpr (l == HEAD + 1) {
           // GNB holds d cin: the head's gradient is [d sigma_raw, d geo, 0...] (thread (r, p): columns 4p..4p+3)
           const float* dc = smem + GNB[l] + pr * 68;
@@ -1829,6 +1890,53 @@ extern "C" int nerf_ngp_bwd(const NerfNgpNet* net, const float* w, const float* 
   else
     ngp_bwd_kernel<8><<<grid, 256, sm, st>>>(P, w, enc, enc_stride, x_d, M, d_rgb_sigma, d_enc, partial, wt,
                                                  ntiles);
+  }
+  const unsigned rblocks = (unsigned)nerf_cdiv(P.total / 4, RED_COLS4);
+  if (nerf_aligned16(d_w))
+    ngp_reduce_kernel<true><<<rblocks, 256, 0, st>>>(partial, P.total, grid, d_w, accumulate);
+  else
+    ngp_reduce_kernel<false><<<rblocks, 256, 0, st>>>(partial, P.total, grid, d_w, accumulate);
+  return nerf_launch_status();
+}
+
+// nerf_ngp_bwd + nerf_hash_encode_bwd in one launch for the production shape with a linear / smoothstep F = 2 grid:
+// the table gradient is scatter-added into d_table from inside the MLP backward (no d_enc in HBM).
+extern "C" int nerf_ngp_bwd_hash(const NerfNgpNet* net, const NerfHashGrid* hgrid, const float* w, const float* enc,
+                                 int enc_stride, const float* x_d, int64_t M, const float* d_rgb_sigma,
+                                 const float* aabb, float enc_eps, float* d_table, float* d_w, int accumulate,
+                                 void* ws, int64_t ws_bytes, hipStream_t st) {
+  NgpPlan P;
+  HashArgs a;
+  if (!net || !hgrid || !d_w || M < 0 || !make_plan(*net, true, P) || enc_stride < net->in_dim ||
+      !hash_args(hgrid, nullptr, a))
+    return NERF_E_ARG;
+  if (a.F != 2 || a.interp == 0 || a.L > 16 || a.L * a.F != net->in_dim || !is_prod_plan(P)) return NERF_E_UNSUPPORTED;
+  if (M == 0) {
+    if (!accumulate) (void)hipMemsetAsync(d_w, 0, P.total * sizeof(float), st);
+    return nerf_launch_status();
+  }
+  if (!w || !enc || !x_d || !d_rgb_sigma || !d_table || !ws) return NERF_E_ARG;
+  if (!nerf_aligned16(w) || !nerf_aligned16(d_rgb_sigma) || !nerf_aligned16(ws)) return NERF_E_ALIGN;
+  if (aabb) {
+    a.has_aabb = 1;
+    for (int c = 0; c < 3; ++c) { a.mn[c] = aabb[c]; a.ext[c] = aabb[3 + c] - aabb[c]; }
+    a.eps = enc_eps;
+  }
+  const int grid = bwd_grid(M);
+  if (ws_bytes < ((int64_t)grid + 1) * P.total * 4) return NERF_E_WORKSPACE;
+  const int64_t ntiles = nerf_cdiv(M, NGP_BROWS);
+  float* partial = reinterpret_cast<float*>(ws);
+  float* wt = partial + (int64_t)grid * P.total;
+  ngp_wt_kernel<<<P.nl, 256, 0, st>>>(P, w, wt);
+  const size_t smp = (size_t)ngp_prod::SMEM * 4;
+  if (P.sigmoid) {
+    allow_lds(ngp_bwd_prod_kernel<1, true>);
+    ngp_bwd_prod_kernel<1, true><<<grid, 256, smp, st>>>(w, wt, enc, enc_stride, P.in_dim, x_d, M, d_rgb_sigma,
+                                                           nullptr, partial, ntiles, a, d_table);
+  } else {
+    allow_lds(ngp_bwd_prod_kernel<0, true>);
+    ngp_bwd_prod_kernel<0, true><<<grid, 256, smp, st>>>(w, wt, enc, enc_stride, P.in_dim, x_d, M, d_rgb_sigma,
+                                                           nullptr, partial, ntiles, a, d_table);
   }
   const unsigned rblocks = (unsigned)nerf_cdiv(P.total / 4, RED_COLS4);
   if (nerf_aligned16(d_w))

@@ -207,6 +207,24 @@ def ngp_bwd(net: NerfNgpNet, w_packed, enc, x_d, d_rgb_sigma, d_enc=None, d_w=No
     return d_enc, d_w
 
 
+def ngp_bwd_hash(net: NerfNgpNet, grid: NerfHashGrid, w_packed, enc, x_d, d_rgb_sigma, d_table, aabb=None,
+                 enc_eps=1e-6, d_w=None, accumulate=False):
+    """nerf_ngp_bwd_hash: MLP backward + table scatter (d_table += ...) in one launch -> d_w, or None when the
+    expert's shape has no fused kernel (the caller then runs ngp_bwd + hash_encode_bwd)."""
+    M = x_d.shape[0]
+    if d_w is None:
+        d_w = torch.empty_like(w_packed)
+    ws = ngp_workspace(net, M, x_d.device)
+    ab = (ctypes.c_float * 6)(*[float(v) for v in aabb]) if aabb is not None else None
+    rc = lib().nerf_ngp_bwd_hash(_addr(net), _addr(grid), ptr(w_packed), ptr(enc), enc.stride(0), ptr(x_d), M,
+                                 ptr(d_rgb_sigma), ab, float(enc_eps), ptr(d_table), ptr(d_w), int(accumulate),
+                                 ptr(ws), ws.numel(), stream())
+    if rc == E_UNSUPPORTED:
+        return None
+    check(rc, "nerf_ngp_bwd_hash")
+    return d_w
+
+
 # ------------------------------------------------------------------------------------------ encoders
 
 def level_resolutions(levels, min_res, max_res):
@@ -471,10 +489,23 @@ class _NgpFn(torch.autograd.Function):
         g = g.contiguous().float()
         if x_d.shape[0] == 0:
             return None, torch.zeros_like(model.xyz_encoder.hash_table), torch.zeros_like(w_packed), None
+        d_table = None
+        if ctx.needs_input_grad[1]:
+            # MLP backward + table scatter in one launch (production shape): straight into a FlatAdam-owned
+            # table's .grad view, else into a fresh zero gradient
+            t = ctx.table
+            flat = getattr(t, "_nerf_flat_grad", False) and t.grad is not None
+            tgt = t.grad if flat else torch.zeros((ctx.rows, model.xyz_encoder.grid.features_per_level),
+                                                  dtype=torch.float32, device=x_d.device)
+            h = TIMING.start("bwd_hash", x_d.shape[0])
+            d_w = ngp_bwd_hash(model.net_struct, model.xyz_encoder.grid, w_packed, enc, x_d, g, tgt,
+                               model._aabb_host, model._eps)
+            TIMING.stop(h)
+            if d_w is not None:
+                return None, (None if flat else tgt), d_w, None
         h = TIMING.start("mlp_bwd", x_d.shape[0])
         d_enc, d_w = ngp_bwd(model.net_struct, w_packed, enc, x_d, g)
         TIMING.stop(h)
-        d_table = None
         if ctx.needs_input_grad[1]:
             h = TIMING.start("hash_bwd", x_d.shape[0])
             t = ctx.table

@@ -109,13 +109,19 @@ class NGPTrainer:
         _, _, _, _, _, drgb = K.composite_fwd(rs, t, bg, 1.0, gt=gt, color_space=self.color_space,
                                               inv_count=inv_count, loss_sum=self.loss_buf)
         d_rs = K.composite_bwd(rs, t, bg, drgb)
-        e = self._ev("mlp_bwd")
-        d_enc, _ = G.ngp_bwd(m.net_struct, self.w(), enc, xd, d_rs, d_w=self.grads[self.T:])
+        e = self._ev("bwd_hash")  # MLP backward + table scatter in one launch (production shape)
+        fused = G.ngp_bwd_hash(m.net_struct, m.xyz_encoder.grid, self.w(), enc, xd, d_rs,
+                               self.grads[: self.T].view(-1, self.F), m._aabb_host, m._eps,
+                               d_w=self.grads[self.T:])
         self._end(e)
-        e = self._ev("hash_bwd")
-        G.hash_encode_bwd(m.xyz_encoder.grid, xd, d_enc, 0, m._aabb_host, m._eps,
-                          d_table=self.grads[: self.T].view(-1, self.F))
-        self._end(e)
+        if fused is None:
+            e = self._ev("mlp_bwd")
+            d_enc, _ = G.ngp_bwd(m.net_struct, self.w(), enc, xd, d_rs, d_w=self.grads[self.T:])
+            self._end(e)
+            e = self._ev("hash_bwd")
+            G.hash_encode_bwd(m.xyz_encoder.grid, xd, d_enc, 0, m._aabb_host, m._eps,
+                              d_table=self.grads[: self.T].view(-1, self.F))
+            self._end(e)
         allreduce_flat(self.gbuf, self.world_size)
         self.step_count += 1
         if self.grad_clip is not None and self.grad_clip > 0:

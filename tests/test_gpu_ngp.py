@@ -456,3 +456,38 @@ def test_fwd_enc_fused_bitwise(N, levels, M):
     torch.cuda.synchronize()
     assert torch.equal(enc.cpu(), enc_ref.cpu())
     assert torch.equal(out.cpu(), out_ref.cpu())
+
+
+@pytest.mark.parametrize("levels,M", [(16, 33), (16, 40000), (8, 7777)])
+def test_bwd_hash_fused_vs_pair(N, levels, M):
+    """nerf_ngp_bwd_hash (MLP backward + the table scatter from inside the kernel) against nerf_ngp_bwd +
+    nerf_hash_encode_bwd: d_w bitwise (the same MLP backward and reduce), d_table the same fp32 terms added by
+    atomics in another order (within 1e-6 of scale), accumulating into a non-zero target."""
+    from nerf_amd import ngp as G
+    from nerf_amd.ngp import InstantNGP
+    torch.manual_seed(12)
+    box = torch.tensor([[-1.5] * 3, [1.5] * 3])
+    net = InstantNGP(scene_box=box, hidden=64, sigma_depth=2, color_hidden=64, color_depth=2,
+                     dir_encoding="spherical",
+                     hash_enc_conf=dict(levels=levels, features_per_level=2, log2_hashmap_size=14, min_res=8,
+                                        max_res=512, interpolation="Linear")).to(DEV)
+    with torch.no_grad():
+        net.xyz_encoder.hash_table.uniform_(-0.5, 0.5)
+    g = torch.Generator().manual_seed(M + 2)
+    x_d = torch.cat([torch.rand(M, 3, generator=g) * 3.4 - 1.7,
+                     torch.nn.functional.normalize(torch.randn(M, 3, generator=g), dim=-1)], -1).to(DEV)
+    gout = torch.randn(M, 4, generator=g).to(DEV)
+    w = net.packed().detach()
+    tab = net.xyz_encoder.hash_table.detach()
+    enc = G.hash_encode(net.xyz_encoder.grid, tab, x_d, net._aabb_host, net._eps)
+    base = torch.randn(tab.shape, generator=g).to(DEV) * 1e-3
+    dt_f = base.clone()
+    dw_f = G.ngp_bwd_hash(net.net_struct, net.xyz_encoder.grid, w, enc, x_d, gout, dt_f, net._aabb_host, net._eps)
+    assert dw_f is not None
+    d_enc, dw_p = G.ngp_bwd(net.net_struct, w, enc, x_d, gout)
+    dt_p = base.clone()
+    G.hash_encode_bwd(net.xyz_encoder.grid, x_d, d_enc, tab.shape[0], net._aabb_host, net._eps, d_table=dt_p)
+    torch.cuda.synchronize()
+    assert torch.equal(dw_f.cpu(), dw_p.cpu())
+    scale = float(dt_p.abs().max())
+    assert float((dt_f - dt_p).abs().max()) <= 1e-6 * scale

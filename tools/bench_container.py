@@ -195,6 +195,8 @@ def main():
     # bwd 12 + L*F*4 + 2*8*L*F*4 (atomic read-modify-write)
     L, F = 16, 2
     bps = {"hash_fwd": 12 + 8 * L * F * 4 + L * F * 4, "hash_bwd": 12 + L * F * 4 + 2 * 8 * L * F * 4}
+    # the fused launches of the production shape: the same gathers / atomics on their HBM side
+    bps.update(fwd_enc=bps["hash_fwd"], density_enc=bps["hash_fwd"], bwd_hash=bps["hash_bwd"])
     hk = max((k for k in bps if k in per), key=lambda k: ms.get(k, 0.0))
     tot_ms = sum(t for t, _ in per[hk])
     ach = bps[hk] * rows[hk] / (tot_ms * 1e-3) / 1e9

@@ -129,26 +129,30 @@ def main():
     M = a.batch * a.samples
     # algorithmic bytes per sample: positions 12 B; fwd gathers 8 corners x L x F fp32 + writes L*F fp32;
     # bwd reads d_enc L*F fp32 and read-modify-writes 8 x L x F fp32 in the table gradient
+    # (fwd_enc / bwd_hash: the fused launches of the production shape, whose HBM side is the same gathers / atomics)
     by = {"hash_fwd": M * (12 + 8 * L * F * 4 + L * F * 4),
           "hash_bwd": M * (12 + L * F * 4 + 2 * 8 * L * F * 4)}
-    dom = max((k for k in ("hash_fwd", "hash_bwd") if k in ms), key=lambda k: ms[k])
+    by["fwd_enc"], by["bwd_hash"] = by["hash_fwd"], by["hash_bwd"]
+    dom = max((k for k in by if k in ms), key=lambda k: ms[k])
+    bk = "bwd_hash" if "bwd_hash" in ms else "hash_bwd"
     ach = by[dom] / (ms[dom] * 1e-3) / 1e9
     # the table-gradient scatter is bound by the memory-side float-atomic unit, not by HBM bytes: count the 64-B
     # atomic requests hash_bwd issues for one step's sample positions (tools/hash_requests.py)
     from nerf_amd import ngp_trainer as NT
     from hash_requests import ATOMIC_REQ_PEAK, count_requests
     seen = {}
-    orig = NT.G.hash_encode_bwd
+    fname, xarg = ("ngp_bwd_hash", 4) if bk == "bwd_hash" else ("hash_encode_bwd", 1)
+    orig = getattr(NT.G, fname)
 
-    def spy(grid, x, *args, **kw):
-        seen.setdefault("x", x.detach().clone())
-        return orig(grid, x, *args, **kw)
-    NT.G.hash_encode_bwd = spy
+    def spy(*args, **kw):
+        seen.setdefault("x", args[xarg].detach().clone())
+        return orig(*args, **kw)
+    setattr(NT.G, fname, spy)
     one(a.warmup + 2 * a.steps)
-    NT.G.hash_encode_bwd = orig
+    setattr(NT.G, fname, orig)
     nreq = count_requests(seen["x"], list(model.xyz_encoder.grid.resolutions)[:L],
                           hc["log2_hashmap_size"], model._aabb_host, model._eps)
-    req_s = nreq / (ms["hash_bwd"] * 1e-3)
+    req_s = nreq / (ms[bk] * 1e-3)
     out = {
         "metric": "rays/sec (train step), Instant-NGP expert (SURVEY §8f row 1), 800x800 Lego-style, "
                   f"{a.samples} stratified samples",
@@ -162,7 +166,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "bytes_per_launch": by[dom],
                      "mean_launch_ms": round(ms[dom], 4)},
-        "atomic_roofline": {"bound": "float-atomic requests", "kernel": "hash_bwd", "requests_per_launch": nreq,
+        "atomic_roofline": {"bound": "float-atomic requests", "kernel": bk, "requests_per_launch": nreq,
                             "achieved": round(req_s / 1e9, 2), "peak": round(ATOMIC_REQ_PEAK / 1e9, 2),
                             "unit": "G 64-B requests/s", "frac": round(req_s / ATOMIC_REQ_PEAK, 4)},
         "final_loss": round(float(loss.item()), 6),
