@@ -8,6 +8,7 @@ for f in csrc/*.hip; do
   b=$(basename $f .hip); X=""
   [ $b = mlp_bf16 ] && X="-mllvm -disable-promote-alloca-to-lds $2"
   { [ $b = ngp ] || [ $b = moe ] || [ $b = meta ]; } && X="-ffp-contract=off $2"
+  [ $b = adam ] && X="$2"
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $X -c $f -o /tmp/exp_$1/$b.o &
 done
 wait
