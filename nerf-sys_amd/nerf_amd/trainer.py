@@ -136,9 +136,11 @@ class NeRFTrainer:
             self._bg[n] = b
         return b
 
-    def enable_timing(self, n_steps: int = 1):
-        """Pre-create one set of HIP events per upcoming step (no host sync inside the timed steps):
-        the library records them around the fine net's trunk GEMM launches."""
+    def enable_timing(self, n_steps: int = 1, skip: int = 0):
+        """Pre-create one set of HIP events per instrumented step (no host sync inside the timed steps): the
+        library records them around the fine net's trunk GEMM launches of the n_steps steps that follow the next
+        `skip` steps.  Each recorded event costs the stream ~10-25 us (a gap before the next launch), so a bench
+        instruments a few of its timed steps, not all of them."""
         if n_steps <= 0:
             self.timing = None
             return
@@ -148,10 +150,13 @@ class NeRFTrainer:
             for e in st["fwd"] + st["bwd"]:
                 e.record()  # materialise the event handles
         torch.cuda.synchronize()
-        self.timing = {"pool": sets, "used": [], "M": None}
+        self.timing = {"pool": sets, "used": [], "M": None, "skip": int(skip)}
 
     def _next_events(self):
         if not self.timing or not self.timing["pool"]:
+            return None
+        if self.timing["skip"] > 0:
+            self.timing["skip"] -= 1
             return None
         ev = self.timing["pool"].pop(0)
         self.timing["used"].append(ev)
