@@ -330,6 +330,149 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const float* __restrict
   }
 }
 
+// ------------------------------------------------------------------------------------------ 16x16x4 forms
+// The same GEMMs on v_mfma_f32_16x16x4_f32 (equal FLOP per cycle, exact fp32 fmaf chains like the 32x32x2 form).
+// MI355X_MICROARCH.md "DVFS give-back" (7): under load the 16x16 shape holds a higher clock than the 32x32 one;
+// measured at the C2 fine-net trunk shape in tools/gemm_bench16.hip (interleaved with the 32x32x2 kernels above).
+// gemm_nt16_kernel: 128x128 block tile, BK-deep LDS slabs (80-B / 144-B row pitch), register staging and XCD remap
+// as gemm_nt_body; each wave owns 64x64 as 4x4 16x16 blocks.  Lane l supplies row (l & 15) and k-slot g = l >> 4;
+// a 16-k half-slab is split k = 4g + s for MFMA s = 0..3, so one ds_read_b128 per row fragment feeds four MFMAs.
+// Operands swapped (the tile is C^T): lane l holds output row m = .. + (l & 15), columns n = .. + 4g + r (r = 0..3)
+// -> one float4 store per 16x16 block; ReLU bitmask words OR'd over the four k-slot groups.
+typedef float nerf_f32x4 __attribute__((ext_vector_type(4)));
+
+template <int BM, int BN, int WAVES_M, int EPI, int MINW = 4, int BK = 16>
+__global__ __launch_bounds__(256, MINW) void gemm_nt16_kernel(const float* __restrict__ A, int lda,
+                                                             const float* __restrict__ B, int ldb,
+                                                             const float* __restrict__ bias, float* __restrict__ C,
+                                                             int ldc, const uint32_t* __restrict__ mbits, int ldmb,
+                                                             uint32_t* __restrict__ mbits_out, int K, int n_ntiles) {
+  constexpr int LS = BK + 4, C4 = BK / 4;
+  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  static_assert(TN % 2 == 0, "mask words span two 16-column blocks");
+  constexpr int A_F4 = BM * C4, B_F4 = BN * C4;
+  constexpr int A_PER = (A_F4 + 255) / 256, B_PER = (B_F4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LS];
+
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
+  const int64_t m0 = (int64_t)mt * BM;
+  const int n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int lr = lane & 15, lg = lane >> 4;
+  const float* Ab = A + m0 * lda;
+  const float* Bb = B + (int64_t)n0 * ldb;
+
+  float4 ra[A_PER], rb[B_PER];
+#define N16_GLOAD(k0_)                                                                         \
+  _Pragma("unroll") for (int i = 0; i < A_PER; ++i) {                                         \
+    const int f = tid + 256 * i;                                                               \
+    if (A_F4 % 256 == 0 || f < A_F4)                                                           \
+      ra[i] = *reinterpret_cast<const float4*>(Ab + (int64_t)(f / C4) * lda + (k0_) + (f % C4) * 4); \
+  }                                                                                            \
+  _Pragma("unroll") for (int i = 0; i < B_PER; ++i) {                                         \
+    const int f = tid + 256 * i;                                                               \
+    if (B_F4 % 256 == 0 || f < B_F4)                                                           \
+      rb[i] = *reinterpret_cast<const float4*>(Bb + (int64_t)(f / C4) * ldb + (k0_) + (f % C4) * 4); \
+  }
+#define N16_SSTORE(buf_)                                                                       \
+  {                                                                                            \
+    float* As_ = smem + (buf_) * (BM + BN) * LS;                                               \
+    float* Bs_ = As_ + BM * LS;                                                                \
+    _Pragma("unroll") for (int i = 0; i < A_PER; ++i) {                                       \
+      const int f = tid + 256 * i;                                                             \
+      if (A_F4 % 256 == 0 || f < A_F4)                                                         \
+        *reinterpret_cast<float4*>(As_ + (f / C4) * LS + (f % C4) * 4) = ra[i];                \
+    }                                                                                          \
+    _Pragma("unroll") for (int i = 0; i < B_PER; ++i) {                                       \
+      const int f = tid + 256 * i;                                                             \
+      if (B_F4 % 256 == 0 || f < B_F4)                                                         \
+        *reinterpret_cast<float4*>(Bs_ + (f / C4) * LS + (f % C4) * 4) = rb[i];                \
+    }                                                                                          \
+  }
+
+  nerf_f32x4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = nerf_f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  N16_GLOAD(0);
+  N16_SSTORE(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    N16_GLOAD((kt + 1 < nk ? kt + 1 : kt) * BK);
+    const float* As = smem + cur * (BM + BN) * LS;
+    const float* Bs = As + BM * LS;
+#pragma unroll
+    for (int hh = 0; hh < BK / 16; ++hh) {  // k = 16 hh + 4 g + s
+      float4 af[TM], bf[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) af[a] = *reinterpret_cast<const float4*>(As + (wm * WTM + a * 16 + lr) * LS + 16 * hh + 4 * lg);
+#pragma unroll
+      for (int b = 0; b < TN; ++b) bf[b] = *reinterpret_cast<const float4*>(Bs + (wn * WTN + b * 16 + lr) * LS + 16 * hh + 4 * lg);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(bf[b][s], af[a][s], acc[a][b], 0, 0, 0);
+    }
+    N16_SSTORE(cur ^ 1);
+    __syncthreads();
+  }
+
+#undef N16_GLOAD
+#undef N16_SSTORE
+  // epilogue: lane holds row m = mw + 16a + lr, columns nb + 4lg + r of 16-column block b
+  const int64_t mw = m0 + wm * WTM;
+  const int nw = n0 + wn * WTN;
+#pragma unroll
+  for (int bp = 0; bp < TN / 2; ++bp) {
+    const int g = (nw + 32 * bp) >> 5;  // mask word of columns [32 g, 32 g + 32)
+    float4 bv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bv[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) bv[h] = *reinterpret_cast<const float4*>(bias + nw + 32 * bp + 16 * h + 4 * lg);
+    }
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const int64_t m = mw + a * 16 + lr;
+      uint32_t word = 0;
+      if (EPI == EPI_MASK) word = mbits[m * ldmb + g];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const nerf_f32x4 v0 = acc[a][2 * bp + h];
+        float v[4] = {v0[0], v0[1], v0[2], v0[3]};
+        const float bb[4] = {bv[h].x, bv[h].y, bv[h].z, bv[h].w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int bit = 16 * h + 4 * lg + r;
+          if (EPI == EPI_BIAS) v[r] += bb[r];
+          if (EPI == EPI_BIAS_RELU) {
+            v[r] = fmaxf(v[r] + bb[r], 0.f);
+            word |= (v[r] > 0.f ? 1u : 0u) << bit;
+          }
+          if (EPI == EPI_MASK) v[r] = ((word >> bit) & 1u) ? v[r] : 0.f;
+        }
+        *reinterpret_cast<float4*>(C + m * ldc + nw + 32 * bp + 16 * h + 4 * lg) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+      if (EPI == EPI_BIAS_RELU && mbits_out) {
+        word |= __shfl_xor(word, 16, 64);
+        word |= __shfl_xor(word, 32, 64);
+        if (lg == 0) mbits_out[m * ldmb + g] = word;
+      }
+    }
+  }
+}
+
 // dst[i] = (acc ? dst[i] : 0) + sum_{s<S} src[s*slab + i]   (float4 lanes, deterministic order)
 static __global__ void reduce_splits_kernel(const float* __restrict__ src, int64_t slab, int S, float* __restrict__ dst,
                                      int64_t n4, int accumulate) {

@@ -177,6 +177,13 @@ __global__ void transpose_kernel(TJobs jobs) {
 
 // ------------------------------------------------------------------ launch helpers
 
+// 16x16x4 trunk forward / input-gradient GEMMs (gemm.hpp): waves per SIMD the register budget is sized for.
+// tools/gemm_bench16.hip (MI355X, C2 fine-net shape, 9 interleaved rounds): fwd 0.839 / dgrad 0.817 ms per 256x256
+// launch at 3 against 0.901 / 0.874 for the 32x32x2 kernel (2: 0.861 / 0.821, 4: 0.858; BK = 32: 0.957 / 0.940).
+#ifndef NERF_NT16_MINW
+#define NERF_NT16_MINW 3
+#endif
+
 // MINW = 4 waves per SIMD: the register budget (128 unified VGPR+AGPR per lane) that lets four 256-thread
 // workgroups share a CU; measured +9..12 % over the unconstrained allocation (tools/gemm_bench.hip).
 template <int BM, int BN, int WAVES_M, int EPI>
@@ -185,6 +192,13 @@ int launch_nt(const float* A, int lda, const float* B, int ldb, const float* bia
   if (M % BM || N % BN || K % 16) return NERF_E_ARG;
   const int ntn = N / BN;
   const int64_t nblk = (M / BM) * ntn;
+#ifndef NERF_GEMM32
+  if constexpr (BM == 128 && BN == 128 && WAVES_M == 2) {  // the trunk GEMMs: 16x16x4 form (gemm.hpp)
+    gemm_nt16_kernel<128, 128, 2, EPI, NERF_NT16_MINW><<<(unsigned)nblk, 256, 0, st>>>(A, lda, B, ldb, bias, C, ldc, mbits,
+                                                                                       N / 32, mbits_out, K, ntn);
+    return NERF_OK;
+  }
+#endif
   gemm_nt_kernel<BM, BN, WAVES_M, EPI, (BN >= 128 ? 4 : 1)><<<(unsigned)nblk, 256, 0, st>>>(A, lda, B, ldb, bias, C, ldc, mbits,
                                                                            N / 32, mbits_out, K, ntn);
   return NERF_OK;

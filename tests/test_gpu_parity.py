@@ -198,6 +198,24 @@ def test_mlp_ragged_and_fast_weights(net):
         _close(a, b, rel_scale=True, what="fast-weights grad")
 
 
+def _kink_rows(p64, x_d64, eps):
+    """Rows with any ReLU pre-activation within eps of 0 in the fp64 oracle forward (test infrastructure: records
+    the inputs of the oracle's torch.relu calls)."""
+    seen = []
+    relu = torch.relu
+
+    def rec(x):
+        seen.append(x.detach().abs().amin(dim=-1))
+        return relu(x)
+
+    torch.relu = rec
+    try:
+        O.vanilla_forward(p64, x_d64)
+    finally:
+        torch.relu = relu
+    return torch.stack(seen, 1).amin(1) < eps
+
+
 def test_mlp_backward_multi_split_ragged(net):
     """Weight gradients at sizes with several split-M slabs (S = Mp / 2048): M = 9000 (S = 4) and M = 40001
     (S = 19, rows per split 2176 -> the last split is short and the second half of its colour-backward pair is
@@ -206,37 +224,31 @@ def test_mlp_backward_multi_split_ragged(net):
     bitwise identical (fixed reduction order, no atomics).
 
     ReLU boundary flips: a pre-activation within rounding of 0 passes the gradient in one evaluation and
-    blocks it in another while the forward output moves by ~1e-7, so the unit's row term enters one gradient
-    and not the other.  At 40001 rows x 2048 trunk units a few flips are expected (measured: 2 units at
-    trunk.6, spreading to ~5 % of the elements of trunk.4-5 through the input gradient).  So: everything
-    within 1e-4 x max|grad| at M = 9000 and for the tensors above the trunk (trunk.7, heads, colour branch) at
-    M = 40001; trunk.0-6 at M = 40001 within 1e-2 x max|grad| and 1e-2 relative L2 error (a dropped 1088-row
-    half-split moves the gradient by ~3 %)."""
+    blocks it in another (the fp32 GPU forward vs the fp64 oracle), so that row's term enters one gradient and
+    not the other.  Rows with any pre-activation within 2e-6 of 0 in the fp64 forward (~4 % of the rows; fp32
+    pre-activations sit within 1.1e-6 of the fp64 ones) get a zero output gradient in BOTH evaluations; every
+    other row is compared at the north-star 1e-4 of scale (a dropped split or 16-row sub-slab moves the
+    gradient far beyond that)."""
     p = mlp_params("w/")
     g = torch.Generator().manual_seed(21)
     for M in (9000, 40001):
         x_d = torch.cat([torch.rand(M, 3, generator=g) * 4 - 2,
                          torch.nn.functional.normalize(torch.randn(M, 3, generator=g), dim=-1)], -1)
         gout = torch.randn(M, 4, generator=g)
+        p64 = {k: v.double().requires_grad_(True) for k, v in p.items()}
+        kink = _kink_rows({k: v.detach() for k, v in p64.items()}, x_d.double(), 2e-6)
+        assert kink.float().mean().item() < 0.1, "too many rows near a ReLU kink"
+        gout[kink] = 0.0
         fast = {k: v.to(DEV).requires_grad_(True) for k, v in p.items()}
         runs = []
         for _ in range(2):
             out = net(x_d.to(DEV), params=fast)
             runs.append(torch.autograd.grad((out * gout.to(DEV)).sum(), list(fast.values())))
-        p64 = {k: v.double().requires_grad_(True) for k, v in p.items()}
         ref = O.vanilla_forward(p64, x_d.double())
         gr = torch.autograd.grad((ref * gout.double()).sum(), [p64[k] for k in fast])
         for k, a, a2, b in zip(fast, runs[0], runs[1], gr):
             assert torch.equal(a, a2), f"M={M} {k}: backward not bitwise reproducible"
-            flips_possible = M > 10000 and k.startswith("trunk.") and not k.startswith("trunk.7")
-            if not flips_possible:
-                _close(a, b, rel_scale=True, what=f"M={M} grad {k}")
-                continue
-            err = (a.double().cpu() - b).abs()
-            scale = max(1.0, b.abs().max().item())
-            assert err.max().item() <= 1e-2 * scale, f"M={M} {k}: max err {err.max().item():.3e}"
-            rel = (err.norm() / b.norm()).item()
-            assert rel <= 1e-2, f"M={M} {k}: relative L2 error {rel:.3e}"
+            _close(a, b, rel_scale=True, what=f"M={M} grad {k} ({int(kink.sum())} kink rows excluded)")
 
 
 def test_mlp_inference_equals_training_forward(net, K):
