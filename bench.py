@@ -47,7 +47,7 @@ import torch  # noqa: E402  (importing torch initialises no GPU)
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "rays/sec (train step) + full-image PSNR, 800×800 Lego, 64+128 samples"
-FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 / 16x16x4_f32, dense
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak
 MAC_PER_EVAL = 500864
@@ -251,8 +251,8 @@ def roofline(tm, bf16, overlap):
     }
     eligible = [k for k in cls if not (overlap and k == "fwd")]
     dom = max(eligible, key=lambda k: cls[k])
-    names = {"fwd": "gemm_nt fwd (bias+ReLU)", "wgrad": "gemm_wgrad (split-M, 128x128 tiles)",
-             "dgrad": "gemm_nt dgrad (ReLU mask)"}
+    names = {"fwd": "gemm_nt16 fwd (16x16x4, bias+ReLU)", "wgrad": "gemm_wgrad (32x32x2, split-M, 128x128 tiles)",
+             "dgrad": "gemm_nt16 dgrad (16x16x4, ReLU mask)"}
     ms = cls[dom]
     ach = flop256 / (ms * 1e-3) / 1e12
     kern = f"{names[dom]}, fine net M={M}: trunk 256x256 layers {K256}"

@@ -14,8 +14,8 @@ from collections import defaultdict
 root = sys.argv[1]
 M_FINE = 4096 * 192
 CLASSES = {
-    "fwd": ("gemm_nt_kernel<128, 128, 2, 1,", 0),
-    "dgrad": ("gemm_nt_kernel<128, 128, 2, 2,", 0),
+    "fwd": ("gemm_nt16_kernel<128, 128, 2, 1,", 0),
+    "dgrad": ("gemm_nt16_kernel<128, 128, 2, 2,", 0),
     "wgrad": ("gemm_wgrad_kernel<128, 128, 2,", 0),
 }
 if len(sys.argv) > 2 and sys.argv[2] == "bf16fused":  # the fused bf16 MLP (bench.py roofline_bf16 classes)
