@@ -32,6 +32,8 @@ def main():
     pr.disable()
     st = pstats.Stats(pr)
     st.sort_stats("tottime").print_stats(35)
+    st.sort_stats("cumulative").print_stats(45)
+    st.print_callers("_named_members|named_modules|data_ptr")
 
 
 if __name__ == "__main__":
