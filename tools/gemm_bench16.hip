@@ -16,6 +16,8 @@
 //   loads — the IR has already sunk them, so it only fences the scheduler — wgrad 0.923 vs 0.862, nt16 fwd 0.853 vs
 //   0.838; loads for slab k + 2 issued before the barrier that ends slab k (software pipelined): wgrad 0.923, nt16 fwd
 //   1.036 / dgrad 1.017 (slower: the wait for the older loads then counts the newer ones in flight).
+//   A persistent 16x16x4 kernel whose last k-slab loads slab 0 of the workgroup's next tile (gemm_nt16p.hpp): dgrad
+//   1.786 ms at 1024 workgroups / 1.491 at 768 vs 0.826 (its k-loop is no longer fully unrolled).
 //   Tried on the library kernel and not kept: staggering the first generation of workgroups by s_sleep (slot or
 //   hashed, 0.886-0.946: slower), an epilogue staged through LDS so that every store writes whole 128-B lines
 //   (fwd 0.875 vs 0.863, dgrad 0.851 vs 0.858: within noise).
