@@ -17,7 +17,8 @@
 //   0.838; loads for slab k + 2 issued before the barrier that ends slab k (software pipelined): wgrad 0.923, nt16 fwd
 //   1.036 / dgrad 1.017 (slower: the wait for the older loads then counts the newer ones in flight).
 //   A persistent 16x16x4 kernel whose last k-slab loads slab 0 of the workgroup's next tile (gemm_nt16p.hpp): dgrad
-//   1.786 ms at 1024 workgroups / 1.491 at 768 vs 0.826 (its k-loop is no longer fully unrolled).
+//   1.786 ms at 1024 workgroups / 1.491 at 768 vs 0.826 with an if/else between the two loads, 0.907 / 0.890 vs 0.825
+//   with branch-free pointer selects: the prologue of a new tile is not what the ~13 % per-tile cost is made of.
 //   Chunk-major LDS slabs ([4-float chunk][row], conflict-free for every ds_read_b128 phase; PMC: the 16x16x4 kernel
 //   shows 5.2e7 LDS bank-conflict cycles per launch vs 2.7e7 for the 32x32x2 one): fwd 0.866 vs 0.837, dgrad 0.833 vs
 //   0.831 — the conflicts do not bound it (PMC: MFMA busy 0.80 for fwd / dgrad at 2.3-2.4 GHz, wgrad 0.77).

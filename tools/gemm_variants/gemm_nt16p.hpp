@@ -1,7 +1,8 @@
 // Experiment: persistent gemm_nt16 — each workgroup walks tiles t = blockIdx.x + k * gridDim.x (same XCD for a grid
 // that is a multiple of 8), and the last k-slab of tile t loads slab 0 of tile t + G, so the next tile's prologue
 // (first global load, LDS store, barrier) overlaps the current tile's last MFMA block and epilogue.
-// Measured (tools/gemm_bench16.hip): dgrad 1.786 ms at 1024 workgroups, 1.491 at 768, vs 0.826 for gemm_nt16_kernel.
+// Measured (tools/gemm_bench16.hip): with an if/else between the two loads, dgrad 1.786 ms at 1024 workgroups, 1.491
+// at 768, vs 0.826 for gemm_nt16_kernel; with the branch-free selects below 0.907 / 0.890 vs 0.825.
 #pragma once
 #include "../../nerf-sys_amd/csrc/gemm.hpp"
 
@@ -78,10 +79,12 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt16p_kernel(const float* __re
 #pragma unroll
       for (int b = 0; b < TN; ++b) acc[a][b] = nerf_f32x4{0.f, 0.f, 0.f, 0.f};
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) {
-        P16_GLOAD(Ab, Bb, (kt + 1) * BK);
-      } else {
-        P16_GLOAD(An, Bn, 0);
+      {
+        const bool last = kt + 1 == nk;  // branch-free: the last slab loads slab 0 of the next tile
+        const float* Ap = last ? An : Ab;
+        const float* Bp = last ? Bn : Bb;
+        const int k0 = last ? 0 : (kt + 1) * BK;
+        P16_GLOAD(Ap, Bp, k0);
       }
       const float* As = smem + cur * (BM + BN) * LS;
       const float* Bs = As + BM * LS;
