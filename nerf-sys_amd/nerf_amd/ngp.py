@@ -32,7 +32,6 @@ import torch.nn as nn
 from torch.autograd.function import once_differentiable
 
 from ._lib import check, lib, need, ptr, stream
-from ._params import OwnParamCache
 from .vanilla import VanillaNeRF
 
 _INTERP = {"Nearest": 0, "Linear": 1, "Smoothstep": 2}
@@ -528,7 +527,7 @@ class _Block(nn.Module):
         self.linear = nn.Linear(i, o)
 
 
-class InstantNGP(OwnParamCache):
+class InstantNGP(nn.Module):
     """MetaNGP (models/inr/meta_ngp.py:15-255) on the HIP kernels; same constructor and parameter names."""
 
     def __init__(self, *, occ_conf: Optional[Dict] = None, scene_box=None, hidden: int = 64, sigma_depth: int = 2,
@@ -725,7 +724,7 @@ class InstantNGP(OwnParamCache):
                 "color": {"params": list(self.color_mlp.parameters())}}
 
     def tensors(self, params=None):
-        own = self.own_params()
+        own = dict(self.named_parameters())
         if params is None:
             return [own[n] for n in self.layout.names]
         return [params.get(n, own[n]) for n in self.layout.names]

@@ -24,7 +24,6 @@ import torch.nn as nn
 from torch.autograd.function import once_differentiable
 
 from . import kernels as K
-from ._params import OwnParamCache
 from ._lib import lib
 
 PARAM_SHAPES = OrderedDict()
@@ -152,7 +151,7 @@ class _ColorMLP(nn.Module):
         self.color_out = nn.Linear(128, 3)
 
 
-class VanillaNeRF(OwnParamCache):
+class VanillaNeRF(nn.Module):
     """HIP-backed equivalent of MetaNeRF(encoding_dir="frequency") with the (M,6)->(M,4) contract."""
 
     def __init__(self):
@@ -201,7 +200,7 @@ class VanillaNeRF(OwnParamCache):
 
     # ---- packing
     def tensors(self, params=None):
-        own = self.own_params()
+        own = dict(self.named_parameters())
         if params is None:
             return [own[n] for n in PARAM_SHAPES]
         return [params.get(n, own[n]) for n in PARAM_SHAPES]
