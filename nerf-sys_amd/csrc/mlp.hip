@@ -304,7 +304,8 @@ extern "C" int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* 
   // heads
   TRY(nt<EPI_BIAS>(in, ld_in, Wt(16), 256, Wt(17), W.O16, 32, nullptr, nullptr, Mp, 32, 256, st));
   build_cin_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(x_d, W.O16, M, Mp, W.CIN);
-  TRY(nt<EPI_BIAS_RELU>(W.CIN, 64, Wt(18), 64, Wt(19), W.C0, 128, nullptr, nullptr, Mp, 128, 64,
+  // K = 48: the colour input has 42 real columns (15 geo + 27 direction PE), columns 48..63 are zero in CIN
+  TRY(nt<EPI_BIAS_RELU>(W.CIN, 64, Wt(18), 64, Wt(19), W.C0, 128, nullptr, nullptr, Mp, 128, 48,
                         st));
   TRY(nt<EPI_BIAS>(W.C0, 128, Wt(20), 128, Wt(21), W.O3, 32, nullptr, nullptr, Mp, 32, 128, st));
   head_out_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(W.O3, W.O16, M, rgb_sigma);
