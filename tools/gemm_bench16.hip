@@ -34,6 +34,7 @@
 #include <cmath>
 #include "gemm_variants/gemm_nt16.hpp"
 #include "gemm_variants/gemm_wgrad_t.hpp"
+#include "gemm_variants/gemm_wgrad8.hpp"
 #include "gemm_variants/gemm_diag.hpp"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
@@ -79,6 +80,7 @@ int main(int argc, char** argv) {
       {"wgrd lib 32x32x2", -3, {}},
       {"wgrd LDS-transposed", -5, {}},
       {"wgrd LDS-transposed MINW=2", -5, {}},
+      {"wgrd 8 waves 128x256", -5, {}},
   };
   auto run = [&](int v) {
     switch (v) {
@@ -93,6 +95,7 @@ int main(int argc, char** argv) {
       case 8: gemm_nt16_kernel<128, 128, 2, EPI_MASK, 2, 32><<<nb, 256>>>(A, K, B, K, bias, C, N, mb, 8, nullptr, K, ntn); break;
       case 9: gemm_wgrad_kernel<128, 128, 2><<<4 * 256, 256>>>(A, K, C, N, P, 256, P + 65536, slab, M / 256, M, 2, 4); break;
       case 10: gemm_wgrad_t_kernel<128, 128, 2><<<4 * 256, 256>>>(A, K, C, N, P, 256, P + 65536, slab, M / 256, M, 2, 4); break;
+      case 12: gemm_wgrad8_kernel<128, 256, 2><<<2 * 256, 512>>>(A, K, C, N, P, 256, P + 65536, slab, M / 256, M, 1, 2); break;
       case 11: gemm_wgrad_t_kernel<128, 128, 2, 2><<<4 * 256, 256>>>(A, K, C, N, P, 256, P + 65536, slab, M / 256, M, 2, 4); break;
     }
   };
