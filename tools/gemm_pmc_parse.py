@@ -1,28 +1,35 @@
-"""Per-kernel SQ / GRBM counters of tools/gemm_pmc.sh runs: MFMA busy fraction and the effective clock.
-MI355X_MICROARCH.md: SQ_VALU_MFMA_BUSY_CYCLES counts cycles (summed over SIMDs), GRBM_GUI_ACTIVE is summed over the
-8 XCDs, so clock = GRBM_GUI_ACTIVE / 8 / kernel wall time; MFMA busy per SIMD = MFMA_BUSY / (256 CUs x 4 SIMDs x
-GRBM_GUI_ACTIVE / 8).  Usage: python tools/gemm_pmc_parse.py gpurun_out/gpmc/p1"""
+"""Per-kernel SQ / GRBM counters of a rocprofv3 --pmc run (tools/gemm_pmc.sh, tools/pmc_mfma_bench.sh): MFMA busy
+fraction and effective clock per (kernel, grid).  MI355X_MICROARCH.md: SQ_VALU_MFMA_BUSY_CYCLES counts cycles summed
+over the SIMDs, GRBM_GUI_ACTIVE is summed over the 8 XCDs, so per dispatch clock = GRBM_GUI_ACTIVE / 8 / wall and MFMA
+busy per SIMD = MFMA_BUSY / (256 CUs x 4 SIMDs x GRBM_GUI_ACTIVE / 8).  Wall times come from the counter collection's
+own per-dispatch timestamps (profiled dispatches run serialised).  Usage: python tools/gemm_pmc_parse.py DIR"""
 import collections
 import csv
 import glob
+import statistics
 import sys
 
 root = sys.argv[1]
-ctr = collections.defaultdict(lambda: collections.defaultdict(list))
+disp = collections.defaultdict(dict)
+meta = {}
 for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        key = (r["Kernel_Name"][:70], r.get("Grid_Size", ""))
-        ctr[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
-dur = collections.defaultdict(list)
-for f in glob.glob(f"{root}/**/*kernel_trace.csv", recursive=True):
-    for r in csv.DictReader(open(f)):
-        dur[r["Kernel_Name"][:70]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
-for (name, grid), d in sorted(ctr.items()):
-    m = {k: sum(v) / len(v) for k, v in d.items()}
-    ts = dur.get(name)
-    t = sorted(ts)[len(ts) // 2] if ts else float("nan")
-    clk = m.get("GRBM_GUI_ACTIVE", 0) / 8 / t / 1e9 if ts else float("nan")
-    busy = m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (1024 * m.get("GRBM_GUI_ACTIVE", 1) / 8)
-    print(f"{name:70s} grid {grid:>9s} wall {t * 1e3:7.3f} ms  clock {clk:5.2f} GHz  MFMA busy {busy:5.3f}  "
-          f"waits/wave-cycles {m.get('SQ_WAIT_ANY', 0) / max(m.get('SQ_WAVE_CYCLES', 1), 1):5.3f}  "
-          f"LDS conflicts {m.get('SQ_LDS_BANK_CONFLICT', 0):.3g}")
+        d = r["Dispatch_Id"]
+        disp[d][r["Counter_Name"]] = float(r["Counter_Value"])
+        meta[d] = (r["Kernel_Name"][:70], r["Grid_Size"], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
+for d, c in disp.items():
+    name, grid, t = meta[d]
+    g = c.get("GRBM_GUI_ACTIVE", 0.0)
+    a = agg[(name, grid)]
+    a["wall"].append(t)
+    if t > 0 and g > 0:
+        a["clock"].append(g / 8 / t / 1e9)
+        a["busy"].append(c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (1024 * g / 8))
+    if c.get("SQ_WAVE_CYCLES"):
+        a["wait"].append(c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"])
+    a["lds"].append(c.get("SQ_LDS_BANK_CONFLICT", 0.0))
+med = lambda xs: statistics.median(xs) if xs else float("nan")
+for (name, grid), a in sorted(agg.items()):
+    print(f"{name:70s} grid {grid:>9s} n {len(a['wall']):3d}  wall {med(a['wall']) * 1e3:7.3f} ms  clock {med(a['clock']):5.2f} GHz  "
+          f"MFMA busy {med(a['busy']):5.3f}  waits/wave-cycles {med(a['wait']):5.3f}  LDS conflicts {med(a['lds']):.3g}")
