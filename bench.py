@@ -238,8 +238,8 @@ def roofline_bf16(tm):
             "classes": cls, "rule": "largest total time per step (mean launch x launches) among the fused MLP kernels"}
 
 
-def roofline(tm, bf16, overlap):
-    if bf16 and os.environ.get("NERF_BF16_FUSED", "1") != "0" and os.environ.get("NERF_BF16_FUSED_BWD", "1") != "0":
+def roofline(tm, bf16, overlap, bf16_flags=0):
+    if bf16 and not bf16_flags:
         return roofline_bf16(tm)
     M = tm["M"]
     mean = lambda xs: sum(xs) / len(xs)
@@ -256,7 +256,7 @@ def roofline(tm, bf16, overlap):
     ms = cls[dom]
     ach = flop256 / (ms * 1e-3) / 1e12
     kern = f"{names[dom]}, fine net M={M}: trunk 256x256 layers {K256}"
-    if bf16:  # the layered bf16 path (NERF_BF16_FUSED=0 / NERF_BF16_FUSED_BWD=0 A/B runs)
+    if bf16:  # the layered bf16 path (--bf16-flags A/B runs)
         names = {k: v.replace("gemm_nt", "gemm_nt_bf16").replace("gemm_wgrad", "gemm_wgrad_bf16") for k, v in names.items()}
         kern = f"{names[dom]}, fine net M={M}: trunk 256x256 layers {K256}"
         # bf16 layers are HBM-bound: algorithmic bytes per launch per sample row = bf16 rows in (256 * 2 B) +

@@ -117,12 +117,22 @@ int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
 /* bf16 variants (BASELINE configs[2]: "bf16 MLP with fp32 compositing"): the same network, packed fp32
  * parameters, inputs and outputs as nerf_mlp_fwd/bwd; the layer GEMMs run on bf16 MFMA with fp32
  * accumulation and the activations / activation gradients live in the workspace as bf16.  The weight
- * gradient d_w is fp32.  Not bit-compatible with the fp32 path (tolerance: bf16 rounding). */
+ * gradient d_w is fp32.  Not bit-compatible with the fp32 path (tolerance: bf16 rounding).
+ * flags (0 = the production kernels; a bitwise OR of):
+ *   NERF_BF16_LAYERED_FWD  one GEMM launch per layer instead of the fused single-launch forward;
+ *   NERF_BF16_LAYERED_BWD  one dgrad + one wgrad GEMM launch per layer instead of the fused per-layer backward.
+ *                          The backward of a workspace must be called with the same NERF_BF16_LAYERED_BWD bit as
+ *                          the training forward that filled it (the layered backward reads ReLU bitmasks that only
+ *                          such a forward writes).
+ * The layered launches are the bitwise references of the fused kernels (tests/test_gpu_bf16.py); unknown bits ->
+ * NERF_E_ENUM.  The split counts are compile-time constants (NERF_BF16_MAX_SPLITS, NERF_BF16_NARROW_MUL). */
+#define NERF_BF16_LAYERED_FWD 1
+#define NERF_BF16_LAYERED_BWD 2
 int64_t nerf_mlp_workspace_bytes_bf16(int64_t M, int training);
 int nerf_mlp_fwd_bf16(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws, int64_t ws_bytes,
-                      int training, hipEvent_t* events, hipStream_t stream);
+                      int training, int flags, hipEvent_t* events, hipStream_t stream);
 int nerf_mlp_bwd_bf16(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
-                      int64_t ws_bytes, hipEvent_t* events, hipStream_t stream);
+                      int64_t ws_bytes, int flags, hipEvent_t* events, hipStream_t stream);
 /* events: as for nerf_mlp_fwd / nerf_mlp_bwd. */
 
 /* ------------------------------------------------------------------ compositing + loss */
@@ -206,6 +216,9 @@ typedef struct {
   int32_t dir_encoding;
   int32_t sh_levels;
   int32_t use_sigmoid_rgb;
+  int32_t generic_kernels; /* 0: the compile-time production-shape kernels when the shape is MetaNGP's default (the
+                              fused *_enc / bwd_hash entry points need them); 1: always the plan-driven generic
+                              kernels (their reference in the tests; the fused entry points return NERF_E_UNSUPPORTED) */
 } NerfNgpNet;
 
 /* Packed parameter layout: per layer (trunk 0..sd-1, head, colour 0..cd-1, out) W (Npad x Kpad) then

@@ -19,8 +19,6 @@
 #include "mlp_tail.hpp"
 #include "mlp_common.hpp"
 
-#include <stdlib.h>
-
 namespace {
 using namespace nerf_mlp;
 
@@ -42,11 +40,16 @@ struct WSB {
 
 // split-M partial slabs of the weight gradient: one per >= 1024 rows, at most NERF_BF16_MAX_SPLITS (128) — the fused
 // backward runs two workgroups per split, so 128 splits fill the 256 CUs in one round (256 splits took two rounds and
-// doubled the slab traffic: 526 MB of partials per fine-net backward).  The env override is read per call (A/B runs;
-// the workspace query and the kernels must see the same value).
+// doubled the slab traffic: 526 MB of partials per fine-net backward).  A compile-time constant (tools/ A/B builds
+// pass -DNERF_BF16_MAX_SPLITS=...), so the workspace query and the kernels always agree.
+#ifndef NERF_BF16_MAX_SPLITS
+#define NERF_BF16_MAX_SPLITS 128
+#endif
+#ifndef NERF_BF16_NARROW_MUL
+#define NERF_BF16_NARROW_MUL 2  // sub-splits per split of the narrow trunk.0 / trunk.4-encoding weight gradients
+#endif
 int bf16_splits(int64_t Mp) {
-  int mx = 128;
-  if (const char* e = getenv("NERF_BF16_MAX_SPLITS")) mx = atoi(e) > 0 ? atoi(e) : 128;
+  const int mx = NERF_BF16_MAX_SPLITS;
   int64_t sp = Mp / 1024;
   return (int)(sp < 1 ? 1 : (sp > mx ? mx : sp));
 }
@@ -91,10 +94,8 @@ WSB carve_b(void* base, int64_t M, int training) {
     w.partial = (float*)take((int64_t)w.S * L.total * 4);
     w.partial2 = (float*)take((int64_t)w.S * (L.total - L.off[16]) * 4);  // second-half tail sums (fused backward)
     // the narrow weight gradients of the fused backward (trunk.0, trunk.4's encoding columns) over S2 = 4 S sub-splits
-    {  // NERF_BF16_NARROW_MUL (A/B runs): sub-splits per split
-      int mul = 2;
-      if (const char* e = getenv("NERF_BF16_NARROW_MUL")) mul = atoi(e) > 0 ? atoi(e) : 2;
-      int64_t s2 = (int64_t)mul * w.S, cap = Mp / 256;
+    {
+      int64_t s2 = (int64_t)NERF_BF16_NARROW_MUL * w.S, cap = Mp / 256;
       w.S2 = (int)(s2 > cap ? (cap < 1 ? 1 : cap) : s2);
       w.rps2 = round_up(nerf_cdiv(Mp, w.S2), 64);
     }
@@ -336,22 +337,14 @@ int wgradb(const nerf_bf16* G, int ldg, const nerf_bf16* X, int ldx, int tensor_
 
 }  // namespace
 
-// NERF_BF16_FUSED_BWD=0 selects the layered backward (a dgrad and a wgrad GEMM launch per trunk layer) for A/B
-// measurements; the default fuses both per layer (mlp_bf16_bwd.hpp).
-bool fused_bwd_enabled() {
-  const char* e = getenv("NERF_BF16_FUSED_BWD");
-  return !(e && e[0] == '0');
-}
-
-// NERF_BF16_FUSED=0 selects the layer-by-layer forward (one GEMM launch per layer, activations through HBM) for
-// A/B measurements; the default is the fused single-launch forward (mlp_bf16_fused.hpp).
-bool fused_fwd_enabled() {
-  const char* e = getenv("NERF_BF16_FUSED");  // read per call: tests switch paths inside one process
-  return !(e && e[0] == '0');
-}
+// Path selection is an explicit argument (include/nerf_amd.h NERF_BF16_LAYERED_*): NERF_BF16_LAYERED_BWD selects the
+// layered backward (a dgrad and a wgrad GEMM launch per trunk layer; its forward also writes the ReLU bitmasks),
+// NERF_BF16_LAYERED_FWD the layer-by-layer forward (one GEMM launch per layer, activations through HBM).  The
+// defaults are the fused kernels (mlp_bf16_fused.hpp, mlp_bf16_bwd.hpp); the layered launches are their bitwise
+// references in the tests.
 
 int fused_forward(const float* w, const float* x_d, int64_t M, float* rgb_sigma, const WSB& W, int training,
-                  hipEvent_t* ev, hipStream_t st) {
+                  bool layered_bwd, hipEvent_t* ev, hipStream_t st) {
   using namespace nerf_fused;
   const Layout& L = layout();
   const FragTab T = frag_tab();
@@ -385,7 +378,7 @@ int fused_forward(const float* w, const float* x_d, int64_t M, float* rgb_sigma,
   A.ntiles = (int)(Mp / BMF);  // Mp is a multiple of 256: whole 128-row tiles
   const int grid = A.ntiles < n_cu ? A.ntiles : n_cu;  // persistent, one workgroup per CU (LDS ~87 KB)
   if (ev) (void)hipEventRecord(ev[0], st);
-  if (training && !fused_bwd_enabled())  // the layered backward reads ReLU bitmasks
+  if (training && layered_bwd)  // the layered backward reads ReLU bitmasks
     mlp_fwd_fused_bf16_kernel<true, true><<<grid, 512, 0, st>>>(A);
   else if (training)
     mlp_fwd_fused_bf16_kernel<true, false><<<grid, 512, 0, st>>>(A);
@@ -501,8 +494,9 @@ extern "C" int64_t nerf_mlp_workspace_bytes_bf16(int64_t M, int training) {
 }
 
 extern "C" int nerf_mlp_fwd_bf16(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws,
-                                 int64_t ws_bytes, int training, hipEvent_t* ev, hipStream_t st) {
+                                 int64_t ws_bytes, int training, int flags, hipEvent_t* ev, hipStream_t st) {
   NERF_CHECK_ARG(w && x_d && rgb_sigma && ws && M >= 0);
+  if (flags & ~(NERF_BF16_LAYERED_FWD | NERF_BF16_LAYERED_BWD)) return NERF_E_ENUM;
   if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(rgb_sigma)) return NERF_E_ALIGN;
   const WSB W = carve_b(ws, M, training);
   if (ws_bytes < W.bytes) return NERF_E_WORKSPACE;
@@ -511,7 +505,8 @@ extern "C" int nerf_mlp_fwd_bf16(const float* w, const float* x_d, int64_t M, fl
   const int64_t Mp = W.Mp;
   auto Wb = [&](int t) { return W.Wb + L.off[t]; };
   auto Bias = [&](int t) { return w + L.off[t]; };
-  if (fused_fwd_enabled()) return fused_forward(w, x_d, M, rgb_sigma, W, training, ev, st);
+  if (!(flags & NERF_BF16_LAYERED_FWD))
+    return fused_forward(w, x_d, M, rgb_sigma, W, training, (flags & NERF_BF16_LAYERED_BWD) != 0, ev, st);
 
   to_bf16_kernel<<<(unsigned)nerf_cdiv(L.total / 4 + 1, 256), 256, 0, st>>>(w, L.total, W.Wb);
   pe_xyz_bf16_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(x_d, M, Mp, W.X3E);
@@ -538,8 +533,9 @@ extern "C" int nerf_mlp_fwd_bf16(const float* w, const float* x_d, int64_t M, fl
 }
 
 extern "C" int nerf_mlp_bwd_bf16(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate,
-                                 void* ws, int64_t ws_bytes, hipEvent_t* ev, hipStream_t st) {
+                                 void* ws, int64_t ws_bytes, int flags, hipEvent_t* ev, hipStream_t st) {
   NERF_CHECK_ARG(w && d_rgb_sigma && d_w && ws && M >= 0);
+  if (flags & ~(NERF_BF16_LAYERED_FWD | NERF_BF16_LAYERED_BWD)) return NERF_E_ENUM;
   if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(d_w) || !nerf_aligned16(d_rgb_sigma))
     return NERF_E_ALIGN;
   const WSB W = carve_b(ws, M, 1);
@@ -552,7 +548,7 @@ extern "C" int nerf_mlp_bwd_bf16(const float* w, int64_t M, const float* d_rgb_s
   const int64_t Mp = W.Mp;
   auto Wt = [&](int t) { return w + L.off[t]; };
 
-  if (fused_bwd_enabled()) return fused_backward(w, M, d_rgb_sigma, d_w, accumulate, W, ev, st);
+  if (!(flags & NERF_BF16_LAYERED_BWD)) return fused_backward(w, M, d_rgb_sigma, d_w, accumulate, W, ev, st);
   // bf16 transposed weights for the input-gradient GEMMs (the bf16 forward copy W.Wb is reused for nothing
   // here: the backward GEMMs contract over the output dimension)
   nerf_bf16* T = W.WTb;

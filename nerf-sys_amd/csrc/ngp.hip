@@ -80,6 +80,7 @@ bool make_plan(const NerfNgpNet& n, bool save, NgpPlan& P) {
   if (n.dir_encoding == 0 && (n.sh_levels < 1 || n.sh_levels > 5)) return false;
   if (n.dir_encoding != 0 && n.dir_encoding != 1) return false;
   if (n.geo_feat_dim + dir_dim > 64) return false;
+  if (n.generic_kernels != 0 && n.generic_kernels != 1) return false;
   P.nl = n.sigma_depth + n.color_depth + 2;
   if (P.nl > NGP_MAX_LAYERS) return false;
   P.n_trunk = n.sigma_depth;
@@ -1612,12 +1613,10 @@ int bwd_grid(int64_t M) {
 }
 
 // the plan is the production expert's (ngp_bwd_prod_kernel's compile-time shape and LDS layout);
-// NERF_NGP_PROD=0 keeps the generic kernel (A/B measurements, tests)
-bool is_prod_plan(const NgpPlan& P) {
-  const char* e = getenv("NERF_NGP_PROD");  // read per call: tests switch it between launches
-  const bool on = !(e && e[0] == '0');
+// net.generic_kernels = 1 keeps the generic kernel (its reference in the tests, A/B measurements)
+bool is_prod_plan(const NerfNgpNet& net, const NgpPlan& P) {
   using namespace ngp_prod;
-  if (!on || P.nl != NL || P.head != HEAD || P.total != TOTAL || P.dir_mode != 0 || P.sh_levels != 4 ||
+  if (net.generic_kernels || P.nl != NL || P.head != HEAD || P.total != TOTAL || P.dir_mode != 0 || P.sh_levels != 4 ||
       P.geo != GEO || P.dir_dim != DIRD || P.in_dim > 32 || P.enc_buf != ENC || P.enc_ld != 36 ||
       P.cin_buf != CIN || P.cin_ld != 36 || P.g0 != G0 || P.g1 != G1 || P.dsig != DSIG || P.bsum != BSUM ||
       P.smem_floats != SMEM)
@@ -1678,13 +1677,13 @@ extern "C" int nerf_hash_encode(const NerfHashGrid* grid, const float* table, co
   return nerf_launch_status();
 }
 
-// NERF_HASH_BWD_AGG=0 selects the per-(sample, level) kernel without run aggregation (A/B measurements)
-static bool hash_bwd_aggregate() {
-  static const bool on = [] {
-    const char* e = getenv("NERF_HASH_BWD_AGG");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+// -DNERF_HASH_BWD_NOAGG builds the per-(sample, level) kernel without run aggregation (tools/ A/B builds)
+static constexpr bool hash_bwd_aggregate() {
+#ifdef NERF_HASH_BWD_NOAGG
+  return false;
+#else
+  return true;
+#endif
 }
 
 extern "C" int nerf_hash_encode_bwd(const NerfHashGrid* grid, const float* x, int64_t x_stride, int64_t M,
@@ -1761,7 +1760,7 @@ extern "C" int nerf_ngp_fwd(const NerfNgpNet* net, const float* w, const float* 
   if (!w || !enc || !x_d || !rgb_sigma) return NERF_E_ARG;
   if (!nerf_aligned16(w) || !nerf_aligned16(rgb_sigma)) return NERF_E_ALIGN;
   NgpPlan Pb;  // the production shape runs the compile-time kernel (its check is on the backward plan's layout)
-  if (make_plan(*net, true, Pb) && is_prod_plan(Pb)) {
+  if (make_plan(*net, true, Pb) && is_prod_plan(*net, Pb)) {
     const unsigned blocks = (unsigned)nerf_cdiv(M, NGP_BROWS);
     const size_t smp = (size_t)ngp_prod::F_SMEM * 4;
     if (P.sigmoid)
@@ -1784,7 +1783,7 @@ extern "C" int nerf_ngp_density(const NerfNgpNet* net, const float* w, const flo
   if (!w || !enc || !sigma) return NERF_E_ARG;
   if (!nerf_aligned16(w)) return NERF_E_ALIGN;
   NgpPlan Pb;
-  if (make_plan(*net, true, Pb) && is_prod_plan(Pb)) {
+  if (make_plan(*net, true, Pb) && is_prod_plan(*net, Pb)) {
     ngp_fwd_prod_kernel<1, 0><<<(unsigned)nerf_cdiv(M, NGP_BROWS), 256, (size_t)ngp_prod::F_SMEM * 4, st>>>(
         w, enc, enc_stride, P.in_dim, nullptr, M, sigma);
     return nerf_launch_status();
@@ -1802,7 +1801,7 @@ extern "C" int nerf_ngp_density_enc(const NerfNgpNet* net, const NerfHashGrid* g
   HashArgs a;
   if (!net || !grid || M < 0 || x_stride < 3 || !make_plan(*net, false, P) || !hash_args(grid, nullptr, a))
     return NERF_E_ARG;
-  if (a.F != 2 || a.L > 16 || a.L * a.F != net->in_dim || !make_plan(*net, true, Pb) || !is_prod_plan(Pb))
+  if (a.F != 2 || a.L > 16 || a.L * a.F != net->in_dim || !make_plan(*net, true, Pb) || !is_prod_plan(*net, Pb))
     return NERF_E_UNSUPPORTED;
   if (M == 0) return NERF_OK;
   if (!table || !w || !x || !sigma) return NERF_E_ARG;
@@ -1824,7 +1823,7 @@ extern "C" int nerf_ngp_fwd_enc(const NerfNgpNet* net, const NerfHashGrid* grid,
   HashArgs a;
   if (!net || !grid || M < 0 || !make_plan(*net, false, P) || !hash_args(grid, nullptr, a)) return NERF_E_ARG;
   if (enc_stride < a.L * a.F) return NERF_E_ARG;
-  if (a.F != 2 || a.L > 16 || a.L * a.F != net->in_dim || !make_plan(*net, true, Pb) || !is_prod_plan(Pb))
+  if (a.F != 2 || a.L > 16 || a.L * a.F != net->in_dim || !make_plan(*net, true, Pb) || !is_prod_plan(*net, Pb))
     return NERF_E_UNSUPPORTED;
   if (M == 0) return NERF_OK;
   if (!table || !w || !x_d || !enc || !rgb_sigma) return NERF_E_ARG;
@@ -1866,7 +1865,7 @@ extern "C" int nerf_ngp_bwd(const NerfNgpNet* net, const float* w, const float* 
   float* partial = reinterpret_cast<float*>(ws);
   float* wt = partial + (int64_t)grid * P.total;
   ngp_wt_kernel<<<P.nl, 256, 0, st>>>(P, w, wt);
-  if (is_prod_plan(P)) {
+  if (is_prod_plan(*net, P)) {
     const size_t smp = (size_t)ngp_prod::SMEM * 4;
     if (P.sigmoid) {
       allow_lds(ngp_bwd_prod_kernel<1>);
@@ -1910,7 +1909,7 @@ extern "C" int nerf_ngp_bwd_hash(const NerfNgpNet* net, const NerfHashGrid* hgri
   if (!net || !hgrid || !d_w || M < 0 || !make_plan(*net, true, P) || enc_stride < net->in_dim ||
       !hash_args(hgrid, nullptr, a))
     return NERF_E_ARG;
-  if (a.F != 2 || a.interp == 0 || a.L > 16 || a.L * a.F != net->in_dim || !is_prod_plan(P)) return NERF_E_UNSUPPORTED;
+  if (a.F != 2 || a.interp == 0 || a.L > 16 || a.L * a.F != net->in_dim || !is_prod_plan(*net, P)) return NERF_E_UNSUPPORTED;
   if (M == 0) {
     if (!accumulate) (void)hipMemsetAsync(d_w, 0, P.total * sizeof(float), st);
     return nerf_launch_status();

@@ -42,8 +42,8 @@ def lib():
             "nerf_mlp_fwd": [P, P, I64, P, P, I64, I, P, P],
             "nerf_mlp_bwd": [P, I64, P, P, I, P, I64, P, P],
             "nerf_mlp_workspace_bytes_bf16": [I64, I],
-            "nerf_mlp_fwd_bf16": [P, P, I64, P, P, I64, I, P, P],
-            "nerf_mlp_bwd_bf16": [P, I64, P, P, I, P, I64, P, P],
+            "nerf_mlp_fwd_bf16": [P, P, I64, P, P, I64, I, I, P, P],
+            "nerf_mlp_bwd_bf16": [P, I64, P, P, I, P, I64, I, P, P],
             "nerf_composite_fwd": [P, P, P, I64, I, F, P, P, P, P, P, I, F, P, P, P],
             "nerf_composite_bwd": [P, P, P, I64, I, F, P, P, P, P, P, P],
             "nerf_grad_sqnorm": [P, I64, P, P],

@@ -276,9 +276,12 @@ def _render_container_occ(model, rays, params, bg_color_default, chunk, render_s
 
     def before_sync():
         # host work that needs no marched sizes, issued while the march's count pass runs on the GPU (before the
-        # host read of the packed sizes): each expert's packed MLP (cached for this render) and the background
+        # host read of the packed sizes): each Instant-NGP expert's packed MLP (cached by pack_scope for this render;
+        # other expert types do not cache, so packing them here would only be repeated in their forward) and the
+        # background
+        from .ngp import InstantNGP
         for k, sub in enumerate(model.submodules):
-            if hasattr(sub, "packed"):
+            if isinstance(sub, InstantNGP):
                 sub.packed(sub_params[k])
         early["bg"] = _get_bg_rgb(model, d, params, rays, N, bg_color_default)
 

@@ -114,6 +114,10 @@ def freq_encode(x, L, include_input=True):
 
 
 PRECISIONS = ("fp32", "bf16")
+# bf16 path selection (include/nerf_amd.h): 0 = the fused production kernels; the layered launches are their
+# bitwise references.  A workspace's backward must use the NERF_BF16_LAYERED_BWD bit of its training forward.
+BF16_LAYERED_FWD = 1
+BF16_LAYERED_BWD = 2
 
 
 def _check_precision(precision):
@@ -139,7 +143,7 @@ def _events_arg(events):
     return arr
 
 
-def mlp_fwd(w_packed, x_d, ws, training, out=None, events=None, precision="fp32"):
+def mlp_fwd(w_packed, x_d, ws, training, out=None, events=None, precision="fp32", bf16_flags=0):
     need(w_packed, "packed weights"), need(x_d, "x_d")
     _check_precision(precision)
     M = x_d.shape[0]
@@ -147,14 +151,14 @@ def mlp_fwd(w_packed, x_d, ws, training, out=None, events=None, precision="fp32"
         out = _empty((M, 4), x_d)
     if precision == "bf16":
         check(lib().nerf_mlp_fwd_bf16(ptr(w_packed), ptr(x_d), M, ptr(out), ptr(ws), ws.numel(), int(training),
-                                      _events_arg(events), stream()), "nerf_mlp_fwd_bf16")
+                                      int(bf16_flags), _events_arg(events), stream()), "nerf_mlp_fwd_bf16")
         return out
     check(lib().nerf_mlp_fwd(ptr(w_packed), ptr(x_d), M, ptr(out), ptr(ws), ws.numel(), int(training),
                              _events_arg(events), stream()), "nerf_mlp_fwd")
     return out
 
 
-def mlp_bwd(w_packed, M, d_rgb_sigma, ws, d_w=None, accumulate=False, events=None, precision="fp32"):
+def mlp_bwd(w_packed, M, d_rgb_sigma, ws, d_w=None, accumulate=False, events=None, precision="fp32", bf16_flags=0):
     need(w_packed, "packed weights"), need(d_rgb_sigma, "d_rgb_sigma")
     _check_precision(precision)
     if d_w is None:
@@ -162,7 +166,7 @@ def mlp_bwd(w_packed, M, d_rgb_sigma, ws, d_w=None, accumulate=False, events=Non
         accumulate = False
     if precision == "bf16":
         check(lib().nerf_mlp_bwd_bf16(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws),
-                                      ws.numel(), _events_arg(events), stream()), "nerf_mlp_bwd_bf16")
+                                      ws.numel(), int(bf16_flags), _events_arg(events), stream()), "nerf_mlp_bwd_bf16")
         return d_w
     check(lib().nerf_mlp_bwd(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws), ws.numel(),
                              _events_arg(events), stream()), "nerf_mlp_bwd")

@@ -65,55 +65,3 @@ def image_psnr(pred_linear, gt_u8_or_srgb, color_space: str = "linear") -> float
     gt = gt_u8_or_srgb.float() / 255.0 if gt_u8_or_srgb.dtype == torch.uint8 else gt_u8_or_srgb.float()
     a, b = color_space_transformer(pred_linear.float(), gt.to(pred_linear.device), color_space)
     return psnr(F.mse_loss(a, b).item())
-
-
-def compute_fim_loss(P, model, data, params=None, active_module=None, *, grad_buffer=None, update_fisher=False,
-                     clamp_factor=5):
-    """Fisher-weighted loss (nerfs/losses.py:35-151): one render through the HIP path, per-ray MSE.
-
-    Without a Fisher store on the container and the active expert (``model.fisher_store`` / ``model.fim_loss``
-    and ``expert.fisher_store.tracked``, the reference's own guard at :81-87) it is the plain mean of the per-ray
-    MSE.  With them, the gradients of that loss w.r.t. the tracked tensors give the Fisher weight
-    (``expert.fim_loss.fim_weight``; per ray with ``P.fim_per_sample``), the weighted loss is returned and, on
-    the support path (``grad_buffer`` given or ``update_fisher``), the weighted gradients are written into
-    ``grad_buffer`` and the store is updated from the squared unweighted gradients."""
-    pred = render_rays(model, data["rays"], ray_samples=P.ray_samples, params=params, active_module=active_module,
-                       chunk=P.chunk_points)[0]
-    pred, gt = color_space_transformer(pred, data["rgbs"], getattr(P, "color_space", "linear"))
-    per_ray = F.mse_loss(pred, gt, reduction="none").mean(dim=-1)
-    base = per_ray.mean()
-    if active_module is None or not (hasattr(model, "fisher_store") and hasattr(model, "fim_loss")):
-        return base
-    expert = model.submodules[active_module]
-    store = expert.fisher_store
-    if not store.tracked:
-        return base
-    names = [n for n, _ in store.tracked]
-    tensors = [t for _, t in store.tracked]
-    if str(getattr(P, "algo", "")).lower() not in ("fomaml", "reptile"):
-        raise NotImplementedError("Fisher-weighted loss with second-order gradients is not on the HIP path")
-    support = bool(grad_buffer) or bool(update_fisher)  # need_grads of the reference (:56)
-    per_sample = bool(getattr(P, "fim_per_sample", False))
-    g0 = torch.autograd.grad(base, tensors, allow_unused=True, retain_graph=(not support) or per_sample)
-    gd = {n: g.detach() for n, g in zip(names, g0) if g is not None}
-    lim = (1.0 / clamp_factor, float(clamp_factor))
-    if per_sample:
-        w = expert.fim_loss.fim_weight(gd, mse_i=per_ray, per_sample=True, clamp=lim)
-        loss = (w.detach() * per_ray).mean()
-        if not support:
-            return loss
-        gw = torch.autograd.grad(loss, tensors, allow_unused=True)
-    else:
-        w = expert.fim_loss.fim_weight(gd, per_sample=False, clamp=lim).detach()
-        loss = w * base
-        if not support:
-            return loss
-        gw = [None if g is None else w * g for g in g0]
-    if update_fisher and gd:
-        with torch.no_grad():
-            store.update_from_grads({n: g.pow(2) for n, g in gd.items()})
-    if grad_buffer is not None:
-        for n, g in zip(names, gw):
-            if g is not None:
-                grad_buffer[n] = g
-    return loss

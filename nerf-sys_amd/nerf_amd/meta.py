@@ -21,7 +21,7 @@ from typing import List, Optional
 import torch
 
 from ._lib import check, lib, ptr, stream
-from .losses import compute_fim_loss, compute_mse_loss
+from .losses import compute_mse_loss
 
 
 def _ptr_array(tensors):
@@ -66,9 +66,10 @@ def sgd_update(fast: "OrderedDict[str, torch.Tensor]", grads, inner_lr: float) -
 
 
 def compute_loss(P, model, data, params=None, active_module=None, **kwargs):
-    """nerfs/losses.py:154-166 dispatcher."""
+    """nerfs/losses.py:154-166 dispatcher.  The Fisher-information loss (nerfs/losses.py:35-151) is dead code in the
+    reference (no module defines ``fisher_store``; SURVEY §2 row 4, out of scope) and is refused."""
     if getattr(P, "fim", False):
-        return compute_fim_loss(P, model, data, params, active_module, **kwargs)
+        raise NotImplementedError("compute_fim_loss is out of scope (SURVEY §2 row 4); set P.fim = False")
     return compute_mse_loss(P, model, data, params, active_module)
 
 
@@ -96,13 +97,8 @@ def task_adapt(P, model, support, inner_lr, iterations, active_module: Optional[
     fast = extract_module_params(base, copy=(algo == "reptile"))
     losses = []
     for _ in range(int(iterations)):
-        grad_buf = {}
-        loss = compute_loss(P, model, support, params=fast, active_module=active_module, grad_buffer=grad_buf,
-                            update_fisher=True)
-        if grad_buf:  # the Fisher-weighted loss already produced weighted gradients (meta_core.py:47-50)
-            grads = [grad_buf.get(n) for n in fast.keys()]
-        else:
-            grads = torch.autograd.grad(loss, tuple(fast.values()), create_graph=False, allow_unused=True)
+        loss = compute_loss(P, model, support, params=fast, active_module=active_module)
+        grads = torch.autograd.grad(loss, tuple(fast.values()), create_graph=False, allow_unused=True)
         fast = sgd_update(fast, grads, inner_lr)
         losses.append(loss.detach())
     return fast, losses

@@ -47,7 +47,7 @@ class NerfNgpNet(ctypes.Structure):
     _fields_ = [("in_dim", ctypes.c_int32), ("hidden", ctypes.c_int32), ("sigma_depth", ctypes.c_int32),
                 ("geo_feat_dim", ctypes.c_int32), ("color_hidden", ctypes.c_int32),
                 ("color_depth", ctypes.c_int32), ("dir_encoding", ctypes.c_int32), ("sh_levels", ctypes.c_int32),
-                ("use_sigmoid_rgb", ctypes.c_int32)]
+                ("use_sigmoid_rgb", ctypes.c_int32), ("generic_kernels", ctypes.c_int32)]
 
 
 def _addr(s):

@@ -21,17 +21,19 @@ _SHARD_ALIGN = 64  # floats: every rank's shard starts 256-B aligned (float4 Ada
 
 
 class FlatAdam:
-    """world_size > 1 shards the optimiser (``shard=True``, the default there): the flat gradient is
+    """``shard=True`` (opt-in, world_size > 1) shards the optimiser: the flat gradient is
     reduce-scattered (each rank receives the rank-mean of ONE 1/N slice), each rank runs the clip and Adam on its
     slice only (m / v are slice-sized), and the updated parameter slices are all-gathered into every rank's flat
     buffer.  The bytes on the wire equal one all-reduce of the gradient; the optimiser's HBM traffic and m / v memory
     drop N-fold (at N = 8 the production container's 134 M-element Adam, 0.75 ms per step on one GPU, becomes ~0.1
     ms).  A touched-rows exchange of the hash tables does not pay at these batch sizes: one 4096-ray step touches
     ~61 % of an expert's 2^20-entry levels (tools/hash_requests.py), and an (index, value) pair costs
-    more bytes than the dense value at that density.  shard=False keeps the replicated update (one all-reduce)."""
+    more bytes than the dense value at that density.  shard=False (the default) keeps the replicated update (one
+    all-reduce): the sharded collectives have only run emulated (gloo, two ranks on one GPU), never over RCCL, so
+    they stay opt-in until an 8-GPU run covers them."""
 
     def __init__(self, groups: List[Dict], betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 grad_clip=1.0, world_size: int = 1, shard=None):
+                 grad_clip=1.0, world_size: int = 1, shard: bool = False):
         if len(groups) > 8:
             raise ValueError("at most 8 parameter groups (nerf_adam segments)")
         params = [p for g in groups for p in g["params"]]
@@ -40,7 +42,7 @@ class FlatAdam:
         dev = params[0].device
         n = sum(p.numel() for p in params)
         self.world_size = int(world_size)
-        self.shard = (self.world_size > 1) if shard is None else (bool(shard) and self.world_size > 1)
+        self.shard = bool(shard) and self.world_size > 1
         if self.shard:
             import torch.distributed as dist
             self.rank = dist.get_rank()

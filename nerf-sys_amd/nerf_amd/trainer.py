@@ -58,7 +58,8 @@ class NeRFTrainer:
                  n_importance: int = 128, lr_sigma: float = 2e-3, lr_color: float = 2e-3, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.0, grad_clip: Optional[float] = 1.0,
                  color_space: str = "linear", bg: str = "white", sigma_scale: float = 1.0,
-                 world_size: int = 1, device="cuda", overlap: bool = True, precision: str = "fp32"):
+                 world_size: int = 1, device="cuda", overlap: bool = True, precision: str = "fp32",
+                 overlap_with: str = "fwd", bf16_flags: int = 0):
         L = PackedLayout.get()
         self.L = L
         self.P = L.total
@@ -84,6 +85,7 @@ class NeRFTrainer:
         if precision not in K.PRECISIONS:
             raise ValueError(f"precision must be one of {K.PRECISIONS}")
         self.precision = precision  # MLP GEMMs: fp32 (configs[1]) or bf16 (configs[2]); compositing stays fp32
+        self.bf16_flags = int(bf16_flags)  # K.BF16_LAYERED_* (A/B runs of the layered bf16 launches)
         self.betas, self.eps, self.wd = betas, eps, weight_decay
         self.grad_clip = grad_clip
         if color_space not in _CS:
@@ -104,12 +106,13 @@ class NeRFTrainer:
         # 28.1-28.5 ms vs 29.6 ms on one stream; joining the streams before the fine backward instead of at
         # the end of the step serialises it (34.2 ms); stream priorities change nothing.
         self.overlap = bool(overlap) and self.n_nets == 2 and self.device.type == "cuda"
-        # what the coarse backward runs beside: the fine forward (default) or the fine backward (NERF_OVERLAP=bwd,
+        # what the coarse backward runs beside: the fine forward (default) or the fine backward (overlap_with="bwd",
         # A/B runs).  Measured on MI355X: fp32 27.4 (fwd) vs 28.4 ms (bwd); bf16 7.30 vs 7.36 ms (the fused bf16
         # forward is one persistent launch holding every CU's LDS, so the coarse backward mostly queues behind it
         # either way).
-        import os
-        self.overlap_with = os.environ.get("NERF_OVERLAP") or "fwd"
+        if overlap_with not in ("fwd", "bwd"):
+            raise ValueError("overlap_with must be 'fwd' or 'bwd'")
+        self.overlap_with = overlap_with
         self._side = torch.cuda.Stream(device=self.device) if self.overlap else None
 
     # ---- helpers
@@ -176,7 +179,7 @@ class NeRFTrainer:
         t_c = K.sample_stratified(rays, S, True, u_strat, seed)
         xd_c = K.build_xd(rays, t_c)
         ws_c = self._workspace("c", N * S)
-        rs_c = K.mlp_fwd(self.w(0), xd_c, ws_c, True, precision=self.precision)
+        rs_c = K.mlp_fwd(self.w(0), xd_c, ws_c, True, precision=self.precision, bf16_flags=self.bf16_flags)
         _, _, w_c, _, _, drgb_c = K.composite_fwd(rs_c, t_c, bg, self.sigma_scale, gt=gt,
                                                   color_space=self.color_space, inv_count=inv_count,
                                                   loss_sum=self.loss_buf)
@@ -189,7 +192,7 @@ class NeRFTrainer:
             self._side.wait_event(fork)
             with torch.cuda.stream(self._side):
                 d_rs_c = K.composite_bwd(rs_c, t_c, bg, drgb_c, sigma_scale=self.sigma_scale)
-                K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=False, precision=self.precision)
+                K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=False, precision=self.precision, bf16_flags=self.bf16_flags)
                 done = torch.cuda.Event()
                 done.record(self._side)
             return done
@@ -202,7 +205,7 @@ class NeRFTrainer:
             ws_f = self._workspace("f", N * (S + NI))
             ev = self._next_events()
             rs_f = K.mlp_fwd(self.w(fine_k), xd_f, ws_f, True, events=ev["fwd"] if ev else None,
-                             precision=self.precision)
+                             precision=self.precision, bf16_flags=self.bf16_flags)
             if self.overlap and self.overlap_with == "bwd":
                 side_done = coarse_bwd_on_side()
             _, _, _, _, _, drgb_f = K.composite_fwd(rs_f, t_f, bg, self.sigma_scale, gt=gt,
@@ -210,7 +213,7 @@ class NeRFTrainer:
                                                     loss_sum=self.loss_buf)
             d_rs_f = K.composite_bwd(rs_f, t_f, bg, drgb_f, sigma_scale=self.sigma_scale)
             K.mlp_bwd(self.w(fine_k), N * (S + NI), d_rs_f, ws_f, d_w=self.g(fine_k), accumulate=False,
-                      events=ev["bwd"] if ev else None, precision=self.precision)
+                      events=ev["bwd"] if ev else None, precision=self.precision, bf16_flags=self.bf16_flags)
             if ev:
                 self.timing["M"] = N * (S + NI)
         if side_done is not None:
@@ -218,7 +221,7 @@ class NeRFTrainer:
         else:
             d_rs_c = K.composite_bwd(rs_c, t_c, bg, drgb_c, sigma_scale=self.sigma_scale)
             K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=(fine_k == 0 and NI > 0),
-                      precision=self.precision)
+                      precision=self.precision, bf16_flags=self.bf16_flags)
         allreduce_flat(self.gbuf, self.world_size)
         self.step_count += 1
         if self.grad_clip is not None and self.grad_clip > 0:

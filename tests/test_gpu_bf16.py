@@ -103,9 +103,9 @@ def test_bf16_engine_tracks_fp32_loss(K):
     assert (a[-10:].mean() - b[-10:].mean()).abs() <= 0.15 * b[-10:].mean()
 
 
-def test_fused_forward_matches_layered(K, wpk, monkeypatch):
+def test_fused_forward_matches_layered(K, wpk):
     """The single-launch fused bf16 forward (mlp_bf16_fused.hpp) against the layer-by-layer bf16 GEMM path
-    (NERF_BF16_FUSED=0): the same bf16 rounding points and k order, only the bias enters the fp32 accumulator
+    (bf16_flags=BF16_LAYERED_FWD): the same bf16 rounding points and k order, only the bias enters the fp32 accumulator
     first instead of last — outputs agree to bf16 rounding flips, the saved activations feed the same backward."""
     M = 5000  # two row tiles short of a multiple of 256: pad rows in the last tile
     x = _xd(M, 9).to(DEV)
@@ -113,11 +113,11 @@ def test_fused_forward_matches_layered(K, wpk, monkeypatch):
     gup = (torch.randn(M, 4, generator=g) * 1e-3).to(DEV)
     res = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("NERF_BF16_FUSED", mode)
+        fl = K.BF16_LAYERED_FWD if mode == "0" else 0
         ws = K.mlp_workspace(M, True, DEV, "bf16")
-        out = K.mlp_fwd(wpk, x, ws, True, precision="bf16")
-        d_w = K.mlp_bwd(wpk, M, gup, ws, precision="bf16")
-        inf = K.mlp_fwd(wpk, x, K.mlp_workspace(M, False, DEV, "bf16"), False, precision="bf16")
+        out = K.mlp_fwd(wpk, x, ws, True, precision="bf16", bf16_flags=fl)
+        d_w = K.mlp_bwd(wpk, M, gup, ws, precision="bf16", bf16_flags=fl)
+        inf = K.mlp_fwd(wpk, x, K.mlp_workspace(M, False, DEV, "bf16"), False, precision="bf16", bf16_flags=fl)
         assert torch.equal(out, inf), f"mode {mode}: inference != training forward"
         res[mode] = (out.cpu(), d_w.cpu())
     (o0, g0), (o1, g1) = res["0"], res["1"]
@@ -134,10 +134,10 @@ def test_fused_forward_matches_layered(K, wpk, monkeypatch):
 
 
 @pytest.mark.parametrize("M", [1, 5000, 40001, 786432])
-def test_fused_backward_matches_layered(K, wpk, monkeypatch, M):
+def test_fused_backward_matches_layered(K, wpk, M):
     """The fused per-layer bf16 backward (mlp_bf16_bwd.hpp: input + weight gradient of a trunk layer in one launch,
     ReLU mask from the saved input; the head / colour "tail" in one launch, mlp_bf16_tail.hpp) against the layered
-    launches (NERF_BF16_FUSED_BWD=0): the same bf16 operands, rounding points and MFMA k order, so dZ7 and the
+    launches (bf16_flags=BF16_LAYERED_BWD): the same bf16 operands, rounding points and MFMA k order, so dZ7 and the
     256-wide trunk weight gradients are BITWISE equal; the trunk biases (column sums by the io waves that stage the
     rows), the head / colour sums (each split in two row halves) and the narrow trunk.0 / trunk.4-encoding sums (4x
     finer sub-splits) are the same fp32 terms in another fixed order: within 1e-5 of their scale, and bitwise
@@ -149,12 +149,12 @@ def test_fused_backward_matches_layered(K, wpk, monkeypatch, M):
     g = torch.Generator().manual_seed(23)
     gup = (torch.randn(M, 4, generator=g) * 1e-3).to(DEV)
     ws = K.mlp_workspace(M, True, DEV, "bf16")
-    monkeypatch.setenv("NERF_BF16_FUSED_BWD", "0")  # a forward for the layered backward also writes its ReLU bitmasks
-    K.mlp_fwd(wpk, x, ws, True, precision="bf16")
+    # a forward for the layered backward also writes its ReLU bitmasks (the fused backward ignores them)
+    K.mlp_fwd(wpk, x, ws, True, precision="bf16", bf16_flags=K.BF16_LAYERED_BWD)
     res = {}
     for mode in ("0", "1", "1b"):
-        monkeypatch.setenv("NERF_BF16_FUSED_BWD", mode[0])
-        res[mode] = K.mlp_bwd(wpk, M, gup, ws, precision="bf16").cpu()
+        fl = K.BF16_LAYERED_BWD if mode == "0" else 0
+        res[mode] = K.mlp_bwd(wpk, M, gup, ws, precision="bf16", bf16_flags=fl).cpu()
         torch.cuda.synchronize()
     assert torch.isfinite(res["1"]).all()
     assert torch.equal(res["1"], res["1b"]), "fused backward not reproducible"

@@ -252,37 +252,11 @@ def test_reptile_many_tensors_chunked():
         assert torch.equal(m.t[n].cpu(), ref[n]), n
 
 
-def test_fim_loss_fallback_and_weighted():
-    """compute_fim_loss (nerfs/losses.py:35-151): without a Fisher store it is the plain MSE; with one (a stub
-    store / weight of the reference's interface) the loss and the support-path gradient buffer are the
-    weighted ones and the store receives the squared unweighted gradients."""
-    from nerf_amd.losses import compute_fim_loss, compute_mse_loss
+def test_fim_loss_refused():
+    """compute_fim_loss (nerfs/losses.py:35-151) is dead code in the reference: P.fim raises."""
+    from nerf_amd.meta import compute_loss
     z = load("meta")
-    model, net = _meta_model()
+    model, _ = _meta_model()
     P = types.SimpleNamespace(algo="fomaml", fim=True, ray_samples=32, chunk_points=1 << 20, color_space="linear")
-    data = {"rays": z["rays"].to(DEV), "rgbs": z["gt"].to(DEV)}
-    base = compute_mse_loss(P, model, data, active_module=0)
-    assert torch.allclose(compute_fim_loss(P, model, data, active_module=0), base, rtol=1e-6, atol=0)
-
-    tracked = [(n, p) for n, p in net.meta_named_parameters() if n.startswith("color_mlp")]
-
-    class Store:
-        def __init__(self):
-            self.tracked, self.updates = tracked, []
-
-        def update_from_grads(self, sq):
-            self.updates.append(sq)
-
-    class Weight:
-        def fim_weight(self, grads, mse_i=None, per_sample=False, clamp=(0.2, 5.0)):
-            return torch.tensor(2.0, device=DEV)
-
-    net.fisher_store, net.fim_loss = Store(), Weight()
-    model.fisher_store, model.fim_loss = True, True
-    buf = {}
-    loss = compute_fim_loss(P, model, data, active_module=0, grad_buffer=buf, update_fisher=True)
-    assert torch.allclose(loss, 2.0 * base, rtol=1e-6, atol=0)
-    ref = torch.autograd.grad(compute_mse_loss(P, model, data, active_module=0), [p for _, p in tracked])
-    for (n, _), g in zip(tracked, ref):
-        assert torch.allclose(buf[n], 2.0 * g, rtol=1e-5, atol=1e-9), n
-        assert torch.allclose(net.fisher_store.updates[0][n], g.pow(2), rtol=1e-5, atol=1e-12), n
+    with pytest.raises(NotImplementedError):
+        compute_loss(P, model, {"rays": z["rays"].to(DEV), "rgbs": z["gt"].to(DEV)}, active_module=0)

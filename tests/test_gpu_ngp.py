@@ -344,10 +344,10 @@ def test_ngp_deep_config_vs_oracle(N, depths):
 
 
 @pytest.mark.parametrize("levels,M", [(16, 1), (16, 33), (16, 777), (8, 40001)])
-def test_ngp_production_backward_kernel(N, levels, M, monkeypatch):
+def test_ngp_production_backward_kernel(N, levels, M):
     """The compile-time production-shape backward (ngp_bwd_prod_kernel: 2 x 64 sigma, 1 + 15 head, SH degree 4,
     2 x 64 colour, enc <= 32 wide) against the oracle's gradients and against the generic plan-driven kernel
-    (NERF_NGP_PROD=0) on the same inputs; ragged tile counts included."""
+    (NerfNgpNet.generic_kernels = 1) on the same inputs; ragged tile counts included."""
     from nerf_amd.ngp import InstantNGP
     torch.manual_seed(5)
     box = torch.tensor([[-1.5] * 3, [1.5] * 3])
@@ -363,7 +363,7 @@ def test_ngp_production_backward_kernel(N, levels, M, monkeypatch):
     gup = torch.randn(M, 4, generator=g)
 
     def grads(prod):
-        monkeypatch.setenv("NERF_NGP_PROD", "1" if prod else "0")
+        net.net_struct.generic_kernels = 0 if prod else 1
         net.zero_grad(set_to_none=True)
         out = net(x_d.to(DEV))
         (out * gup.to(DEV)).sum().backward()
@@ -390,8 +390,9 @@ def test_ngp_production_backward_kernel(N, levels, M, monkeypatch):
         assert _err(gp[n], gg[n]) <= tol, n
 
 
+@pytest.mark.parametrize("interp", ["Linear", "Smoothstep", "Nearest"])
 @pytest.mark.parametrize("levels,M", [(16, 1), (16, 4097), (8, 50001)])
-def test_density_enc_fused_bitwise(N, levels, M):
+def test_density_enc_fused_bitwise(N, levels, M, interp):
     """nerf_ngp_density_enc (hash encoding into LDS + sigma trunk/head in one launch) is bitwise the two-launch
     nerf_hash_encode + nerf_ngp_density path, points inside and outside the box."""
     from nerf_amd import ngp as G
@@ -401,7 +402,7 @@ def test_density_enc_fused_bitwise(N, levels, M):
     net = InstantNGP(scene_box=box, hidden=64, sigma_depth=2, color_hidden=64, color_depth=2,
                      dir_encoding="spherical",
                      hash_enc_conf=dict(levels=levels, features_per_level=2, log2_hashmap_size=14, min_res=8,
-                                        max_res=512, interpolation="Linear")).to(DEV)
+                                        max_res=512, interpolation=interp)).to(DEV)
     with torch.no_grad():
         net.xyz_encoder.hash_table.uniform_(-0.5, 0.5)
     g = torch.Generator().manual_seed(M)
@@ -431,8 +432,9 @@ def test_density_enc_unsupported_shape_falls_back(N):
     assert s.shape == (100, 1) and torch.isfinite(s).all()
 
 
+@pytest.mark.parametrize("interp", ["Linear", "Smoothstep", "Nearest"])
 @pytest.mark.parametrize("levels,M", [(16, 1), (16, 4097), (8, 50001)])
-def test_fwd_enc_fused_bitwise(N, levels, M):
+def test_fwd_enc_fused_bitwise(N, levels, M, interp):
     """nerf_ngp_fwd_enc (encoding into LDS and to HBM + the fused MLP forward in one launch) is bitwise the
     nerf_hash_encode + nerf_ngp_fwd pair: rgb_sigma and the enc the backward reads."""
     from nerf_amd import ngp as G
@@ -442,7 +444,7 @@ def test_fwd_enc_fused_bitwise(N, levels, M):
     net = InstantNGP(scene_box=box, hidden=64, sigma_depth=2, color_hidden=64, color_depth=2,
                      dir_encoding="spherical",
                      hash_enc_conf=dict(levels=levels, features_per_level=2, log2_hashmap_size=14, min_res=8,
-                                        max_res=512, interpolation="Linear")).to(DEV)
+                                        max_res=512, interpolation=interp)).to(DEV)
     with torch.no_grad():
         net.xyz_encoder.hash_table.uniform_(-0.5, 0.5)
     g = torch.Generator().manual_seed(M + 1)
@@ -458,11 +460,13 @@ def test_fwd_enc_fused_bitwise(N, levels, M):
     assert torch.equal(out.cpu(), out_ref.cpu())
 
 
+@pytest.mark.parametrize("interp", ["Linear", "Smoothstep"])
 @pytest.mark.parametrize("levels,M", [(16, 33), (16, 40000), (8, 7777)])
-def test_bwd_hash_fused_vs_pair(N, levels, M):
+def test_bwd_hash_fused_vs_pair(N, levels, M, interp):
     """nerf_ngp_bwd_hash (MLP backward + the table scatter from inside the kernel) against nerf_ngp_bwd +
     nerf_hash_encode_bwd: d_w bitwise (the same MLP backward and reduce), d_table the same fp32 terms added by
-    atomics in another order (within 1e-6 of scale), accumulating into a non-zero target."""
+    atomics in another order (within 1e-6 of scale), accumulating into a non-zero target.  Linear and Smoothstep
+    grids (the in-kernel corner weights are hash_level's, re-derived for the scatter); Nearest has no fused kernel."""
     from nerf_amd import ngp as G
     from nerf_amd.ngp import InstantNGP
     torch.manual_seed(12)
@@ -470,7 +474,7 @@ def test_bwd_hash_fused_vs_pair(N, levels, M):
     net = InstantNGP(scene_box=box, hidden=64, sigma_depth=2, color_hidden=64, color_depth=2,
                      dir_encoding="spherical",
                      hash_enc_conf=dict(levels=levels, features_per_level=2, log2_hashmap_size=14, min_res=8,
-                                        max_res=512, interpolation="Linear")).to(DEV)
+                                        max_res=512, interpolation=interp)).to(DEV)
     with torch.no_grad():
         net.xyz_encoder.hash_table.uniform_(-0.5, 0.5)
     g = torch.Generator().manual_seed(M + 2)

@@ -5,7 +5,7 @@ with the algorithmic rates: MFMA FLOP = 2 * 500,864 MAC per sample (forward), 4 
 
   python tools/bench_mlp.py [--precision bf16] [--M 786432] [--iters 20]
 
-NERF_BF16_FUSED=0 in the environment selects the layer-by-layer bf16 forward for A/B runs."""
+--bf16-flags selects the layered bf16 launches for A/B runs (1 = layer-by-layer forward, 2 = layered backward)."""
 import argparse
 import json
 import os
@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--precision", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--M", type=int, default=786432)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--bf16-flags", type=int, default=0)
     a = ap.parse_args()
     from nerf_amd import kernels as K
     from nerf_amd.vanilla import VanillaNeRF
@@ -51,11 +52,12 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / a.iters
 
-    res = {"precision": a.precision, "M": a.M, "fused_fwd": os.environ.get("NERF_BF16_FUSED", "1") != "0"}
-    res["fwd_infer_ms"] = timeit(lambda: K.mlp_fwd(w, x, ws_i, False, out=out, precision=a.precision))
-    res["fwd_train_ms"] = timeit(lambda: K.mlp_fwd(w, x, ws_t, True, out=out, precision=a.precision))
-    K.mlp_fwd(w, x, ws_t, True, out=out, precision=a.precision)
-    res["bwd_ms"] = timeit(lambda: K.mlp_bwd(w, a.M, gup, ws_t, d_w=d_w, precision=a.precision))
+    res = {"precision": a.precision, "M": a.M, "bf16_flags": a.bf16_flags}
+    fl = a.bf16_flags
+    res["fwd_infer_ms"] = timeit(lambda: K.mlp_fwd(w, x, ws_i, False, out=out, precision=a.precision, bf16_flags=fl))
+    res["fwd_train_ms"] = timeit(lambda: K.mlp_fwd(w, x, ws_t, True, out=out, precision=a.precision, bf16_flags=fl))
+    K.mlp_fwd(w, x, ws_t, True, out=out, precision=a.precision, bf16_flags=fl)
+    res["bwd_ms"] = timeit(lambda: K.mlp_bwd(w, a.M, gup, ws_t, d_w=d_w, precision=a.precision, bf16_flags=fl))
     for k in ("fwd_infer", "fwd_train"):
         res[k + "_tflops"] = round(2 * MAC * a.M / (res[k + "_ms"] * 1e-3) / 1e12, 1)
     res["bwd_tflops"] = round(4 * MAC * a.M / (res["bwd_ms"] * 1e-3) / 1e12, 1)

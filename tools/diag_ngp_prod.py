@@ -25,7 +25,7 @@ gup = torch.randn(M, 4, generator=g)
 
 
 def grads(prod):
-    os.environ["NERF_NGP_PROD"] = "1" if prod else "0"
+    net.net_struct.generic_kernels = 0 if prod else 1
     net.zero_grad(set_to_none=True)
     out = net(x_d.cuda())
     (out * gup.cuda()).sum().backward()
