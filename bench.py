@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark: rays/sec of the full NeRF train step (BASELINE.json configs[1]: Lego-style 800x800,
 64 coarse + 128 fine hierarchical, fp32, two networks), data parallel over N GPUs (one process per
-GPU, ONE RCCL all-reduce of the flat gradient buffer per step).
+GPU, the flat gradient buffer all-reduced over RCCL in two buckets per step: coarse net as soon as its backward
+ends, fine net + loss after the fine backward).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--strong] [--path engine|dropin] [--precision fp32|bf16]
 
@@ -22,13 +23,19 @@ Prints ONE JSON line on rank 0 (contract in the task statement), with
                   With --precision bf16 the MLP is one fused forward launch plus one fused backward launch
                   per trunk layer (HBM-bound): the kernel with the largest total time per step is reported
                   against the HBM peak, with algorithmic bytes per launch (roofline_bf16).
+  bf16 / fp32   — the other MLP precision's engine step timed in the same run (BASELINE configs[2] beside
+                  configs[1]), with its own roofline, step MFMA fraction and (N = 1) its drop-in loop body.
+  psnr          — (N = 1) the metric's PSNR half: both precisions' engines, from the same seed-0 weights and
+                  batches, continue to --psnr-steps total steps (outside the timed region), then render every
+                  held-out 800x800 view; mean full-image PSNR per precision and the bf16 - fp32 gap.
+  dp            — (N > 1) per-rank step time (max / min) and HIP-event time of each all-reduce bucket.
   cpu_baseline  — the CPU oracle (a restatement of the reference's PyTorch path, pinned to its golden
                   vectors) running the same train step (4096 rays, 64+128, 2 nets), median of >= 5 steps
-                  on this host (rank 0, N=1).
+                  on this host's CPU share (rank 0, N=1); `all_cores` beside it at os.cpu_count() threads.
   dropin        — (N=1) the reference's own loop body (an/pipelines/online_stage/runtime_adapt.py:286-310:
-                  render_rays -> compute_mse_loss -> backward -> clip_grad_norm_ -> torch Adam) on this
-                  repo's drop-in render_rays + VanillaNeRF autograd path, same workload, timed beside the
-                  fused engine.  --path dropin makes it the reported value.
+                  render_rays -> compute_mse_loss -> backward -> clip_grad_norm_ -> torch Adam; under
+                  autocast + GradScaler for bf16) on this repo's drop-in render_rays + VanillaNeRF autograd
+                  path, same workload, timed beside the fused engine.  --path dropin makes it the reported value.
 """
 import argparse
 import json
@@ -76,7 +83,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in path measurement beside the engine")
     ap.add_argument("--no-psnr", action="store_true",
-                    help="skip the full-image PSNR of one held-out view rendered after the timed steps")
+                    help="skip the full-image PSNR record (training to --psnr-steps + held-out renders, N = 1 only)")
     ap.add_argument("--no-overlap", action="store_true", help="run the coarse-net backward on the main stream")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (the product); gloo = rehearsal of N ranks sharing the visible GPUs")
@@ -84,6 +91,13 @@ def parse():
                     help="MLP GEMM precision: fp32 = BASELINE configs[1] (default, the headline), bf16 = configs[2]")
     ap.add_argument("--timing-steps", type=int, default=3,
                     help="timed steps (the last ones) whose fine-net launches are bracketed by HIP events")
+    ap.add_argument("--bf16-flags", type=int, default=0,
+                    help="A/B runs of the layered bf16 launches (1 = layered forward, 2 = layered backward)")
+    ap.add_argument("--no-other-precision", action="store_true",
+                    help="skip the sub-record of the other MLP precision (bf16 beside fp32, or fp32 beside bf16)")
+    ap.add_argument("--psnr-steps", type=int, default=3000,
+                    help="total train steps of each precision's engine before the held-out PSNR renders")
+    ap.add_argument("--psnr-views", type=int, default=2, help="held-out 800x800 views rendered for the PSNR")
     return ap.parse_args()
 
 
@@ -115,13 +129,23 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(S, NI, n, steps):
-    """The CPU oracle's train step (same op graph: 2 nets, 64+128, MSE coarse+fine, clip, Adam) on an n-ray
-    batch through a Blender-style camera: one warm-up step on 128 rays, then the median of `steps` steps.
-    Threads = the host CPU share this process is given (OMP_NUM_THREADS on the GPU box), not os.cpu_count(),
-    which there reports the whole machine."""
+def _cpu_share():
+    """What this process may run on: the affinity mask and the cgroup v2 CPU quota (cpu.max), if readable."""
+    info = {"host_cpus": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+def _oracle_step_rate(S, NI, n, steps, threads, budget_s=None):
     from oracle import nerf_oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     torch.set_num_threads(threads)
     torch.manual_seed(0)
     g = torch.Generator().manual_seed(0)
@@ -136,35 +160,71 @@ def cpu_baseline(S, NI, n, steps):
         t0 = time.perf_counter()
         tr.step(rays, gt, S, n_importance=NI)
         times.append(time.perf_counter() - t0)
-    med = statistics.median(times)
-    return {"value": round(n / med, 2), "unit": "rays/s", "cores": threads, "kind": "port",
-            "sample": f"median of {steps} oracle train steps x {n} rays (64+128, 2 nets, fp32, MSE coarse+fine, "
-                      f"clip, Adam): {med:.2f} s/step (steps {', '.join(f'{t:.2f}' for t in times)} s)",
-            "host_cpus": os.cpu_count(), "cpu_model": _cpu_model(), "torch_threads": torch.get_num_threads()}
+        if budget_s is not None and sum(times) > budget_s:
+            break
+    return statistics.median(times), times
 
 
-def dropin_run(rb, dev, a, world, rank, n_local):
+def cpu_baseline(S, NI, n, steps):
+    """The CPU oracle's train step (same op graph: 2 nets, 64+128, MSE coarse+fine, clip, Adam) on an n-ray
+    batch through a Blender-style camera: one warm-up step on 128 rays, then the median of `steps` steps.
+    Threads = the host CPU share this process is given (OMP_NUM_THREADS on the GPU box: 16 of the machine's CPUs).
+    BASELINE.md §3 asks for torch.set_num_threads(os.cpu_count()): that leg runs beside it as `all_cores` on a
+    smaller sample (1024 rays, median of <= 3 steps, ~30 s budget) — on the GPU box os.cpu_count() reports the whole
+    machine, more threads than this process's share (affinity / cgroup quota are reported with it)."""
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    med, times = _oracle_step_rate(S, NI, n, steps, threads)
+    rec = {"value": round(n / med, 2), "unit": "rays/s", "cores": threads, "kind": "port",
+           "sample": f"median of {steps} oracle train steps x {n} rays (64+128, 2 nets, fp32, MSE coarse+fine, "
+                     f"clip, Adam): {med:.2f} s/step (steps {', '.join(f'{t:.2f}' for t in times)} s)",
+           "cpu_model": _cpu_model(), "torch_threads": torch.get_num_threads(), **_cpu_share()}
+    allc = os.cpu_count() or 1
+    if allc != threads:
+        n2 = min(n, 1024)
+        med2, times2 = _oracle_step_rate(S, NI, n2, 3, allc, budget_s=30.0)
+        rec["all_cores"] = {"value": round(n2 / med2, 2), "unit": "rays/s", "cores": allc,
+                            "torch_threads": torch.get_num_threads(),
+                            "sample": f"median of {len(times2)} oracle train steps x {n2} rays at "
+                                      f"torch.set_num_threads(os.cpu_count()={allc}) (BASELINE.md §3): "
+                                      f"{', '.join(f'{t:.2f}' for t in times2)} s"}
+        torch.set_num_threads(threads)
+    return rec
+
+
+def dropin_run(rb, dev, a, world, rank, n_local, precision="fp32"):
     """The reference loop body (runtime_adapt.py:286-310) on the drop-in surface: HierarchicalNeRF (coarse +
     fine VanillaNeRF, autograd through the HIP MLP / compositing / sampling ops) -> compute_mse_loss (coarse +
-    fine terms) -> backward -> clip_grad_norm_(1.0) -> torch.optim.Adam ('sigma' / 'color' groups).  The ray
-    batch comes from images resident in HBM (the reference's DataLoader + .to(device) is not timed)."""
+    fine terms) -> backward -> clip_grad_norm_(1.0) -> torch.optim.Adam ('sigma' / 'color' groups).  precision
+    "bf16" runs it as the reference's use_amp=True body (configs/train.json): autocast(fp16) around the loss ->
+    GradScaler scale / unscale_ / step / update; the expert then dispatches to the bf16 MLP kernels
+    (vanilla.amp_precision).  Adam is torch's fused implementation (no host sync inside GradScaler.step; foreach
+    if this torch build lacks it).  The ray batch comes from images resident in HBM (the reference's DataLoader +
+    .to(device) is not timed)."""
     from types import SimpleNamespace
     from nerf_amd.losses import compute_mse_loss
     from nerf_amd.vanilla import HierarchicalNeRF
     torch.manual_seed(0)
     model = HierarchicalNeRF().to(dev).train()
     grp = model.get_param_groups()
-    opt = torch.optim.Adam([{"params": grp["sigma"]["params"], "lr": 2e-3},
-                            {"params": grp["color"]["params"], "lr": 2e-3}])
+    groups = [{"params": grp["sigma"]["params"], "lr": 2e-3}, {"params": grp["color"]["params"], "lr": 2e-3}]
+    try:
+        opt, kind = torch.optim.Adam(groups, fused=True), "torch.optim.Adam(fused=True)"
+    except (RuntimeError, ValueError):
+        opt, kind = torch.optim.Adam(groups, foreach=True), "torch.optim.Adam(foreach=True)"
+    use_amp = precision == "bf16"
+    scaler = torch.amp.GradScaler("cuda", enabled=use_amp)
     P = SimpleNamespace(ray_samples=a.samples, n_importance=a.importance, chunk_points=1 << 22, color_space="linear")
 
     def one(step):
         rays, gt = _batch(rb, a, step, rank, world, n_local)
-        loss = compute_mse_loss(P, model, {"rays": rays, "rgbs": gt})
         opt.zero_grad(set_to_none=True)
-        loss.backward()
+        with torch.autocast("cuda", dtype=torch.float16, enabled=use_amp):
+            loss = compute_mse_loss(P, model, {"rays": rays, "rgbs": gt})
+        scaler.scale(loss).backward()
+        scaler.unscale_(opt)
         torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
-        opt.step()
+        scaler.step(opt)
+        scaler.update()
         return loss
 
     for s in range(a.warmup):
@@ -175,10 +235,14 @@ def dropin_run(rb, dev, a, world, rank, n_local):
         loss = one(s)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    return {"value": round(n_local * a.steps / el, 1), "unit": "rays/s", "ms_per_step": round(el / a.steps * 1e3, 3),
-            "final_loss": round(float(loss.item()), 6),
-            "path": "render_rays + HierarchicalNeRF(VanillaNeRF x2) autograd + compute_mse_loss + "
-                    "clip_grad_norm_ + torch.optim.Adam (runtime_adapt.py:286-310)"}
+    rec = {"value": round(n_local * a.steps / el, 1), "unit": "rays/s", "ms_per_step": round(el / a.steps * 1e3, 3),
+           "final_loss": round(float(loss.item()), 6), "optimizer": kind,
+           "path": "render_rays + HierarchicalNeRF(VanillaNeRF x2) autograd + compute_mse_loss + "
+                   "clip_grad_norm_ + " + kind + " (runtime_adapt.py:286-310)"}
+    if use_amp:
+        rec["amp"] = ("torch.autocast(fp16) -> bf16 MLP kernels + fp32 compositing; GradScaler scale "
+                      f"{scaler.get_scale():.0f} after {a.warmup + a.steps} steps (halves on any inf)")
+    return rec
 
 
 def _batch(rb, a, step, rank, world, n_local):
@@ -280,6 +344,102 @@ def roofline(tm, bf16, overlap, bf16_flags=0):
     return roof
 
 
+def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl):
+    """The fused train step (NeRFTrainer) timed over a.steps after a.warmup: value, ms/step, the live-event roofline,
+    and (N > 1) the per-rank exchange diagnostics.  Returns (record, trainer, (coarse, fine))."""
+    from nerf_amd.trainer import NeRFTrainer
+    from nerf_amd.vanilla import VanillaNeRF
+    torch.manual_seed(0)   # the same initial weights for every precision (the PSNR comparison starts from them)
+    coarse, fine = VanillaNeRF().to(dev), VanillaNeRF().to(dev)
+    tr = NeRFTrainer(coarse, fine, n_samples=a.samples, n_importance=a.importance, world_size=world, device=dev,
+                     overlap=not a.no_overlap, precision=precision,
+                     bf16_flags=a.bf16_flags if precision == "bf16" else 0)
+
+    def one(step):
+        rays, gt = _batch(rb, a, step, rank, world, n_local)
+        return tr.step(rays, gt, seed=step * world + rank)
+
+    for s in range(a.warmup):
+        loss = one(s)
+    torch.cuda.synchronize()
+    n_ev = max(1, min(a.timing_steps, a.steps))
+    tr.enable_timing(n_ev, skip=a.steps - n_ev)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(a.warmup, a.warmup + a.steps):
+        loss = one(s)
+    barrier()
+    torch.cuda.synchronize()
+    el_local = time.perf_counter() - t0
+    tm = tr.collect_timing()
+    el = el_local
+    dp = None
+    if world > 1:
+        ar = tm.get("allreduce") or []
+        nb = max((len(x) for x in ar), default=0)
+        ar_mean = [sum(x[b] for x in ar if len(x) > b) / max(1, len(ar)) for b in range(2)] if nb else [0.0, 0.0]
+        mine = torch.tensor([el_local] + ar_mean, dtype=torch.float64, device=dev)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        rows = [x.tolist() for x in allr]
+        el = max(r[0] for r in rows)
+        dp = {"world_size": dist.get_world_size(), "backend": "nccl (RCCL)" if nccl else "gloo (rehearsal)",
+              "step_ms_max": round(el / a.steps * 1e3, 3), "step_ms_min": round(min(r[0] for r in rows) / a.steps * 1e3, 3),
+              "allreduce_ms_per_rank": [[round(r[1], 4), round(r[2], 4)] for r in rows],
+              "allreduce_note": "HIP events on the launching stream around each bucket's all_reduce (bucket 1 = coarse "
+                                "net gradient, issued on the side stream right after the coarse backward; bucket 2 = "
+                                "fine gradient + loss, after the fine backward), mean over the event steps; includes "
+                                "the wait for the slowest rank",
+              "bytes_per_step": int(tr.gbuf.numel() * 4)}
+    rec = {"value": round(n_local * world * a.steps / el, 1), "ms_per_step": round(el / a.steps * 1e3, 3),
+           "final_loss": round(float(loss.item()), 6),
+           "roofline": dict(roofline(tm, precision == "bf16", tr.overlap, tr.bf16_flags), event_steps=n_ev)}
+    peak = BF16_MFMA_PEAK_TFLOPS if precision == "bf16" else FP32_MFMA_PEAK_TFLOPS
+    rec["step_mfma_frac"] = round(rec["value"] * FLOP_PER_RAY / world / 1e12 / peak, 4)
+    if dp:
+        rec["dp"] = dp
+    return rec, tr, (coarse, fine)
+
+
+def psnr_run(a, rb, scene, runs, rank, world, n_local):
+    """The metric's PSNR half (runtime_adapt.py:150-157): every engine trainer in ``runs`` (precision -> (trainer,
+    (coarse, fine)), all started from the same seed-0 weights and fed the same batches) continues to a.psnr_steps
+    total steps, then renders every held-out 800x800 view (64 + 128, fp32 compositing) — outside the timed region."""
+    from nerf_amd.losses import image_psnr
+    from nerf_amd.ray_rendering import render_image
+    fx, fy, cx, cy = scene.intrinsics
+    out = {}
+    for prec, (tr, (coarse, fine)) in runs.items():
+        done = tr.step_count
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s in range(done, a.psnr_steps):
+            rays, gt = _batch(rb, a, s, rank, world, n_local)
+            tr.step(rays, gt, seed=s * world + rank)
+        torch.cuda.synchronize()
+        train_s = time.perf_counter() - t0
+        tr.sync_to_modules()
+        coarse.eval(), fine.eval()
+        ps = []
+        for v in range(scene.test_poses.shape[0]):
+            img, _, _ = render_image(coarse, H=scene.H, W=scene.W, fx=fx, fy=fy, cx=cx, cy=cy, c2w=scene.test_poses[v],
+                                     near=scene.near, far=scene.far, ray_samples=a.samples, n_importance=a.importance,
+                                     fine_model=fine, ndc=(scene.focal, 1.0) if scene.ndc else None)
+            ps.append(image_psnr(img, scene.test_images[v], "linear"))
+        coarse.train(), fine.train()
+        out[prec] = {"psnr": round(sum(ps) / len(ps), 3), "per_view": [round(p, 3) for p in ps],
+                     "steps": tr.step_count, "train_s_after_timed": round(train_s, 2)}
+    rec = {"steps": a.psnr_steps, "views": int(scene.test_poses.shape[0]), "image": f"{scene.W}x{scene.H}",
+           "samples": [a.samples, a.importance], **out,
+           "protocol": "engine trainers from the same seed-0 weights and the same 4096-ray batches / jitter seeds, "
+                       "trained to `steps` total steps (the timed steps included), then full-image PSNR of each "
+                       "held-out view in linear colour space (runtime_adapt.py:150-157), averaged"}
+    if "fp32" in out and "bf16" in out:
+        rec["bf16_minus_fp32_db"] = round(out["bf16"]["psnr"] - out["fp32"]["psnr"], 3)
+    return rec
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -302,60 +462,41 @@ def main():
         if world > 1:
             dist.barrier(device_ids=[dev.index]) if nccl else dist.barrier()
 
-    if a.path == "dropin" and (world > 1 or a.precision != "fp32"):
-        raise SystemExit("--path dropin runs on one GPU in fp32 (the reference loop body has no gradient exchange)")
+    if a.path == "dropin" and world > 1:
+        raise SystemExit("--path dropin runs on one GPU (the reference loop body has no gradient exchange)")
     if a.strong and a.batch % world:
         raise SystemExit("--strong needs --batch divisible by the number of GPUs")
     n_local = a.batch // world if a.strong else a.batch
 
     from nerf_amd.scene import make_blender_scene, make_llff_scene
-    from nerf_amd.trainer import NeRFTrainer, RayBatcher
-    from nerf_amd.vanilla import VanillaNeRF
+    from nerf_amd.trainer import RayBatcher
 
     torch.manual_seed(0)
+    n_test = 1 if a.no_psnr else a.psnr_views
     if a.scene == "llff":
-        scene = make_llff_scene(n_train=min(a.train_views, 20), n_test=1, seed=0, device=dev)
+        scene = make_llff_scene(n_train=min(a.train_views, 20), n_test=n_test, seed=0, device=dev)
     else:
-        scene = make_blender_scene(n_train=a.train_views, n_test=1, H=800, W=800, seed=0, device=dev)
+        scene = make_blender_scene(n_train=a.train_views, n_test=n_test, H=800, W=800, seed=0, device=dev)
     rb = RayBatcher(scene, dev)
     bf16 = a.precision == "bf16"
+    other = "fp32" if bf16 else "bf16"
 
+    runs = {}
     engine = None
     if a.path == "engine" or world == 1:
-        coarse, fine = VanillaNeRF().to(dev), VanillaNeRF().to(dev)
-        tr = NeRFTrainer(coarse, fine, n_samples=a.samples, n_importance=a.importance, world_size=world, device=dev,
-                         overlap=not a.no_overlap, precision=a.precision)
-
-        def one(step):
-            rays, gt = _batch(rb, a, step, rank, world, n_local)
-            return tr.step(rays, gt, seed=step * world + rank)
-
-        for s in range(a.warmup):
-            loss = one(s)
-        torch.cuda.synchronize()
-        n_ev = max(1, min(a.timing_steps, a.steps))
-        tr.enable_timing(n_ev, skip=a.steps - n_ev)
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for s in range(a.warmup, a.warmup + a.steps):
-            loss = one(s)
-        barrier()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el], device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        engine = {"value": round(n_local * world * a.steps / el, 1), "ms_per_step": round(el / a.steps * 1e3, 3),
-                  "final_loss": round(float(loss.item()), 6),
-                  "roofline": dict(roofline(tr.collect_timing(), bf16, tr.overlap), event_steps=n_ev)}
-
+        engine, tr, nets = engine_run(a, dev, rb, world, rank, n_local, a.precision, barrier, nccl)
+        runs[a.precision] = (tr, nets)
     drop = None
-    if world == 1 and (a.path == "dropin" or not a.no_dropin) and not bf16:
-        drop = dropin_run(rb, dev, a, world, rank, n_local)
+    if world == 1 and (a.path == "dropin" or not a.no_dropin):
+        drop = dropin_run(rb, dev, a, world, rank, n_local, a.precision)
+    sub = None
+    if not a.no_other_precision and a.path == "engine":
+        sub, tr2, nets2 = engine_run(a, dev, rb, world, rank, n_local, other, barrier, nccl)
+        runs[other] = (tr2, nets2)
+        if world == 1 and not a.no_dropin:
+            sub["dropin"] = dropin_run(rb, dev, a, world, rank, n_local, other)
+            sub["dropin_vs_engine"] = round(sub["dropin"]["value"] / sub["value"], 4)
 
-    peak_step = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
     main_res = drop if a.path == "dropin" else engine
     value = main_res["value"]
     out = {
@@ -374,29 +515,22 @@ def main():
                    "path": a.path},
         "rccl_ranks": world, "backend": ("nccl (RCCL)" if nccl else "gloo (rehearsal)") if world > 1 else None,
         "roofline": engine["roofline"] if engine else None,
-        "step_mfma_frac": round(value * FLOP_PER_RAY / world / 1e12 / peak_step, 4),
+        "step_mfma_frac": round(value * FLOP_PER_RAY / world / 1e12 /
+                                (BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS), 4),
         "final_loss": main_res["final_loss"],
     }
+    if engine and engine.get("dp"):
+        out["dp"] = engine["dp"]
     if a.path == "dropin" and engine:
         out["engine"] = {k: engine[k] for k in ("value", "ms_per_step")}
     elif drop:
         out["dropin"] = drop
-    if out.get("dropin") or out.get("engine"):
-        e, d = (engine, drop)
-        out["dropin_vs_engine"] = round(d["value"] / e["value"], 4)
-    if not a.no_psnr and rank == 0 and engine:
-        from nerf_amd.ray_rendering import render_image
-        tr.sync_to_modules()
-        coarse.eval()
-        fx, fy, cx, cy = scene.intrinsics
-        img, _, _ = render_image(coarse, H=scene.H, W=scene.W, fx=fx, fy=fy, cx=cx, cy=cy, c2w=scene.test_poses[0],
-                                 near=scene.near, far=scene.far, ray_samples=a.samples, n_importance=a.importance,
-                                 fine_model=fine.eval(), ndc=(scene.focal, 1.0) if scene.ndc else None)
-        from nerf_amd.losses import image_psnr
-        out["psnr_after_steps"] = round(image_psnr(img, scene.test_images[0], "linear"), 3)
-        out["psnr_note"] = ("held-out view after warmup+steps train steps (outside the timed region); "
-                            "convergence: tools/train_psnr.py, profiles/r01/psnr_*.jsonl (fp32 28.1 dB / bf16 "
-                            "28.1 dB after 3000 steps)")
+    if drop and engine:
+        out["dropin_vs_engine"] = round(drop["value"] / engine["value"], 4)
+    if sub:
+        out[other] = sub
+    if not a.no_psnr and rank == 0 and runs and world == 1:
+        out["psnr"] = psnr_run(a, rb, scene, runs, rank, world, n_local)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.samples, a.importance, a.cpu_batch, a.cpu_steps)
     elif rank == 0:
@@ -404,7 +538,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
-        barrier()  # the other ranks wait for rank 0's PSNR render / report before tearing down
+        barrier()  # the other ranks wait for rank 0's report before tearing down
         dist.destroy_process_group()
 
 

@@ -38,11 +38,13 @@ def color_space_transformer(pred_linear, gt_tensor, color_space: str):
     return pred.to(pred_linear.dtype), gt.to(pred_linear.dtype)
 
 
-def compute_mse_loss(P, model, data, params=None, active_module=None, reduction="mean"):
+def compute_mse_loss(P, model, data, params=None, active_module=None, reduction="mean", **render_kwargs):
+    """nerfs/losses.py:10-32; with P.n_importance > 0 the loss is MSE(fine) + MSE(coarse) (canonical NeRF).
+    ``render_kwargs`` pass through to render_rays (e.g. the parity tests' injected jitter u_strat / u_pdf)."""
     gt_rgb, rays = data["rgbs"], data["rays"]
     n_imp = int(getattr(P, "n_importance", 0) or 0)
     out = render_rays(model, rays, ray_samples=P.ray_samples, params=params, active_module=active_module,
-                      chunk=P.chunk_points, n_importance=n_imp, return_extras=True)
+                      chunk=P.chunk_points, n_importance=n_imp, return_extras=True, **render_kwargs)
     pred_rgb, extras = out[0], out[-1]
     cs = getattr(P, "color_space", "linear")
     a, b = color_space_transformer(pred_rgb, gt_rgb, cs)

@@ -216,7 +216,16 @@ def render_image(model, *, H: int, W: int, fx: float, fy: float, cx: float, cy: 
                  ndc: Optional[Tuple[float, float]] = None, rays_per_chunk: int = 1 << 15, use_amp: bool = False,
                  fine_model=None):
     """ray_rendering.py:577-627 — rays from the fused HIP kernel, rendered in ray chunks.
-    ``ndc=(focal, near_plane)`` converts rays to forward-facing NDC first (LLFF config)."""
+    ``ndc=(focal, near_plane)`` converts rays to forward-facing NDC first (LLFF config).  ``use_amp`` renders under
+    ``torch.autocast("cuda", torch.float16)`` as the reference does (:611): the MLP runs its bf16 kernels
+    (vanilla.amp_precision), compositing stays fp32."""
+    if use_amp:
+        with torch.autocast("cuda", dtype=torch.float16):
+            return render_image(model, H=H, W=W, fx=fx, fy=fy, cx=cx, cy=cy, c2w=c2w, scene_box=scene_box, near=near,
+                                far=far, params=params, active_module=active_module, ray_samples=ray_samples,
+                                n_importance=n_importance, chunk_points=chunk_points, bg_color_default=bg_color_default,
+                                center_pixels=center_pixels, ndc=ndc, rays_per_chunk=rays_per_chunk, use_amp=False,
+                                fine_model=fine_model)
     device = next(model.parameters()).device
     rays = rays_for_camera(H, W, fx, fy, cx, cy, c2w.to(device), near=near, far=far, scene_box=scene_box,
                            center_pixels=center_pixels)

@@ -8,7 +8,8 @@ but every stage is a HIP launch on one stream with no host synchronisation:
   pick_pixels+rays_gen(+gt gather) -> sample_stratified -> build_xd -> mlp_fwd(coarse)
   -> composite_fwd(+loss, dL/drgb) -> sample_pdf -> build_xd -> mlp_fwd(fine) -> composite_fwd(+loss)
   -> composite_bwd -> mlp_bwd(fine) -> composite_bwd -> mlp_bwd(coarse)
-  -> [RCCL all_reduce(SUM) of the flat gradient (+ loss) buffer, data parallel]
+  -> [RCCL all_reduce(SUM) of the flat gradient (+ loss) buffer, data parallel: the coarse net's bucket as soon as
+      its side-stream backward ends, the fine net's + loss after the fine backward]
   -> grad_sqnorm -> adam
 
 Both networks live in ONE flat fp32 buffer [coarse | fine] (kernel packed layout), so the data-parallel
@@ -148,9 +149,9 @@ class NeRFTrainer:
             self.timing = None
             return
         mk = lambda k: [torch.cuda.Event(enable_timing=True) for _ in range(k)]
-        sets = [{"fwd": mk(16), "bwd": mk(32)} for _ in range(n_steps)]
+        sets = [{"fwd": mk(16), "bwd": mk(32), "ar": mk(4)} for _ in range(n_steps)]
         for st in sets:
-            for e in st["fwd"] + st["bwd"]:
+            for e in st["fwd"] + st["bwd"] + st["ar"]:
                 e.record()  # materialise the event handles
         torch.cuda.synchronize()
         self.timing = {"pool": sets, "used": [], "M": None, "skip": int(skip)}
@@ -184,6 +185,8 @@ class NeRFTrainer:
                                                   color_space=self.color_space, inv_count=inv_count,
                                                   loss_sum=self.loss_buf)
         side_done = None
+        P = self.P
+        ev_box = [self._next_events() if NI > 0 else None]  # HIP events of this step (timed steps only)
 
         def coarse_bwd_on_side():
             main = torch.cuda.current_stream(self.device)
@@ -192,7 +195,11 @@ class NeRFTrainer:
             self._side.wait_event(fork)
             with torch.cuda.stream(self._side):
                 d_rs_c = K.composite_bwd(rs_c, t_c, bg, drgb_c, sigma_scale=self.sigma_scale)
-                K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=False, precision=self.precision, bf16_flags=self.bf16_flags)
+                K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=False, precision=self.precision,
+                          bf16_flags=self.bf16_flags)
+                # bucket 1 of the data-parallel exchange: the coarse net's gradient is final here, so its all-reduce
+                # starts now and runs beside the fine net's forward / backward (bucket 2 trails the backward)
+                self._exchange(self.gbuf[:P], ev_box[0], 0)
                 done = torch.cuda.Event()
                 done.record(self._side)
             return done
@@ -203,7 +210,7 @@ class NeRFTrainer:
             t_f = K.sample_pdf(t_c, w_c, NI, u=u_pdf, det=False, seed=seed ^ 0x5EED)
             xd_f = K.build_xd(rays, t_f)
             ws_f = self._workspace("f", N * (S + NI))
-            ev = self._next_events()
+            ev = ev_box[0]
             rs_f = K.mlp_fwd(self.w(fine_k), xd_f, ws_f, True, events=ev["fwd"] if ev else None,
                              precision=self.precision, bf16_flags=self.bf16_flags)
             if self.overlap and self.overlap_with == "bwd":
@@ -218,11 +225,12 @@ class NeRFTrainer:
                 self.timing["M"] = N * (S + NI)
         if side_done is not None:
             torch.cuda.current_stream(self.device).wait_event(side_done)
+            self._exchange(self.gbuf[P:], ev_box[0], 1)   # bucket 2: fine gradient + loss
         else:
             d_rs_c = K.composite_bwd(rs_c, t_c, bg, drgb_c, sigma_scale=self.sigma_scale)
             K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=(fine_k == 0 and NI > 0),
                       precision=self.precision, bf16_flags=self.bf16_flags)
-        allreduce_flat(self.gbuf, self.world_size)
+            self._exchange(self.gbuf, ev_box[0], 1)
         self.step_count += 1
         if self.grad_clip is not None and self.grad_clip > 0:
             K.grad_sqnorm(self.grads, self.partials)
@@ -232,6 +240,20 @@ class NeRFTrainer:
         K.adam(self.params, self.grads, self.m, self.v, self.seg_off, self.seg_lr, self.step_count, self.betas,
                self.eps, self.wd, parts, mx)
         return self.loss_buf
+
+    def _exchange(self, buf, ev, bucket):
+        """SUM all-reduce of one bucket of the flat [grad_coarse | grad_fine | loss] buffer over RCCL, on the current
+        stream; with timing events, events["ar"][2 bucket], [2 bucket + 1] bracket it (includes the wait for the
+        slowest rank)."""
+        if self.world_size <= 1:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        if ev:
+            ev["ar"][2 * bucket].record(cur)
+        allreduce_flat(buf, self.world_size)
+        if ev:
+            ev["ar"][2 * bucket + 1].record(cur)
+            ev["ar_used"] = ev.get("ar_used", 0) | (1 << bucket)
 
     def collect_timing(self):
         """Per-launch durations (ms) of the fine net's trunk GEMMs over every timed step:
@@ -243,6 +265,9 @@ class NeRFTrainer:
             out["wgrad"].append([ev["bwd"][4 * i].elapsed_time(ev["bwd"][4 * i + 1]) for i in range(8)])
             out["dgrad"].append([ev["bwd"][4 * i + 2].elapsed_time(ev["bwd"][4 * i + 3]) for i in range(1, 8)])
             out["dgrad_head"].append(ev["bwd"][2].elapsed_time(ev["bwd"][3]))  # head -> trunk.7 input gradient
+            used = ev.get("ar_used", 0)
+            out.setdefault("allreduce", []).append([ev["ar"][2 * b].elapsed_time(ev["ar"][2 * b + 1])
+                                                    for b in range(2) if used >> b & 1])
         return out
 
     @torch.no_grad()

@@ -105,37 +105,52 @@ class PackedLayout:
         return out
 
 
+def amp_precision() -> str:
+    """The MLP precision the caller's autocast region asks for: "bf16" inside ``torch.autocast("cuda")`` with a
+    16-bit dtype (the reference trains under ``torch.cuda.amp.autocast(dtype=torch.float16)`` + GradScaler,
+    pipelines/online_stage/runtime_adapt.py:290-310, configs/train.json "use_amp": true), else "fp32".  Both fp16
+    and bf16 autocast run the bf16 MFMA kernels (fp32 accumulation, fp32 weight gradients): bf16 keeps fp32's
+    exponent range, so a scaled loss never overflows inside the MLP and the GradScaler sees no inf from it.
+    Compositing, loss and sampling stay fp32 either way ("bf16 MLP with fp32 compositing", configs[2])."""
+    if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") in (torch.float16, torch.bfloat16):
+        return "bf16"
+    return "fp32"
+
+
 class VanillaMLPFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x_d, w_packed):
+    def forward(ctx, x_d, w_packed, precision="fp32"):
         x_d = x_d.contiguous().float()
         M = x_d.shape[0]
-        ws = K.mlp_workspace(M, True, x_d.device)
-        out = K.mlp_fwd(w_packed, x_d, ws, training=True)
+        ws = K.mlp_workspace(M, True, x_d.device, precision)
+        out = K.mlp_fwd(w_packed, x_d, ws, training=True, precision=precision)
         ctx.save_for_backward(w_packed)
         ctx.ws = ws
         ctx.M = M
+        ctx.precision = precision
         return out
 
     @staticmethod
     @once_differentiable
     def backward(ctx, g):
         (w_packed,) = ctx.saved_tensors
-        g = g.contiguous()
-        d_w = K.mlp_bwd(w_packed, ctx.M, g, ctx.ws)
+        g = g.contiguous().float()
+        d_w = K.mlp_bwd(w_packed, ctx.M, g, ctx.ws, precision=ctx.precision)
         ctx.ws = None
         if ctx.needs_input_grad[0]:
             raise NotImplementedError("gradient w.r.t. sample positions x_d is not supported by the HIP MLP")
-        return None, d_w
+        return None, d_w, None
 
 
-def mlp_forward(x_d, w_packed):
-    """x_d (M,6) -> (M,4) with a packed weight tensor; inference path when no grad is needed."""
+def mlp_forward(x_d, w_packed, precision: Optional[str] = None):
+    """x_d (M,6) -> (M,4) with a packed weight tensor; inference path when no grad is needed.  precision None
+    follows the caller's autocast region (amp_precision)."""
+    precision = amp_precision() if precision is None else precision
     if torch.is_grad_enabled() and w_packed.requires_grad:
-        return VanillaMLPFn.apply(x_d, w_packed)
+        return VanillaMLPFn.apply(x_d, w_packed, precision)
     x_d = x_d.contiguous().float()
-    ws = K.mlp_workspace(x_d.shape[0], False, x_d.device)
-    return K.mlp_fwd(w_packed.detach(), x_d, ws, training=False)
+    ws = K.mlp_workspace(x_d.shape[0], False, x_d.device, precision)
+    return K.mlp_fwd(w_packed.detach(), x_d, ws, training=False, precision=precision)
 
 
 class _Block(nn.Module):

@@ -4,8 +4,8 @@
   ``scene.ndc`` scene: pixel pick -> rays -> NDC on the device) against ``oracle.get_rays`` + ``oracle.ndc_rays``, and
   two engine train steps against ``OracleTrainer`` on identical jitter (loss to 1e-5, clipped gradients to 1e-4 of
   their scale);
-* C5 — the 8-scene sweep driver (``tools/sweep_scenes.py``) on two small scenes: finite, decreasing loss and a
-  per-scene PSNR above the untrained one;
+* C5 — the 8-scene sweep driver (``tools/sweep_scenes.py``) at its 4096-ray batch on 8 scenes (200x200 views):
+  finite, decreasing loss and a per-scene PSNR above the untrained one, aggregate rays/s;
 * the SURVEY §8(d) matched-trajectory check: 50 engine steps against 50 oracle steps from the same seeds on identical
   jitter (relative loss difference per step)."""
 import math
@@ -79,20 +79,26 @@ def test_c4_llff_ndc_engine_step_vs_oracle(K):
                     _close(v, ref, 1e-4 * max(1.0, ref.abs().max().item()), what=f"C4 net{k} grad {nme}")
 
 
-def test_c5_sweep_driver_two_scenes(K):
+def test_c5_sweep_eight_scenes_4096_ray_batches(K):
+    """configs[4] at its configured batch: tools/sweep_scenes.py's train_scene on all 8 seeded scenes with 4096-ray
+    batches, 64 + 128, two 8x256 nets, 150 bf16 steps each on 200x200 views (the sweep's precision in
+    profiles/r02/sweep/): per scene finite and decreasing loss and a held-out PSNR above the untrained one; the
+    summary reports mean PSNR and the aggregate rays/s (one GPU: the scenes run back to back)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import sweep_scenes
-    recs = [sweep_scenes.train_scene(sid, steps=150, batch=1024, train_views=8, test_views=1, precision="fp32",
-                                     lr=2e-3, dev=torch.device(DEV), H=100, W=100, initial_psnr=True)
-            for sid in (0, 5)]
+    recs = [sweep_scenes.train_scene(sid, steps=150, batch=4096, train_views=20, test_views=1, precision="bf16",
+                                     lr=2e-3, dev=torch.device(DEV), H=200, W=200, initial_psnr=True)
+            for sid in range(8)]
     for r in recs:
         ls = r["losses"]
         assert all(math.isfinite(x) for x in ls), r["scene_seed"]
         first, last = sum(ls[:10]) / 10, sum(ls[-10:]) / 10
         assert last < 0.5 * first, (r["scene_seed"], first, last)
-        assert math.isfinite(r["psnr"]) and r["psnr"] > r["psnr_init"] + 3.0, r
+        assert math.isfinite(r["psnr"]) and r["psnr"] > r["psnr_init"] + 3.0, {k: r[k] for k in r if k != "losses"}
         assert r["rays_per_s"] > 0
-    print({r["scene_seed"]: (r["psnr_init"], r["psnr"]) for r in recs})
+    summ = sweep_scenes.summarize(recs, 4096, "bf16")
+    assert summ["scenes"] == 8 and summ["aggregate_rays_per_s"] > 0
+    print({r["scene_seed"]: (r["psnr_init"], r["psnr"]) for r in recs}, summ)
 
 
 def test_engine_matches_oracle_50_step_trajectory(K):

@@ -1,0 +1,144 @@
+"""The drop-in surface under the reference's own training-loop body (-m gpu).
+
+The north star's contract is that this repo's ``render_rays`` + expert "drop into the existing training loop":
+an/pipelines/online_stage/runtime_adapt.py:286-310 —
+
+    optimizer.zero_grad()
+    with torch.cuda.amp.autocast(enabled=use_amp, dtype=torch.float16):
+        loss = compute_mse_loss(P, model=base, data={"rays": rays, "rgbs": rgbs}, ...)
+    scaler.scale(loss).backward()
+    scaler.unscale_(optimizer); torch.nn.utils.clip_grad_norm_(base.parameters(), grad_clip)
+    scaler.step(optimizer); scaler.update()
+
+* fp32 (use_amp False): the hierarchical step — ``HierarchicalNeRF`` (coarse + fine VanillaNeRF) through
+  ``compute_mse_loss`` (MSE(fine) + MSE(coarse), nerf_amd/losses.py) with the jitter injected, autograd backward,
+  ``clip_grad_norm_(1.0)`` and ``torch.optim.Adam`` — against ``OracleTrainer`` (the CPU restatement pinned to the
+  reference's golden train step): loss to 1e-5, both nets' clipped gradients to 1e-4 of their scale, post-Adam
+  parameters within the update difference the two measured gradients imply (test_gpu_parity._adam_step1_close);
+  then two more steps' losses.
+* AMP (configs/train.json "use_amp": true): inside ``autocast(fp16)`` the expert runs the bf16 MLP kernels
+  (bitwise ``nerf_mlp_fwd_bf16``), compositing stays fp32; the loop body as written with ``GradScaler`` trains,
+  its loss tracks the fp32 loop's from the same seed, and the scaler never finds an inf (its scale stays put)."""
+import types
+
+import pytest
+import torch
+
+from golden_io import load
+from oracle import nerf_oracle as O
+from test_gpu_parity import _adam_step1_close, _close
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def K():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from nerf_amd import kernels
+    return kernels
+
+
+def _model(pc, pf):
+    from nerf_amd.vanilla import HierarchicalNeRF, VanillaNeRF
+    return HierarchicalNeRF(VanillaNeRF().load_reference_state(pc), VanillaNeRF().load_reference_state(pf)).to(DEV)
+
+
+def _adam(model, lr_sigma, lr_color, **kw):
+    grp = model.get_param_groups()
+    return torch.optim.Adam([{"params": grp["sigma"]["params"], "lr": lr_sigma},
+                             {"params": grp["color"]["params"], "lr": lr_color}], **kw)
+
+
+def test_dropin_hierarchical_step_vs_oracle(K):
+    from nerf_amd.losses import compute_mse_loss
+    pc, pf = O.init_vanilla_params(1), O.init_vanilla_params(2)
+    model = _model(pc, pf).train()
+    opt = _adam(model, 2e-3, 1e-3)
+    ot = O.OracleTrainer(pc, pf, lr_sigma=2e-3, lr_color=1e-3)
+    P = types.SimpleNamespace(ray_samples=64, n_importance=128, chunk_points=1 << 22, color_space="linear")
+    rays = load("render")["rays"]
+    g = torch.Generator().manual_seed(17)
+    gt = torch.rand(rays.shape[0], 3, generator=g)
+    nets = {0: model.coarse, 1: model.fine}
+    for step in range(3):
+        us, up = torch.rand(rays.shape[0], 64, generator=g), torch.rand(rays.shape[0], 128, generator=g)
+        opt.zero_grad()
+        loss = compute_mse_loss(P, model, {"rays": rays.to(DEV), "rgbs": gt.to(DEV)}, u_strat=us.to(DEV),
+                                u_pdf=up.to(DEV))
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        lref = ot.step(rays, gt, 64, n_importance=128, training=True, u_strat=us, u_pdf=up)
+        assert abs(loss.item() - lref) < 1e-5 + 1e-4 * lref, (step, loss.item(), lref)
+        if step == 0:
+            for k, net in nets.items():
+                for n, p in net.named_parameters():
+                    ref = ot.nets[k][n]
+                    _close(p.grad, ref.grad, rel_scale=True, what=f"net{k} clipped grad {n}")
+                    lr = 1e-3 if n.startswith("color_mlp") else 2e-3
+                    _adam_step1_close(p, ref, p.grad, ref.grad, lr, what=f"net{k} post-Adam {n}")
+
+
+def test_autocast_dispatches_bf16_kernels(K):
+    """Inside autocast(fp16 or bf16) VanillaNeRF.forward is bitwise the bf16 kernel; outside it, the fp32 one."""
+    from nerf_amd.vanilla import VanillaNeRF, amp_precision
+    net = VanillaNeRF().load_reference_state(O.init_vanilla_params(3)).to(DEV)
+    g = torch.Generator().manual_seed(3)
+    x = torch.cat([torch.rand(3000, 3, generator=g) * 3 - 1.5,
+                   torch.nn.functional.normalize(torch.randn(3000, 3, generator=g), dim=-1)], -1).to(DEV)
+    w = net.packed().detach()
+    ref = {p: K.mlp_fwd(w, x, K.mlp_workspace(3000, False, DEV, p), False, precision=p) for p in ("fp32", "bf16")}
+    assert amp_precision() == "fp32"
+    with torch.no_grad():
+        assert torch.equal(net(x), ref["fp32"])
+        for dt in (torch.float16, torch.bfloat16):
+            with torch.autocast("cuda", dtype=dt):
+                assert amp_precision() == "bf16"
+                out = net(x)
+            assert out.dtype == torch.float32 and torch.equal(out, ref["bf16"]), dt
+    with torch.autocast("cuda", dtype=torch.float16):   # training forward (autograd Function) as well
+        out = net(x)
+    assert out.requires_grad and torch.equal(out.detach(), ref["bf16"])
+
+
+def test_reference_amp_loop_body_with_gradscaler(K):
+    """runtime_adapt.py:290-310 with use_amp=True, as written, on the drop-in surface: 40 steps of 1024-ray batches
+    from a synthetic 100x100 scene, 64 + 128.  The AMP loop learns, its loss stays within 15 % of the fp32 loop's
+    (same seed, same batches, same jitter draws), and GradScaler never skips a step (no inf / nan gradient: its
+    scale is still the initial 2^16, which it halves on every inf)."""
+    from nerf_amd.losses import compute_mse_loss
+    from nerf_amd.scene import make_blender_scene
+    from nerf_amd.trainer import RayBatcher
+    scene = make_blender_scene(n_train=4, n_test=1, H=100, W=100, seed=1, device=DEV)
+    rb = RayBatcher(scene, DEV)
+    P = types.SimpleNamespace(ray_samples=64, n_importance=128, chunk_points=1 << 22, color_space="linear")
+    pc, pf = O.init_vanilla_params(1), O.init_vanilla_params(2)
+    curves = {}
+    for use_amp in (False, True):
+        torch.manual_seed(0)
+        base = _model(pc, pf).train()
+        optimizer = _adam(base, 2e-3, 2e-3)
+        scaler = torch.amp.GradScaler("cuda", enabled=use_amp)
+        ls = []
+        for step in range(40):
+            rays, rgbs = rb.batch(1024, seed=step)
+            optimizer.zero_grad()
+            with torch.cuda.amp.autocast(enabled=use_amp, dtype=torch.float16):
+                loss = compute_mse_loss(P, model=base, data={"rays": rays, "rgbs": rgbs}, params=None,
+                                        active_module=None, reduction="mean")
+            scaler.scale(loss).backward()
+            scaler.unscale_(optimizer)
+            torch.nn.utils.clip_grad_norm_(base.parameters(), 1.0)
+            scaler.step(optimizer)
+            scaler.update()
+            ls.append(float(loss.detach()))
+        if use_amp:
+            assert scaler.get_scale() == 65536.0, f"GradScaler found an inf/nan (scale {scaler.get_scale()})"
+        curves[use_amp] = torch.tensor(ls)
+    a, b = curves[True], curves[False]
+    assert torch.isfinite(a).all()
+    assert a[-10:].mean() < 0.8 * a[:5].mean(), a   # it learns
+    assert (a[-10:].mean() - b[-10:].mean()).abs() <= 0.15 * b[-10:].mean(), (a[-10:].mean(), b[-10:].mean())
+    assert not torch.equal(a, b)  # the AMP loop did run the bf16 kernels

@@ -75,6 +75,21 @@ def train_scene(sid, *, steps, batch, train_views, test_views, precision, lr, de
     return rec
 
 
+def summarize(results, batch, precision, world=1):
+    """configs[4] summary: mean PSNR over the scenes, aggregate rays/s (every GPU trains its scenes concurrently; a
+    GPU's rate = its rays / its training time; summed over GPUs) and the aggregate MFMA-roofline fraction."""
+    per_gpu = {}
+    for r in results:
+        per_gpu.setdefault(r.get("rank", 0), []).append(r)
+    agg = sum(sum(x["steps"] for x in rs) * batch / sum(x["train_s"] for x in rs) for rs in per_gpu.values())
+    return {"config": "configs[4]: 8-scene synthetic sweep, 4096-ray batches, 64+128, 2 x (8x256 MLP)",
+            "precision": precision, "n_gpus": world, "scenes": len(results), "batch": batch,
+            "mean_psnr": round(sum(r["psnr"] for r in results) / len(results), 3),
+            "aggregate_rays_per_s": round(agg, 1),
+            "aggregate_mfma_frac": round(agg * FLOP_PER_RAY / (world * PEAK[precision]), 4),
+            "data": "synthetic (seeded analytic scenes 0..7; nerf_synthetic not in the image)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scenes", type=int, default=8)
@@ -83,6 +98,7 @@ def main():
     ap.add_argument("--lr", type=float, default=2e-3)
     ap.add_argument("--train-views", type=int, default=100)
     ap.add_argument("--test-views", type=int, default=2)
+    ap.add_argument("--size", type=int, default=800, help="image height = width")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -95,7 +111,7 @@ def main():
     results = []
     for sid in range(rank, a.scenes, world):
         rec = train_scene(sid, steps=a.steps, batch=a.batch, train_views=a.train_views, test_views=a.test_views,
-                          precision=a.precision, lr=a.lr, dev=dev)
+                          precision=a.precision, lr=a.lr, dev=dev, H=a.size, W=a.size)
         rec["rank"] = rank
         rec.pop("losses", None)
         print(json.dumps(rec), flush=True)
@@ -106,18 +122,7 @@ def main():
         dist.all_gather_object(allr, results)
         results = [r for rr in allr for r in rr]
     if rank == 0:
-        per_gpu = {}
-        for r in results:
-            per_gpu.setdefault(r["rank"], []).append(r)
-        # aggregate throughput: every GPU trains concurrently; each GPU's rate = its rays / its training time
-        agg = sum(sum(x["steps"] for x in rs) * a.batch / sum(x["train_s"] for x in rs) for rs in per_gpu.values())
-        summary = {"config": "configs[4]: 8-scene synthetic sweep, 4096-ray batches, 64+128, 2 x (8x256 MLP)",
-                   "precision": a.precision, "n_gpus": world, "scenes": len(results),
-                   "mean_psnr": round(sum(r["psnr"] for r in results) / len(results), 3),
-                   "aggregate_rays_per_s": round(agg, 1),
-                   "aggregate_mfma_frac": round(agg * FLOP_PER_RAY / (world * PEAK[a.precision]), 4),
-                   "data": "synthetic (seeded analytic scenes 0..7; nerf_synthetic not in the image)"}
-        print(json.dumps(summary), flush=True)
+        print(json.dumps(summarize(results, a.batch, a.precision, world)), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
