@@ -62,6 +62,15 @@ FLOP_PER_RAY = 769327104       # 6*MAC*(64 coarse + 192 fine evaluations), SURVE
 K256 = [1, 2, 3, 5, 6, 7]      # trunk layers with a 256x256 weight (trunk.0: K=63, trunk.4: K=319)
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """A heartbeat on stderr (stdout carries only the one JSON line): the long legs (PSNR training, the CPU baseline)
+    would otherwise print nothing for minutes."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -160,6 +169,7 @@ def _oracle_step_rate(S, NI, n, steps, threads, budget_s=None):
         t0 = time.perf_counter()
         tr.step(rays, gt, S, n_importance=NI)
         times.append(time.perf_counter() - t0)
+        progress(f"cpu baseline: {n} rays x {threads} threads: step {len(times)}/{steps} {times[-1]:.2f} s")
         if budget_s is not None and sum(times) > budget_s:
             break
     return statistics.median(times), times
@@ -170,7 +180,7 @@ def cpu_baseline(S, NI, n, steps):
     batch through a Blender-style camera: one warm-up step on 128 rays, then the median of `steps` steps.
     Threads = the host CPU share this process is given (OMP_NUM_THREADS on the GPU box: 16 of the machine's CPUs).
     BASELINE.md §3 asks for torch.set_num_threads(os.cpu_count()): that leg runs beside it as `all_cores` on a
-    smaller sample (1024 rays, median of <= 3 steps, ~30 s budget) — on the GPU box os.cpu_count() reports the whole
+    smaller sample (512 rays, median of <= 3 steps, ~30 s budget) — on the GPU box os.cpu_count() reports the whole
     machine, more threads than this process's share (affinity / cgroup quota are reported with it)."""
     threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     med, times = _oracle_step_rate(S, NI, n, steps, threads)
@@ -179,8 +189,18 @@ def cpu_baseline(S, NI, n, steps):
                      f"clip, Adam): {med:.2f} s/step (steps {', '.join(f'{t:.2f}' for t in times)} s)",
            "cpu_model": _cpu_model(), "torch_threads": torch.get_num_threads(), **_cpu_share()}
     allc = os.cpu_count() or 1
-    if allc != threads:
-        n2 = min(n, 1024)
+    quota = rec.get("cgroup_cpu_quota")
+    if allc != threads and quota is not None and quota < allc:
+        # measured on the GPU box (round 3): 256 threads on a 16-CPU cgroup quota ran 512 rays in 68.7 s/step
+        # (7.45 rays/s) — oversubscribing the share 16x measures the scheduler, not the reference path
+        rec["all_cores"] = {"value": None, "cores": allc,
+                            "skipped": f"this process's cgroup CPU quota is {quota} CPUs of os.cpu_count()={allc}: "
+                                       f"torch.set_num_threads({allc}) would oversubscribe the share "
+                                       f"{allc / max(quota, 1e-9):.0f}x (measured once, round 3: 7.45 rays/s on 512 "
+                                       "rays, 68.7 s/step); the baseline above uses the whole quota"}
+    elif allc != threads:
+        n2 = min(n, 512)
+        progress(f"cpu baseline: all-cores leg, {n2} rays at {allc} threads")
         med2, times2 = _oracle_step_rate(S, NI, n2, 3, allc, budget_s=30.0)
         rec["all_cores"] = {"value": round(n2 / med2, 2), "unit": "rays/s", "cores": allc,
                             "torch_threads": torch.get_num_threads(),
@@ -414,9 +434,13 @@ def psnr_run(a, rb, scene, runs, rank, world, n_local):
         done = tr.step_count
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        progress(f"psnr: training the {prec} engine from step {done} to {a.psnr_steps}")
         for s in range(done, a.psnr_steps):
             rays, gt = _batch(rb, a, s, rank, world, n_local)
             tr.step(rays, gt, seed=s * world + rank)
+            if (s + 1) % 250 == 0:
+                torch.cuda.synchronize()
+                progress(f"psnr: {prec} step {s + 1}/{a.psnr_steps}")
         torch.cuda.synchronize()
         train_s = time.perf_counter() - t0
         tr.sync_to_modules()
@@ -483,6 +507,7 @@ def main():
 
     runs = {}
     engine = None
+    progress(f"rank {rank}/{world}: scene ready")
     if a.path == "engine" or world == 1:
         engine, tr, nets = engine_run(a, dev, rb, world, rank, n_local, a.precision, barrier, nccl)
         runs[a.precision] = (tr, nets)
@@ -529,6 +554,7 @@ def main():
         out["dropin_vs_engine"] = round(drop["value"] / engine["value"], 4)
     if sub:
         out[other] = sub
+    progress("timed legs done")
     if not a.no_psnr and rank == 0 and runs and world == 1:
         out["psnr"] = psnr_run(a, rb, scene, runs, rank, world, n_local)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -215,8 +215,12 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, char* lds, int s
                      "+v"(gf[cb][3])::"memory");
       }
       SCHED_FENCE();
+#ifdef NERF_EXP_BWD_NOWG
+      asm volatile("" ::"v"(gf[cb][0]), "v"(gf[cb][1]), "v"(gf[cb][2]), "v"(gf[cb][3]), "v"(xf[cb]));
+#else
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf[cb][j], xf[cb], acc[j], 0, 0, 0);
+#endif
       SCHED_FENCE();
     });
     // ---- input gradient: dX^T[32 kb..][rows 32 mh..] over n in 16 k-steps
@@ -241,7 +245,11 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, char* lds, int s
         asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(wf), "+v"(g)::"memory");
       }
       SCHED_FENCE();
+#ifdef NERF_EXP_BWD_NODG
+      asm volatile("" ::"v"(wf), "v"(g));
+#else
       dacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, g, dacc, 0, 0, 0);
+#endif
       SCHED_FENCE();
     });
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xm[0]), "+v"(xm[1])::"memory");
@@ -261,7 +269,9 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, char* lds, int s
       // this lane now holds columns 16 pr + 8 lh .. + 7 of the block
       const uint4 xv = __builtin_bit_cast(uint4, xm[pr]);
       const uint4 o = make_uint4(relu_mask2(x.x, xv.x), relu_mask2(x.y, xv.y), relu_mask2(y.x, xv.z), relu_mask2(y.y, xv.w));
-#ifdef NERF_EXP_BWD_NT
+#if defined(NERF_EXP_BWD_NOSTORE)
+      asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
+#elif defined(NERF_EXP_BWD_NT)
       __builtin_nontemporal_store(io_u32x4{o.x, o.y, o.z, o.w}, reinterpret_cast<io_u32x4*>(Dt + 16 * pr));
 #else
       *reinterpret_cast<uint4*>(Dt + 16 * pr) = o;
@@ -351,10 +361,12 @@ __device__ __forceinline__ void bias_acc(const IoSet& R, float (&bs)[8]) {
 __device__ __forceinline__ void io_step(IoSet& R, const LayerArgs& A, char* lds, int h, int j, int t, int nT,
                                         int64_t r0, int lane, float (&bs)[8]) {
   raw_barrier();  // T_t: tile t in stage t % 2 is complete; every wave is done with tile t - 1
+#ifndef NERF_EXP_BWD_NOIO
   if (h == 0 && t + 1 < nT) bias_acc(R, bs);
   io_store(R, lds + ((t + 1) % NSTG) * STB, j, lane);
   const int tl = t + 3 < nT ? t + 3 : nT - 1;
   io_load(R, A, r0 + (int64_t)tl * TR, h, j, lane);
+#endif
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile t + 1's LDS writes are done before T_{t+1}
 }
 

@@ -19,6 +19,29 @@ pytestmark = pytest.mark.gpu
 N, S, NI = 256, 64, 128
 
 
+def _by_value(x):
+    """Results cross the queue BY VALUE (numpy): a torch CPU tensor is sent as a shared-memory file descriptor that the
+    parent can only fetch while the worker still lives — a worker that exits first makes the parent's get() fail."""
+    if torch.is_tensor(x):
+        return x.numpy()
+    if isinstance(x, dict):
+        return {k: _by_value(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_by_value(v) for v in x)
+    return x
+
+
+def _to_torch(x):
+    import numpy as np
+    if isinstance(x, np.ndarray):
+        return torch.from_numpy(x)
+    if isinstance(x, dict):
+        return {k: _to_torch(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_torch(v) for v in x)
+    return x
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -67,7 +90,7 @@ def _worker(rank, world, port, q):
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        q.put((rank, _run(world, rank, dev)))
+        q.put((rank, _by_value(_run(world, rank, dev))))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # report instead of hanging the parent on q.get
@@ -84,7 +107,7 @@ def test_trainer_world2_equals_full_batch():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=100) for _ in range(world))
+    res = {r: _to_torch(v) for r, v in (q.get(timeout=100) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
     for r in range(world):
@@ -150,7 +173,7 @@ def _adam_worker(rank, world, port, q, shard):
     try:
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        q.put((rank, _adam_run(world, rank, shard)))
+        q.put((rank, _by_value(_adam_run(world, rank, shard))))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:
@@ -170,7 +193,7 @@ def test_flat_adam_world2(shard):
     procs = [ctx.Process(target=_adam_worker, args=(r, world, port, q, shard)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=100) for _ in range(world))
+    res = {r: _to_torch(v) for r, v in (q.get(timeout=100) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
     for r in range(world):
