@@ -13,13 +13,11 @@ the rank-strided slice of the same global draw (an/scripts/create_clusters.py:79
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
   roofline      — the dominant kernel class of the fine net's trunk GEMMs: the class (fwd / dgrad / wgrad)
-                  with the largest mean launch time among the classes whose launches run alone on the
-                  device (with the default two-stream step the fine forward runs beside the coarse
-                  backward, so its wall durations are not per-kernel times and it is not eligible;
-                  --no-overlap makes it eligible).  Durations are HIP events the library records on the
-                  launch stream inside the last --timing-steps timed steps (default 3: a recorded event
-                  holds the stream ~10-25 us, so instrumenting all of them would slow the step being
-                  timed); achieved = algorithmic FLOP per launch / mean.
+                  with the largest mean launch time.  Durations are HIP events the library records on the
+                  launch stream in --timing-steps (default 3) extra steps AFTER the timed region, run with
+                  every launch alone on the device (the production step overlaps the coarse backward with
+                  the fine forward and the fine weight gradients with its input gradients on three streams,
+                  where a launch's wall time is shared); achieved = algorithmic FLOP per launch / mean.
                   With --precision bf16 the MLP is one fused forward launch plus one fused backward launch
                   per trunk layer (HBM-bound): the kernel with the largest total time per step is reported
                   against the HBM peak, with algorithmic bytes per launch (roofline_bf16).
@@ -94,6 +92,8 @@ def parse():
     ap.add_argument("--no-psnr", action="store_true",
                     help="skip the full-image PSNR record (training to --psnr-steps + held-out renders, N = 1 only)")
     ap.add_argument("--no-overlap", action="store_true", help="run the coarse-net backward on the main stream")
+    ap.add_argument("--no-split-wgrad", action="store_true",
+                    help="fp32: keep the fine net's weight-gradient GEMMs on the main stream (nerf_mlp_bwd)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (the product); gloo = rehearsal of N ranks sharing the visible GPUs")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
@@ -373,7 +373,7 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl):
     coarse, fine = VanillaNeRF().to(dev), VanillaNeRF().to(dev)
     tr = NeRFTrainer(coarse, fine, n_samples=a.samples, n_importance=a.importance, world_size=world, device=dev,
                      overlap=not a.no_overlap, precision=precision,
-                     bf16_flags=a.bf16_flags if precision == "bf16" else 0)
+                     bf16_flags=a.bf16_flags if precision == "bf16" else 0, split_wgrad=not a.no_split_wgrad)
 
     def one(step):
         rays, gt = _batch(rb, a, step, rank, world, n_local)
@@ -382,8 +382,6 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl):
     for s in range(a.warmup):
         loss = one(s)
     torch.cuda.synchronize()
-    n_ev = max(1, min(a.timing_steps, a.steps))
-    tr.enable_timing(n_ev, skip=a.steps - n_ev)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -392,6 +390,18 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl):
     barrier()
     torch.cuda.synchronize()
     el_local = time.perf_counter() - t0
+    # the roofline pass: timing_steps more steps (outside the timed region) with every launch alone on the device —
+    # the coarse backward back on the main stream, the fine weight gradients back in line — and HIP events around the
+    # fine net's trunk GEMMs, so each kernel class's mean launch time is its own (the production step runs them
+    # concurrently on three streams, where a launch's wall time is shared)
+    n_ev = max(1, a.timing_steps)
+    conc = (tr.overlap, tr.split_wgrad)
+    tr.overlap, tr.split_wgrad = False, False
+    tr.enable_timing(n_ev, skip=0)
+    for s in range(a.warmup + a.steps, a.warmup + a.steps + n_ev):
+        one(s)
+    torch.cuda.synchronize()
+    tr.overlap, tr.split_wgrad = conc
     tm = tr.collect_timing()
     el = el_local
     dp = None
@@ -414,7 +424,10 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl):
               "bytes_per_step": int(tr.gbuf.numel() * 4)}
     rec = {"value": round(n_local * world * a.steps / el, 1), "ms_per_step": round(el / a.steps * 1e3, 3),
            "final_loss": round(float(loss.item()), 6),
-           "roofline": dict(roofline(tm, precision == "bf16", tr.overlap, tr.bf16_flags), event_steps=n_ev)}
+           "roofline": dict(roofline(tm, precision == "bf16", False, tr.bf16_flags), event_steps=n_ev,
+                            event_pass="the timing_steps steps after the timed region, every launch alone (no "
+                                       "side-stream coarse backward, fine weight gradients in line)"),
+           "streams": {"coarse_bwd_beside_fine_fwd": tr.overlap, "fine_wgrad_stream": tr.split_wgrad}}
     peak = BF16_MFMA_PEAK_TFLOPS if precision == "bf16" else FP32_MFMA_PEAK_TFLOPS
     rec["step_mfma_frac"] = round(rec["value"] * FLOP_PER_RAY / world / 1e12 / peak, 4)
     if dp:

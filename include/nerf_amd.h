@@ -114,6 +114,18 @@ int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
 /* events: NULL, or 32 hipEvent_t: events[4i+0/1] bracket the weight-gradient GEMM of trunk.i,
  * events[4i+2/3] its input-gradient GEMM (i >= 1); events[2/3] bracket the head's input-gradient GEMM. */
 
+/* nerf_mlp_bwd with the weight-gradient GEMMs on a second stream: the input-gradient chain (colour branch, head and
+ * trunk dgrads) stays on `stream`; each weight-gradient GEMM runs on `wgrad_stream` behind an event recorded on
+ * `stream` after the launch that produced its input; `stream` waits for `wgrad_stream` before the final split reduce,
+ * so d_w is complete in `stream` order.  sync: 10 caller-created hipEvent_t (hipEventDisableTiming is fine).  The
+ * workspace keeps one input-gradient buffer per trunk layer: nerf_mlp_workspace_bytes_2s(M) bytes, filled by a
+ * training nerf_mlp_fwd (the forward part of it is nerf_mlp_workspace_bytes(M, 1)'s).  Same kernels, grids and split
+ * slabs as nerf_mlp_bwd: d_w is bitwise equal.  The events[4i+0/1] of a weight-gradient GEMM are recorded on
+ * wgrad_stream. */
+int64_t nerf_mlp_workspace_bytes_2s(int64_t M);
+int nerf_mlp_bwd_2s(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
+                    int64_t ws_bytes, hipEvent_t* events, hipStream_t stream, hipStream_t wgrad_stream, hipEvent_t* sync);
+
 /* bf16 variants (BASELINE configs[2]: "bf16 MLP with fp32 compositing"): the same network, packed fp32
  * parameters, inputs and outputs as nerf_mlp_fwd/bwd; the layer GEMMs run on bf16 MFMA with fp32
  * accumulation and the activations / activation gradients live in the workspace as bf16.  The weight

@@ -27,6 +27,7 @@ struct WS {
   uint32_t* MB[8];  // ReLU bitmasks of the trunk outputs [Mp][8] (colour layer 0 re-derives its mask from C0 > 0)
   // backward
   float *dA, *dB, *dO16, *WT, *partial, *partial2;
+  float* dZ[8];  // two-stream backward (training == 2): one input-gradient buffer per trunk layer (dZ_i of trunk.i)
   int S;
   int64_t rps;
   int64_t bytes;
@@ -57,8 +58,14 @@ WS carve(void* base, int64_t M, int training) {
   w.O3 = take(Mp * 32);
   if (training) {
     for (int i = 0; i < 8; ++i) w.MB[i] = reinterpret_cast<uint32_t*>(take(Mp * 8));
-    w.dA = take(Mp * 256);
-    w.dB = take(Mp * 256);
+    if (training == 2) {  // the weight-gradient stream reads dZ_i while the input-gradient chain runs ahead
+      for (int i = 0; i < 8; ++i) w.dZ[i] = take(Mp * 256);
+      w.dA = w.dZ[7];
+      w.dB = w.dZ[6];
+    } else {
+      w.dA = take(Mp * 256);
+      w.dB = take(Mp * 256);
+    }
     w.dO16 = take(Mp * 32);
     w.WT = take(WT_FLOATS);
     w.S = n_splits(Mp);
@@ -312,13 +319,33 @@ extern "C" int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* 
   return nerf_launch_status();
 }
 
-extern "C" int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
-                            int64_t ws_bytes, hipEvent_t* ev, hipStream_t st) {
+extern "C" int64_t nerf_mlp_workspace_bytes_2s(int64_t M) {
+  if (M < 0) return -1;
+  return carve(nullptr, M, 2).bytes + 256;
+}
+
+namespace {
+// The backward of nerf_mlp_fwd.  stw == nullptr: every launch on st (nerf_mlp_bwd).  Otherwise the weight-gradient
+// GEMMs go to stw, each behind an event recorded on st after the launch that produced its input (sync[1]: colour
+// branch + head dgrad -> head and trunk.7 wgrads; sync[8 - i], i < 7: trunk.(i+1) dgrad -> trunk.i wgrad), and st
+// waits for stw (sync[9]) before the split reduce; sync[0] is unused.  The same kernels, grids and slabs: bitwise the
+// one-stream result.
+int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
+                 int64_t ws_bytes, hipEvent_t* ev, hipStream_t st, hipStream_t stw, hipEvent_t* sync) {
   NERF_CHECK_ARG(w && d_rgb_sigma && d_w && ws && M >= 0);
+  NERF_CHECK_ARG(!stw || sync);
   if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(d_w) || !nerf_aligned16(d_rgb_sigma))
     return NERF_E_ALIGN;
-  const WS W = carve(ws, M, 1);
+  const bool two = stw != nullptr;
+  const WS W = carve(ws, M, two ? 2 : 1);
   if (ws_bytes < W.bytes) return NERF_E_WORKSPACE;
+  hipStream_t sw = two ? stw : st;  // the weight-gradient stream
+  auto handoff = [&](int k) -> int {  // sw waits for everything issued on st so far
+    if (!two) return hipSuccess;
+    hipError_t e = hipEventRecord(sync[k], st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stw, sync[k], 0);
+    return (int)e;
+  };
   const Layout& L = layout();
   if (M == 0) {
     if (!accumulate) (void)hipMemsetAsync(d_w, 0, L.total * sizeof(float), st);
@@ -354,23 +381,43 @@ extern "C" int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma,
   // dropping them changes no bit of dZ7
   TRY(nt<EPI_MASK>(W.dO16, 32, Wht, 32, nullptr, dcur, 256, W.MB[7], nullptr, Mp, 256, 16, st));
   if (ev) (void)hipEventRecord(ev[3], st);
-  TRY(wgrad(W.dO16, 32, W.Y[7], 256, 16, W, 32, 256, st));
+  TRY(handoff(1));  // dZ7 and dO16 are complete (the colour branch ran before the head dgrad on st)
+  TRY(wgrad(W.dO16, 32, W.Y[7], 256, 16, W, 32, 256, sw));
   // trunk
   for (int i = 7; i >= 0; --i) {
     const float* X = (i == 0) ? W.X3E + 256 : (i == 4 ? W.X3E : W.Y[i - 1]);
     const int ldx = (i == 0 || i == 4) ? 320 : ld_of(W, i - 1);
-    if (ev) (void)hipEventRecord(ev[4 * i], st);
-    TRY(wgrad(dcur, 256, X, ldx, 2 * i, W, 256, KPAD[i], st));
-    if (ev) (void)hipEventRecord(ev[4 * i + 1], st);
+    if (two && i < 7) TRY(handoff(8 - i));  // dZ_i, written by the trunk.(i+1) dgrad: sync[8 - i]
+    if (ev) (void)hipEventRecord(ev[4 * i], sw);
+    TRY(wgrad(dcur, 256, X, ldx, 2 * i, W, 256, KPAD[i], sw));
+    if (ev) (void)hipEventRecord(ev[4 * i + 1], sw);
     if (i > 0) {
+      if (two) dnext = W.dZ[i - 1];  // never the buffer a trailing weight gradient still reads
       if (ev) (void)hipEventRecord(ev[4 * i + 2], st);
       TRY(nt<EPI_MASK>(dcur, 256, WTi[i], 256, nullptr, dnext, 256, W.MB[i - 1], nullptr, Mp, 256, 256, st));
       if (ev) (void)hipEventRecord(ev[4 * i + 3], st);
       float* t = dcur; dcur = dnext; dnext = t;
     }
   }
+  if (two) {  // join: the split reduce reads every weight-gradient slab
+    TRY((int)hipEventRecord(sync[9], stw));
+    TRY((int)hipStreamWaitEvent(st, sync[9], 0));
+  }
   const int64_t n4 = L.total / 4;
   reduce_splits2_kernel<<<(unsigned)nerf_cdiv(n4, 256), 256, 0, st>>>(W.partial, L.total, W.S, d_w, n4, accumulate,
                                                                       W.partial2, L.total - L.off[18], L.off[18] / 4);
   return nerf_launch_status();
+}
+}  // namespace
+
+extern "C" int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
+                            int64_t ws_bytes, hipEvent_t* ev, hipStream_t st) {
+  return mlp_bwd_impl(w, M, d_rgb_sigma, d_w, accumulate, ws, ws_bytes, ev, st, nullptr, nullptr);
+}
+
+extern "C" int nerf_mlp_bwd_2s(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
+                               int64_t ws_bytes, hipEvent_t* ev, hipStream_t st, hipStream_t wgrad_stream,
+                               hipEvent_t* sync) {
+  NERF_CHECK_ARG(wgrad_stream && sync && wgrad_stream != st);
+  return mlp_bwd_impl(w, M, d_rgb_sigma, d_w, accumulate, ws, ws_bytes, ev, st, wgrad_stream, sync);
 }

@@ -370,9 +370,46 @@ __device__ __forceinline__ void io_step(IoSet& R, const LayerArgs& A, char* lds,
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile t + 1's LDS writes are done before T_{t+1}
 }
 
+#ifndef NERF_BWD_IOSETS
+#define NERF_BWD_IOSETS 2
+#endif
+// NERF_BWD_IOSETS == 3: three register sets, tile k in set k % 3; step t stores tile t + 1 and reloads its set with
+// tile t + 4 (three tiles in flight while tile t is computed)
+__device__ __forceinline__ void io_step3(IoSet& R, const LayerArgs& A, char* lds, int h, int j, int t, int nT,
+                                         int64_t r0, int lane, float (&bs)[8]) {
+  raw_barrier();
+  if (h == 0 && t + 1 < nT) bias_acc(R, bs);
+  io_store(R, lds + ((t + 1) % NSTG) * STB, j, lane);
+  const int tl = t + 4 < nT ? t + 4 : nT - 1;
+  io_load(R, A, r0 + (int64_t)tl * TR, h, j, lane);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 __device__ __forceinline__ void bwd_io(const LayerArgs& A, char* lds, int h, int j, int nT, int64_t r0, int lane,
                                        float (&bs)[8]) {
   if (nT == 0) return;
+#if NERF_BWD_IOSETS == 3
+  {
+    IoSet R0, R1, R2;
+    io_load(R0, A, r0, h, j, lane);
+    io_load(R1, A, r0 + (int64_t)(nT > 1 ? 1 : nT - 1) * TR, h, j, lane);
+    io_load(R2, A, r0 + (int64_t)(nT > 2 ? 2 : nT - 1) * TR, h, j, lane);
+    if (h == 0) bias_acc(R0, bs);
+    io_store(R0, lds, j, lane);
+    io_load(R0, A, r0 + (int64_t)(nT > 3 ? 3 : nT - 1) * TR, h, j, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    int t = 0;
+    for (; t + 2 < nT; t += 3) {
+      io_step3(R1, A, lds, h, j, t, nT, r0, lane, bs);
+      io_step3(R2, A, lds, h, j, t + 1, nT, r0, lane, bs);
+      io_step3(R0, A, lds, h, j, t + 2, nT, r0, lane, bs);
+    }
+    if (t < nT) io_step3(R1, A, lds, h, j, t, nT, r0, lane, bs);
+    if (t + 1 < nT) io_step3(R2, A, lds, h, j, t + 1, nT, r0, lane, bs);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+#endif
   IoSet R0, R1;
   io_load(R0, A, r0, h, j, lane);
   io_load(R1, A, r0 + (int64_t)(nT > 1 ? 1 : 0) * TR, h, j, lane);

@@ -231,7 +231,11 @@ __device__ __forceinline__ void stage(nerf_f32x16 (&acc)[4][2], Ring& ring, __am
     nerf_bf16x8 bf[NBW];
 #pragma unroll
     for (int b = 0; b < NBW; ++b) bf[b] = ring[p & 3][b];
+#ifdef NERF_EXP_FWD_NOWLOAD
+    if (false) {
+#else
     if (p + 4 < KS) {
+#endif
       const int kk = kpos<KIND>(p + 4, w);
 #pragma unroll
       for (int b = 0; b < NBW; ++b) ring[p & 3][b] = frag_ld(rs, wcur, nb0 + b, kk, KS, lane);
@@ -240,11 +244,18 @@ __device__ __forceinline__ void stage(nerf_f32x16 (&acc)[4][2], Ring& ring, __am
 #pragma unroll
       for (int b = 0; b < NBWN; ++b) ring[p & 3][b] = frag_ld(rs, wnext, nbn0 + b, kk, KSN, lane);
     }
+#ifdef NERF_EXP_FWD_NOMFMA
+#pragma unroll
+    for (int a = 0; a < TA; ++a) asm volatile("" ::"v"(af[a]));
+#pragma unroll
+    for (int b = 0; b < NBW; ++b) asm volatile("" ::"v"(bf[b]));
+#else
 #pragma unroll
     for (int a = 0; a < TA; ++a)
 #pragma unroll
       for (int b = 0; b < NBW; ++b)
         acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[b], af[a], acc[a][b], 0, 0, 0);
+#endif
     if (p + 1 < KS && p + 1 != BAR) {
 #pragma unroll
       for (int a = 0; a < TA; ++a) af[a] = an[a];
@@ -268,6 +279,13 @@ __device__ __forceinline__ uint32_t relu_pk(float x, float y) {
 template <int TA, int NB>
 __device__ __forceinline__ void relu_to_lds(const nerf_f32x16 (&acc)[4][2], nerf_bf16* dst, int pitch, int ar0, int c0,
                                             int li, int lh) {
+#ifdef NERF_EXP_FWD_NOEPI
+#pragma unroll
+  for (int a = 0; a < TA; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) asm volatile("" ::"v"(acc[a][b]));
+  return;
+#endif
 #pragma unroll
   for (int a = 0; a < TA; ++a) {
     const int r = ar0 + 32 * a + li;

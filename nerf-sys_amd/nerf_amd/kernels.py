@@ -132,6 +132,11 @@ def mlp_workspace_bytes(M, training, precision="fp32"):
     return lib().nerf_mlp_workspace_bytes(M, int(training))
 
 
+def mlp_workspace_bytes_2s(M):
+    """Workspace of the two-stream fp32 backward (nerf_mlp_bwd_2s): one input-gradient buffer per trunk layer."""
+    return lib().nerf_mlp_workspace_bytes_2s(M)
+
+
 def mlp_workspace(M, training, device, precision="fp32"):
     return torch.empty(mlp_workspace_bytes(M, training, precision), dtype=torch.uint8, device=device)
 
@@ -158,7 +163,10 @@ def mlp_fwd(w_packed, x_d, ws, training, out=None, events=None, precision="fp32"
     return out
 
 
-def mlp_bwd(w_packed, M, d_rgb_sigma, ws, d_w=None, accumulate=False, events=None, precision="fp32", bf16_flags=0):
+def mlp_bwd(w_packed, M, d_rgb_sigma, ws, d_w=None, accumulate=False, events=None, precision="fp32", bf16_flags=0,
+            wgrad_stream=None, sync=None):
+    """wgrad_stream (fp32 only): run the weight-gradient GEMMs there (nerf_mlp_bwd_2s; sync = 10 torch.cuda.Events,
+    ws from mlp_workspace_bytes_2s); d_w is complete in the current stream's order either way."""
     need(w_packed, "packed weights"), need(d_rgb_sigma, "d_rgb_sigma")
     _check_precision(precision)
     if d_w is None:
@@ -167,6 +175,13 @@ def mlp_bwd(w_packed, M, d_rgb_sigma, ws, d_w=None, accumulate=False, events=Non
     if precision == "bf16":
         check(lib().nerf_mlp_bwd_bf16(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws),
                                       ws.numel(), int(bf16_flags), _events_arg(events), stream()), "nerf_mlp_bwd_bf16")
+        return d_w
+    if wgrad_stream is not None:
+        if sync is None or len(sync) < 10:
+            raise ValueError("nerf_mlp_bwd_2s needs 10 sync events")
+        check(lib().nerf_mlp_bwd_2s(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws), ws.numel(),
+                                    _events_arg(events), stream(), ctypes.c_void_p(wgrad_stream.cuda_stream),
+                                    _events_arg(sync)), "nerf_mlp_bwd_2s")
         return d_w
     check(lib().nerf_mlp_bwd(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws), ws.numel(),
                              _events_arg(events), stream()), "nerf_mlp_bwd")

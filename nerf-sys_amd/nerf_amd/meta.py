@@ -88,7 +88,9 @@ def snapshot_params(model):
 def task_adapt(P, model, support, inner_lr, iterations, active_module: Optional[int] = None):
     """meta_core.py:14-68. Returns (fast OrderedDict, [detached loss per iteration]).
 
-    First order only (P.algo in {"fomaml", "reptile"}); AMP autocast is not applied (fp32 kernels)."""
+    First order only (P.algo in {"fomaml", "reptile"}).  Like the reference (:30-38) each inner forward runs under
+    autocast(fp16) when P.use_amp (default True) and a GPU is present: vanilla experts then take their bf16 MLP
+    kernels (vanilla.amp_precision); the Instant-NGP kernels stay fp32."""
     algo = str(getattr(P, "algo", "")).lower()
     if algo not in ("fomaml", "reptile"):
         raise NotImplementedError(f"task_adapt: algo {algo!r} needs second-order gradients (create_graph=True), "
@@ -96,8 +98,10 @@ def task_adapt(P, model, support, inner_lr, iterations, active_module: Optional[
     base = model.submodules[active_module] if active_module is not None else model
     fast = extract_module_params(base, copy=(algo == "reptile"))
     losses = []
+    amp_enabled = bool(getattr(P, "use_amp", True)) and torch.cuda.is_available()
     for _ in range(int(iterations)):
-        loss = compute_loss(P, model, support, params=fast, active_module=active_module)
+        with torch.autocast("cuda", dtype=torch.float16, enabled=amp_enabled):
+            loss = compute_loss(P, model, support, params=fast, active_module=active_module)
         grads = torch.autograd.grad(loss, tuple(fast.values()), create_graph=False, allow_unused=True)
         fast = sgd_update(fast, grads, inner_lr)
         losses.append(loss.detach())

@@ -60,7 +60,7 @@ class NeRFTrainer:
                  eps: float = 1e-8, weight_decay: float = 0.0, grad_clip: Optional[float] = 1.0,
                  color_space: str = "linear", bg: str = "white", sigma_scale: float = 1.0,
                  world_size: int = 1, device="cuda", overlap: bool = True, precision: str = "fp32",
-                 overlap_with: str = "fwd", bf16_flags: int = 0):
+                 overlap_with: str = "fwd", bf16_flags: int = 0, split_wgrad: bool = True):
         L = PackedLayout.get()
         self.L = L
         self.P = L.total
@@ -115,6 +115,14 @@ class NeRFTrainer:
             raise ValueError("overlap_with must be 'fwd' or 'bwd'")
         self.overlap_with = overlap_with
         self._side = torch.cuda.Stream(device=self.device) if self.overlap else None
+        # fp32: the fine net's weight-gradient GEMMs on their own stream beside its input-gradient chain
+        # (nerf_mlp_bwd_2s: bitwise the one-stream gradient)
+        self.split_wgrad = bool(split_wgrad) and precision == "fp32" and self.device.type == "cuda"
+        if self.split_wgrad:
+            self._wg = torch.cuda.Stream(device=self.device)
+            self._wg_sync = [torch.cuda.Event() for _ in range(10)]
+            for e in self._wg_sync:
+                e.record()  # materialise the handles
 
     # ---- helpers
     def w(self, k):
@@ -123,9 +131,9 @@ class NeRFTrainer:
     def g(self, k):
         return self.grads[k * self.P:(k + 1) * self.P]
 
-    def _workspace(self, key, M):
+    def _workspace(self, key, M, two_stream=False):
         ws = self._ws.get(key)
-        need = K.mlp_workspace_bytes(M, 1, self.precision)
+        need = K.mlp_workspace_bytes_2s(M) if two_stream else K.mlp_workspace_bytes(M, 1, self.precision)
         if ws is None or ws.numel() < need:
             ws = torch.empty(need, dtype=torch.uint8, device=self.device)
             self._ws[key] = ws
@@ -209,7 +217,7 @@ class NeRFTrainer:
         if NI > 0:
             t_f = K.sample_pdf(t_c, w_c, NI, u=u_pdf, det=False, seed=seed ^ 0x5EED)
             xd_f = K.build_xd(rays, t_f)
-            ws_f = self._workspace("f", N * (S + NI))
+            ws_f = self._workspace("f", N * (S + NI), two_stream=self.split_wgrad)
             ev = ev_box[0]
             rs_f = K.mlp_fwd(self.w(fine_k), xd_f, ws_f, True, events=ev["fwd"] if ev else None,
                              precision=self.precision, bf16_flags=self.bf16_flags)
@@ -220,7 +228,9 @@ class NeRFTrainer:
                                                     loss_sum=self.loss_buf)
             d_rs_f = K.composite_bwd(rs_f, t_f, bg, drgb_f, sigma_scale=self.sigma_scale)
             K.mlp_bwd(self.w(fine_k), N * (S + NI), d_rs_f, ws_f, d_w=self.g(fine_k), accumulate=False,
-                      events=ev["bwd"] if ev else None, precision=self.precision, bf16_flags=self.bf16_flags)
+                      events=ev["bwd"] if ev else None, precision=self.precision, bf16_flags=self.bf16_flags,
+                      wgrad_stream=self._wg if self.split_wgrad else None,
+                      sync=self._wg_sync if self.split_wgrad else None)
             if ev:
                 self.timing["M"] = N * (S + NI)
         if side_done is not None:

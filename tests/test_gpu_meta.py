@@ -183,7 +183,8 @@ def test_task_adapt_golden(algo):
     from nerf_amd.meta import task_adapt
     z = load("meta")
     model, net = _meta_model()
-    P = types.SimpleNamespace(algo=algo, fim=False, ray_samples=32, chunk_points=1 << 20, color_space="linear")
+    P = types.SimpleNamespace(algo=algo, fim=False, use_amp=False, ray_samples=32, chunk_points=1 << 20,
+                              color_space="linear")
     before = {n: p.detach().clone() for n, p in net.meta_named_parameters()}
     fast, losses = task_adapt(P, model, {"rays": z["rays"].to(DEV), "rgbs": z["gt"].to(DEV)}, 0.05, 3,
                               active_module=0)
@@ -250,6 +251,22 @@ def test_reptile_many_tensors_chunked():
     MO.reptile_update(ref, fl, 0.3)
     for n in theta:
         assert torch.equal(m.t[n].cpu(), ref[n]), n
+
+
+def test_task_adapt_amp_runs_bf16_kernels():
+    """P.use_amp (the reference's default, meta_core.py:30-38): the inner forwards run under autocast(fp16), so the
+    vanilla expert takes its bf16 MLP kernels — losses within bf16 rounding of the fp32 golden inner loop (2 %), fast
+    weights finite and different from the fp32 ones."""
+    from nerf_amd.meta import task_adapt
+    z = load("meta")
+    model, net = _meta_model()
+    P = types.SimpleNamespace(algo="reptile", fim=False, use_amp=True, ray_samples=32, chunk_points=1 << 20,
+                              color_space="linear")
+    fast, losses = task_adapt(P, model, {"rays": z["rays"].to(DEV), "rgbs": z["gt"].to(DEV)}, 0.05, 3,
+                              active_module=0)
+    torch.testing.assert_close(torch.stack(losses).cpu(), z["losses"], rtol=2e-2, atol=1e-6)
+    assert all(torch.isfinite(v).all() for v in fast.values())
+    assert any(not torch.equal(v.detach().cpu(), z[f"fast/{n}"]) for n, v in fast.items())
 
 
 def test_fim_loss_refused():
