@@ -92,8 +92,8 @@ def parse():
     ap.add_argument("--no-psnr", action="store_true",
                     help="skip the full-image PSNR record (training to --psnr-steps + held-out renders, N = 1 only)")
     ap.add_argument("--no-overlap", action="store_true", help="run the coarse-net backward on the main stream")
-    ap.add_argument("--no-split-wgrad", action="store_true",
-                    help="fp32: keep the fine net's weight-gradient GEMMs on the main stream (nerf_mlp_bwd)")
+    ap.add_argument("--split-wgrad", action="store_true",
+                    help="fp32: the fine net's weight-gradient GEMMs on a second stream (nerf_mlp_bwd_2s)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (the product); gloo = rehearsal of N ranks sharing the visible GPUs")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
@@ -373,7 +373,7 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl):
     coarse, fine = VanillaNeRF().to(dev), VanillaNeRF().to(dev)
     tr = NeRFTrainer(coarse, fine, n_samples=a.samples, n_importance=a.importance, world_size=world, device=dev,
                      overlap=not a.no_overlap, precision=precision,
-                     bf16_flags=a.bf16_flags if precision == "bf16" else 0, split_wgrad=not a.no_split_wgrad)
+                     bf16_flags=a.bf16_flags if precision == "bf16" else 0, split_wgrad=a.split_wgrad)
 
     def one(step):
         rays, gt = _batch(rb, a, step, rank, world, n_local)

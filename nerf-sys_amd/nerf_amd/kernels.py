@@ -179,6 +179,9 @@ def mlp_bwd(w_packed, M, d_rgb_sigma, ws, d_w=None, accumulate=False, events=Non
     if wgrad_stream is not None:
         if sync is None or len(sync) < 10:
             raise ValueError("nerf_mlp_bwd_2s needs 10 sync events")
+        for e in sync:  # torch creates an event's HIP handle at its first record
+            if not e.cuda_event:
+                e.record()
         check(lib().nerf_mlp_bwd_2s(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws), ws.numel(),
                                     _events_arg(events), stream(), ctypes.c_void_p(wgrad_stream.cuda_stream),
                                     _events_arg(sync)), "nerf_mlp_bwd_2s")

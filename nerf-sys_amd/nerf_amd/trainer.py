@@ -60,7 +60,7 @@ class NeRFTrainer:
                  eps: float = 1e-8, weight_decay: float = 0.0, grad_clip: Optional[float] = 1.0,
                  color_space: str = "linear", bg: str = "white", sigma_scale: float = 1.0,
                  world_size: int = 1, device="cuda", overlap: bool = True, precision: str = "fp32",
-                 overlap_with: str = "fwd", bf16_flags: int = 0, split_wgrad: bool = True):
+                 overlap_with: str = "fwd", bf16_flags: int = 0, split_wgrad: bool = False):
         L = PackedLayout.get()
         self.L = L
         self.P = L.total
@@ -115,8 +115,10 @@ class NeRFTrainer:
             raise ValueError("overlap_with must be 'fwd' or 'bwd'")
         self.overlap_with = overlap_with
         self._side = torch.cuda.Stream(device=self.device) if self.overlap else None
-        # fp32: the fine net's weight-gradient GEMMs on their own stream beside its input-gradient chain
-        # (nerf_mlp_bwd_2s: bitwise the one-stream gradient)
+        # fp32, opt-in: the fine net's weight-gradient GEMMs on their own stream beside its input-gradient chain
+        # (nerf_mlp_bwd_2s: bitwise the one-stream gradient).  Measured on MI355X (C2, two A/B rounds on one box):
+        # 152.3k / 152.2k rays/s against 151.9k / 152.0k in line — both chains are MFMA-bound at ~0.8 busy and
+        # share the CUs, so the overlap buys ~0.2 % for 6.4 GB more workspace; off by default.
         self.split_wgrad = bool(split_wgrad) and precision == "fp32" and self.device.type == "cuda"
         if self.split_wgrad:
             self._wg = torch.cuda.Stream(device=self.device)

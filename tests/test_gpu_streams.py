@@ -2,7 +2,8 @@
 second stream beside the input-gradient chain.  It launches the same kernels on the same grids into the same split
 slabs, so the packed gradient must be BITWISE the one-stream nerf_mlp_bwd's — at a ragged size, at the C2 fine-net
 size, accumulating into a non-zero target — and a NeRFTrainer step with the fine weight gradients on their own
-stream must equal the in-line step (loss, gradient buffer, post-Adam parameters) over three steps."""
+stream must equal the in-line step over three steps: gradient buffer and post-Adam parameters bitwise, the loss scalar
+(summed by per-ray atomics in the compositing kernel) to rounding."""
 import pytest
 import torch
 
@@ -68,6 +69,7 @@ def test_trainer_split_wgrad_equals_inline(K):
         res[split] = out
     for s in range(3):
         a, b = res[False][s], res[True][s]
-        assert a[0] == b[0], (s, a[0], b[0])
+        # the loss scalar is summed by per-ray atomics (order not fixed run to run); the gradients do not depend on it
+        assert abs(a[0] - b[0]) <= 1e-6 * abs(a[0]), (s, a[0], b[0])
         assert torch.equal(a[1], b[1]), f"step {s}: gradient buffers differ"
         assert torch.equal(a[2], b[2]), f"step {s}: parameters differ"

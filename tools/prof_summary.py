@@ -1,4 +1,11 @@
-"""Summarise a rocprofv3 --stats kernel_stats.csv per train step (our kernels only)."""
+"""Summarise a rocprofv3 --stats kernel_stats.csv per train step (our kernels only).
+
+  python tools/prof_summary.py run_kernel_stats.csv STEPS [ROOFLINE_STEPS]
+
+STEPS = engine steps in the profiled run (warmup + timed + roofline pass); ROOFLINE_STEPS (bench.py --timing-steps,
+default 3) = the isolated steps bench.py runs after its timed region for the live roofline: the per-(kernel, grid)
+table then also averages only each population's launches of those last steps — the launches the bench line's
+`roofline.mean_launch_ms` is measured on."""
 import csv
 import sys
 
@@ -33,7 +40,15 @@ if tr:
         if not r["Kernel_Name"].startswith("void gemm_"):
             continue
         blocks = int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"])
-        per[(r["Kernel_Name"].split("(")[0], blocks)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    print("\nper (GEMM kernel, grid) launch averages from the kernel trace:")
-    for (n, b), v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
-        print(f"{sum(v) / len(v):9.1f} us avg  x{len(v):4d}  blocks={b:6d}  {n[:80]}")
+        per[(r["Kernel_Name"].split("(")[0], blocks)].append(
+            (int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+    rsteps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    print("\nper (GEMM kernel, grid) launch averages from the kernel trace (all launches | the launches of the last "
+          f"{rsteps} steps = bench.py's isolated roofline pass):")
+    for (n, b), v in sorted(per.items(), key=lambda kv: -sum(d for _, d in kv[1])):
+        v.sort()
+        k = max(1, round(len(v) * rsteps / steps))
+        tail = [d for _, d in v[-k:]]
+        allv = [d for _, d in v]
+        print(f"{sum(allv) / len(allv):9.1f} us avg x{len(allv):4d} | {sum(tail) / len(tail):9.1f} us avg x{k:3d}  "
+              f"blocks={b:6d}  {n[:80]}")
