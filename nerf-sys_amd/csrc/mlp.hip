@@ -17,6 +17,7 @@
 #include "gemm.hpp"
 #include "mlp_common.hpp"
 #include "mlp_tail.hpp"
+#include "mlp_fwd_tail.hpp"
 
 namespace {
 using namespace nerf_mlp;
@@ -308,7 +309,29 @@ extern "C" int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* 
     in = out;
     ld_in = ld_out;
   }
-  // heads
+  // heads + colour MLP + output activations in ONE launch (mlp_fwd_tail.hpp); NERF_FWD_TAIL_CHAIN keeps the
+  // five-launch chain (head GEMM, colour-input build, colour GEMMs, head_out) for A/B runs
+#ifndef NERF_FWD_TAIL_CHAIN
+  {
+    static int n_cu = 0;
+    if (!n_cu) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
+    }
+    FwdTailArgs T{};
+    T.Y7 = in; T.ldy = ld_in; T.xd = x_d; T.w = w;
+    T.off_wh = L.off[16]; T.off_bh = L.off[17]; T.off_wc0 = L.off[18]; T.off_bc0 = L.off[19];
+    T.off_wc1 = L.off[20]; T.off_bc1 = L.off[21];
+    T.O16 = W.O16; T.CIN = W.CIN; T.C0 = W.C0; T.O3 = W.O3; T.out = rgb_sigma;
+    T.M = M; T.Mp = Mp; T.ntiles = (int)(Mp / FT_ROWS);
+    const int grid = T.ntiles < 2 * n_cu ? T.ntiles : 2 * n_cu;
+    if (training)
+      fwd_tail_kernel<true><<<grid, 256, 0, st>>>(T);
+    else
+      fwd_tail_kernel<false><<<grid, 256, 0, st>>>(T);
+  }
+#else
   TRY(nt<EPI_BIAS>(in, ld_in, Wt(16), 256, Wt(17), W.O16, 32, nullptr, nullptr, Mp, 32, 256, st));
   build_cin_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(x_d, W.O16, M, Mp, W.CIN);
   // K = 48: the colour input has 42 real columns (15 geo + 27 direction PE), columns 48..63 are zero in CIN
@@ -316,6 +339,7 @@ extern "C" int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* 
                         st));
   TRY(nt<EPI_BIAS>(W.C0, 128, Wt(20), 128, Wt(21), W.O3, 32, nullptr, nullptr, Mp, 32, 128, st));
   head_out_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(W.O3, W.O16, M, rgb_sigma);
+#endif
   return nerf_launch_status();
 }
 
