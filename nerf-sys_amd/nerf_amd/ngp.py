@@ -502,6 +502,8 @@ class _NgpFn(torch.autograd.Function):
                                model._aabb_host, model._eps)
             TIMING.stop(h)
             if d_w is not None:
+                if flat:
+                    _table_grad_ready(t)
                 return None, (None if flat else tgt), d_w, None
         h = TIMING.start("mlp_bwd", x_d.shape[0])
         d_enc, d_w = ngp_bwd(model.net_struct, w_packed, enc, x_d, g)
@@ -514,11 +516,20 @@ class _NgpFn(torch.autograd.Function):
                 # a zeroed (rows, F) tensor that autograd would then add (saves ~4 x 134 MB of HBM per expert)
                 hash_encode_bwd(model.xyz_encoder.grid, x_d, d_enc, ctx.rows, model._aabb_host, model._eps,
                                 d_table=t.grad)
+                _table_grad_ready(t)
             else:
                 d_table = hash_encode_bwd(model.xyz_encoder.grid, x_d, d_enc, ctx.rows, model._aabb_host,
                                           model._eps)
             TIMING.stop(h)
         return None, d_table, d_w, None
+
+
+def _table_grad_ready(t):
+    """A FlatAdam-owned table's gradient is complete in stream order (its only writer, this expert's backward, has
+    been enqueued): FlatAdam's bucketed exchange starts that table's all-reduce now (optim.FlatAdam)."""
+    cb = getattr(t, "_nerf_grad_ready", None)
+    if cb is not None:
+        cb(t)
 
 
 class _Block(nn.Module):

@@ -33,7 +33,7 @@ class FlatAdam:
     they stay opt-in until an 8-GPU run covers them."""
 
     def __init__(self, groups: List[Dict], betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 grad_clip=1.0, world_size: int = 1, shard: bool = False):
+                 grad_clip=1.0, world_size: int = 1, shard: bool = False, bucket_tables: bool = True):
         if len(groups) > 8:
             raise ValueError("at most 8 parameter groups (nerf_adam segments)")
         params = [p for g in groups for p in g["params"]]
@@ -80,8 +80,37 @@ class FlatAdam:
         self.params = params
         self.betas, self.eps, self.wd, self.grad_clip = betas, eps, weight_decay, grad_clip
         self.step_count = 0
+        # Bucketed exchange (replicated update, world_size > 1): a parameter whose gradient a HIP backward writes in
+        # place (the Instant-NGP hash tables, 0.54 GB for four experts) is its own bucket: the backward calls
+        # _bucket_ready when it has enqueued its write, and that slice's all-reduce starts at once on the
+        # collective's stream, overlapping the rest of the backward; step() waits for the buckets and all-reduces
+        # the remaining ranges.
+        self.bucket_tables = bool(bucket_tables) and self.world_size > 1 and not self.shard
+        self._slices = {}
+        o = 0
+        for p in params:
+            self._slices[id(p)] = (o, p.numel())
+            o += p.numel()
+        self._inflight = []     # (handle, offset, numel) of buckets started in this step
+        self.exchange_events = None
+        self._fired = set()
+        if self.bucket_tables:
+            for p in params:
+                if p.numel() >= (1 << 20):  # big in-place-written parameters only (tables)
+                    p._nerf_grad_ready = self._bucket_ready
+
+    def _bucket_ready(self, p):
+        import torch.distributed as dist
+        if id(p) in self._fired:
+            raise RuntimeError("bucketed exchange: a bucketed gradient was written twice in one step")
+        self._fired.add(id(p))
+        o, k = self._slices[id(p)]
+        self._inflight.append((dist.all_reduce(self.grad[o:o + k], async_op=True), o, k))
 
     def zero_grad(self):
+        if self._inflight:
+            raise RuntimeError("zero_grad with bucketed all-reduces in flight (call step() first)")
+        self._fired.clear()
         self.grad.zero_()
         lo, hi = self.grad.data_ptr(), self.grad.data_ptr() + self.grad.numel() * 4
         for p in self.params:  # autograd must keep accumulating into the flat views
@@ -92,7 +121,24 @@ class FlatAdam:
         """Data parallel (as for the vanilla step): ONE all-reduce of the flat gradient buffer, then
         the mean over ranks (each rank's loss is its local-batch mean) — the gradient DDP would produce."""
         if self.world_size > 1:
-            allreduce_flat(self.grad, self.world_size)
+            ev = self.exchange_events  # optional (start, end) torch.cuda.Events: the exchange's exposed tail
+            if ev is not None:
+                ev[0].record()
+            if self._inflight:
+                import torch.distributed as dist
+                done = sorted((o, k) for _, o, k in self._inflight)
+                for h, _, _ in self._inflight:
+                    h.wait()  # orders the current stream after the collective (no host sync on RCCL)
+                self._inflight = []
+                lo = 0
+                for o, k in done + [(self.grad.numel(), 0)]:  # the ranges no bucket covered
+                    if o > lo:
+                        dist.all_reduce(self.grad[lo:o])
+                    lo = max(lo, o + k)
+            else:
+                allreduce_flat(self.grad, self.world_size)
+            if ev is not None:
+                ev[1].record()
             self.grad.mul_(1.0 / self.world_size)
 
     def _step_sharded(self):

@@ -139,14 +139,19 @@ def test_trainer_world2_equals_full_batch():
     assert (perr <= bound).all(), f"post-Adam: {int((perr > bound).sum())} elements beyond the implied bound"
 
 
-def _adam_run(world, rank, shard):
-    """Three FlatAdam steps on rank-dependent gradients (the clip binds): parameters after each step."""
+def _adam_run(world, rank, mode):
+    """Three FlatAdam steps on rank-dependent gradients (the clip binds): parameters after each step.  mode: "shard"
+    (reduce-scatter + all-gather), "replicated" (one all-reduce) or "bucketed" (a 1 M-float parameter whose gradient
+    is written in place and announced as complete, as the Instant-NGP table backward does, starting its all-reduce
+    before step(); the other ranges are all-reduced in step())."""
     from nerf_amd.optim import FlatAdam
     torch.manual_seed(0)
     dev = torch.device("cuda", 0)
-    ps = [torch.nn.Parameter(torch.randn(37, 11, device=dev)), torch.nn.Parameter(torch.randn(1000, device=dev)),
-          torch.nn.Parameter(torch.randn(5, 3, device=dev))]
-    opt = FlatAdam([{"params": ps[:1], "lr": 1e-2}, {"params": ps[1:], "lr": 3e-3}], world_size=world, shard=shard)
+    big = mode == "bucketed"
+    shapes = [(37, 11), (1000,), (5, 3)] + ([((1 << 20) + 37,)] if big else []) + [(7,)]
+    ps = [torch.nn.Parameter(torch.randn(sh, device=dev)) for sh in shapes]
+    opt = FlatAdam([{"params": ps[:1], "lr": 1e-2}, {"params": ps[1:], "lr": 3e-3}], world_size=world,
+                   shard=(mode == "shard"), bucket_tables=big)
     out = []
     g = torch.Generator().manual_seed(123)
     gr = [[torch.randn(p.shape, generator=g) for p in ps] for _ in range(3 * max(world, 2))]
@@ -158,13 +163,17 @@ def _adam_run(world, rank, shard):
                     p.grad.copy_(((gr[2 * step][i] + gr[2 * step + 1][i]) * 0.5).to(dev))
                 else:
                     p.grad.copy_(gr[2 * step + rank][i].to(dev))
+                if big and world > 1 and p.numel() >= (1 << 20):
+                    assert getattr(p, "_nerf_grad_ready", None) is not None
+                    p._nerf_grad_ready(p)  # its all-reduce starts here, before step()
+                    assert len(opt._inflight) == 1
         opt.step()
         torch.cuda.synchronize()
         out.append(torch.cat([p.detach().reshape(-1).cpu() for p in ps]))
     return out
 
 
-def _adam_worker(rank, world, port, q, shard):
+def _adam_worker(rank, world, port, q, mode):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "nerf-sys_amd")]
@@ -173,7 +182,7 @@ def _adam_worker(rank, world, port, q, shard):
     try:
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        q.put((rank, _by_value(_adam_run(world, rank, shard))))
+        q.put((rank, _by_value(_adam_run(world, rank, mode))))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:
@@ -181,16 +190,17 @@ def _adam_worker(rank, world, port, q, shard):
         raise
 
 
-@pytest.mark.parametrize("shard", [True, False])
-def test_flat_adam_world2(shard):
-    """FlatAdam at world 2 — sharded (reduce-scatter, clip + Adam on a 1/N slice, all-gather) and replicated
-    (all-reduce) — against the single-process step on the mean gradient; both ranks bitwise equal."""
+@pytest.mark.parametrize("mode", ["shard", "replicated", "bucketed"])
+def test_flat_adam_world2(mode):
+    """FlatAdam at world 2 — sharded (reduce-scatter, clip + Adam on a 1/N slice, all-gather), replicated (one
+    all-reduce) and bucketed (the in-place table bucket's all-reduce started before step()) — against the
+    single-process step on the mean gradient; both ranks bitwise equal."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_adam_worker, args=(r, world, port, q, shard)) for r in range(world)]
+    procs = [ctx.Process(target=_adam_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     res = {r: _to_torch(v) for r, v in (q.get(timeout=100) for _ in range(world))}
@@ -198,7 +208,7 @@ def test_flat_adam_world2(shard):
         p.join(timeout=60)
     for r in range(world):
         assert isinstance(res[r], list), f"rank {r} failed: {res[r]}"
-    full = _adam_run(1, 0, False)
+    full = _adam_run(1, 0, mode)
     for step in range(3):
         assert torch.equal(res[0][step], res[1][step]), f"step {step}: ranks diverged"
         # the rank mean (a + b) / 2 vs the full batch's (a + b) * 0.5 is exact; the clip norm's partial sums are

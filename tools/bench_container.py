@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shard", action="store_true", help="shard FlatAdam over the ranks (reduce-scatter + all-gather)")
+    ap.add_argument("--no-bucket", action="store_true",
+                    help="one all-reduce of the flat gradient in step() instead of per-table buckets started by the "
+                         "hash-table backward")
     return ap.parse_args()
 
 
@@ -133,7 +136,7 @@ def build_step(a, dev, rank=0, world=1):
     model = model.to(dev).train()
     lr = {"encoding": 1e-2, "sigma": 2e-3, "color": 2e-3, "background": 1e-3}
     groups = [{"params": g["params"], "lr": lr[k]} for k, g in model.get_param_groups().items()]
-    opt = FlatAdam(groups, grad_clip=1.0, world_size=world, shard=a.shard)
+    opt = FlatAdam(groups, grad_clip=1.0, world_size=world, shard=a.shard, bucket_tables=not a.no_bucket)
     rb = RayBatcher(scene, dev)
     P = SimpleNamespace(ray_samples=96, chunk_points=262_144 * 17, color_space="linear")
 
@@ -146,6 +149,7 @@ def build_step(a, dev, rank=0, world=1):
         opt.step()
         return loss
 
+    one.opt = opt
     return one, model
 
 
@@ -182,6 +186,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     # per-kernel-class times from HIP events in separate steps
+    exch = None
+    if world > 1:  # the exchange's exposed tail per step: HIP events around FlatAdam's wait + remaining all-reduce
+        ms_ex = []
+        for s in range(a.steps):
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            one.opt.exchange_events = ev
+            one(a.warmup + a.steps + s)
+            torch.cuda.synchronize()
+            ms_ex.append(ev[0].elapsed_time(ev[1]))
+        one.opt.exchange_events = None
+        exch = {"exposed_exchange_ms": round(sum(ms_ex) / len(ms_ex), 4), "bucketed": one.opt.bucket_tables,
+                "grad_bytes": int(one.opt.grad.numel() * 4),
+                "note": "events on the compute stream around FlatAdam's wait for the table buckets (started by each "
+                        "expert's hash backward) plus the all-reduce of the remaining ranges; mean over the steps"}
     G.TIMING.enabled = True
     for s in range(a.steps):
         one(a.warmup + a.steps + s)
@@ -225,6 +243,8 @@ def main():
         "samples_per_step": round((rows.get("fwd_enc", 0) + rows.get("mlp_fwd", 0)) / a.steps),
         "final_loss": round(float(loss.item()), 6),
     }
+    if exch:
+        out["exchange"] = exch
     out["cpu_baseline"] = None if (a.no_cpu_baseline or world > 1) else cpu_baseline(a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
