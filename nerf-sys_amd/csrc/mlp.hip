@@ -35,6 +35,13 @@ struct WS {
 };
 
 constexpr int64_t WT_FLOATS = 7 * 65536 + 256 * 32;
+// the head backward (dZ7, head weight / bias sums) is one pass (head_bwd_kernel) unless NERF_BWD_TAIL_CHAIN keeps the
+// separate head dgrad / wgrad GEMMs for A/B runs; the second-half sums of the split walks start at P2BASE
+#ifndef NERF_BWD_TAIL_CHAIN
+#define P2BASE (layout().off[16])
+#else
+#define P2BASE (layout().off[18])
+#endif
 
 WS carve(void* base, int64_t M, int training) {
   WS w{};
@@ -67,12 +74,12 @@ WS carve(void* base, int64_t M, int training) {
       w.dA = take(Mp * 256);
       w.dB = take(Mp * 256);
     }
-    w.dO16 = take(Mp * 32);
+    w.dO16 = take(Mp * 32);  // [Mp][16] for the fused head backward, [Mp][32] for the chain
     w.WT = take(WT_FLOATS);
     w.S = n_splits(Mp);
     w.rps = round_up(nerf_cdiv(Mp, w.S), 64);  // whole slabs for every wgrad MR
     w.partial = take((int64_t)w.S * layout().total);
-    w.partial2 = take((int64_t)w.S * (layout().total - layout().off[18]));  // colour sums of the second halves
+    w.partial2 = take((int64_t)w.S * (layout().total - P2BASE));  // head + colour sums of the second halves
   }
   w.bytes = (int64_t)((char*)p - (char*)base);
   return w;
@@ -388,25 +395,37 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
     jobs.j[nj++] = TJob{Wt(2 * i), T, 256, 256, KPAD[i]};  // first 256 input cols (h part for trunk.4)
     T += 65536;
   }
+#ifdef NERF_BWD_TAIL_CHAIN
   float* Wht = T;  jobs.j[nj++] = TJob{Wt(16), Wht, 32, 256, 256};  // [256][32]
+#endif
   transpose_kernel<<<dim3(8, 8, nj), 256, 0, st>>>(jobs);
 
   // colour branch + head activations in one kernel: dO16 and the colour weight / bias slabs (two workgroups per
   // split; the second halves' colour sums go to W.partial2 and are added by the final reduce)
-  color_bwd_kernel<float, float><<<2 * W.S, 256, 0, st>>>(d_rgb_sigma, W.O3, W.O16, W.C0, W.CIN, Wt(18), Wt(20), W.dO16, W.partial,
-                                        L.total, L.off[18], L.off[19], L.off[20], L.off[21], W.rps, M, Mp, W.partial2, L.total - L.off[18]);
-  // heads -> dZ7
   float* dcur = W.dA;
   float* dnext = W.dB;
-  // events 2/3 (layer 0 has no input gradient) bracket this head dgrad: same kernel and grid as the trunk
-  // dgrads, so the roofline population matches the profiler's per-(kernel, grid) average
+  // events 2/3 (layer 0 has no input gradient) bracket the backward tail (colour branch + heads -> dZ7)
   if (ev) (void)hipEventRecord(ev[2], st);
-  // K = 16: head rows 16..31 are padding (zero weights, zero dO16 columns), so their products are exact zeros and
-  // dropping them changes no bit of dZ7
+#ifndef NERF_BWD_TAIL_CHAIN
+  // colour branch -> dO16 [Mp][16]; then ONE pass over Y7 for dZ7 and the head weight / bias sums (mlp_tail.hpp)
+  color_bwd_kernel<float, float><<<2 * W.S, 256, 0, st>>>(d_rgb_sigma, W.O3, W.O16, W.C0, W.CIN, Wt(18), Wt(20), W.dO16,
+                                                          W.partial, L.total, L.off[18], L.off[19], L.off[20], L.off[21],
+                                                          W.rps, M, Mp, W.partial2, L.total - P2BASE, P2BASE, 16);
+  head_bwd_kernel<<<2 * W.S, 256, 0, st>>>(W.dO16, W.Y[7], Wt(16), dcur, W.partial, L.total, W.partial2,
+                                           L.total - P2BASE, P2BASE, L.off[16], L.off[17], W.rps, Mp);
+  if (ev) (void)hipEventRecord(ev[3], st);
+  TRY(handoff(1));  // dZ7 and the head / colour slabs are complete
+#else
+  color_bwd_kernel<float, float><<<2 * W.S, 256, 0, st>>>(d_rgb_sigma, W.O3, W.O16, W.C0, W.CIN, Wt(18), Wt(20), W.dO16, W.partial,
+                                        L.total, L.off[18], L.off[19], L.off[20], L.off[21], W.rps, M, Mp, W.partial2,
+                                        L.total - P2BASE, P2BASE, 32);
+  // heads -> dZ7.  K = 16: head rows 16..31 are padding (zero weights, zero dO16 columns), so their products are
+  // exact zeros and dropping them changes no bit of dZ7
   TRY(nt<EPI_MASK>(W.dO16, 32, Wht, 32, nullptr, dcur, 256, W.MB[7], nullptr, Mp, 256, 16, st));
   if (ev) (void)hipEventRecord(ev[3], st);
   TRY(handoff(1));  // dZ7 and dO16 are complete (the colour branch ran before the head dgrad on st)
   TRY(wgrad(W.dO16, 32, W.Y[7], 256, 16, W, 32, 256, sw));
+#endif
   // trunk
   for (int i = 7; i >= 0; --i) {
     const float* X = (i == 0) ? W.X3E + 256 : (i == 4 ? W.X3E : W.Y[i - 1]);
@@ -429,7 +448,7 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
   }
   const int64_t n4 = L.total / 4;
   reduce_splits2_kernel<<<(unsigned)nerf_cdiv(n4, 256), 256, 0, st>>>(W.partial, L.total, W.S, d_w, n4, accumulate,
-                                                                      W.partial2, L.total - L.off[18], L.off[18] / 4);
+                                                                      W.partial2, L.total - P2BASE, P2BASE / 4);
   return nerf_launch_status();
 }
 }  // namespace

@@ -47,8 +47,11 @@ inline const Layout& layout() {
 inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
 // split-M partial slabs of the weight gradient: one per 2048 rows, at most 256
+#ifndef NERF_SPLIT_ROWS
+#define NERF_SPLIT_ROWS 2048
+#endif
 inline int n_splits(int64_t Mp) {
-  int64_t s = Mp / 2048;
+  int64_t s = Mp / NERF_SPLIT_ROWS;
   if (s < 1) s = 1;
   if (s > 256) s = 256;
   return (int)s;

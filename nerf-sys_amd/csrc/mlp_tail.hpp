@@ -50,10 +50,12 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
                                                         TD* __restrict__ dO16, float* __restrict__ partial,
                                                         int64_t slab, int64_t off_w0, int64_t off_b0,
                                                         int64_t off_w1, int64_t off_b1, int64_t rps, int64_t M,
-                                                        int64_t Mp, float* __restrict__ partial2, int64_t cslab) {
+                                                        int64_t Mp, float* __restrict__ partial2, int64_t cslab,
+                                                        int64_t p2base, int ldd) {
   // dC0 overwrites C0 in place and the dgeo halves reuse the CIN tile (one extra barrier each): 70.6 KB of
   // LDS, two workgroups per CU.  Workgroup 2s + h walks half h of split s; half 0 writes the colour sums into
-  // slab s, half 1 into row s of partial2 (cslab floats: the colour region off_w0 .. total of one slab).
+  // slab s, half 1 into row s of partial2 (cslab floats: packed offsets p2base .. total of one slab; p2base <=
+  // off_w0).  dO16 rows have pitch ldd: 32 (columns 16..31 written as zeros) or 16.
   __shared__ __attribute__((aligned(16))) float s_c0[CB_ROWS * CB_C0];
   float* const s_dc0 = s_c0;
   __shared__ __attribute__((aligned(16))) float s_cin[CB_ROWS * CB_CIN];
@@ -76,20 +78,26 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
   }
   for (int i = tid; i < 3 * 128; i += 256) s_w1[i] = Wc1[i];
 
-  // register prefetch of one tile: C0 = 2048 float4 (8 / thread), CIN = 1024 float4 (4 / thread)
-  float4 pc[8], pi[4];
+  // register prefetch of one tile: C0 = 2048 float4 (8 / thread), CIN = 1024 float4 (4 / thread); wave 0 also
+  // prefetches the tile's head outputs: d_rgb_sigma (M rows: the row index is clamped, the value zeroed below for
+  // m >= M), the three colour pre-activations of O3 and sigma_raw of O16.
+  float4 pc[8], pi[4], pg = make_float4(0.f, 0.f, 0.f, 0.f), po = pg;
+  float ps = 0.f;
+  // r0, r1, rps and the half length are multiples of CB_ROWS (the host rounds rps to 64; Mp is a multiple of 256),
+  // so every row of a tile is < r1 and the loads carry no row guard (a guarded load became a branch with a
+  // vmcnt(0) drain after it); a uniform tile base + 32-bit lane offsets keeps no 64-bit address per load live
   auto fetch = [&](int64_t t0) {
+    const TA* c0t = C0 + t0 * 128;
+    const TA* cit = CIN + t0 * 64;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int f = tid + 256 * u, r = f >> 5, c4 = f & 31;
-      const int64_t m = t0 + r;
-      pc[u] = m < r1 ? tail_ld4(C0 + m * 128 + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    for (int u = 0; u < 8; ++u) pc[u] = tail_ld4(c0t + (tid + 256 * u) * 4);  // row f >> 5, float4 f & 31
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int f = tid + 256 * u, r = f >> 4, c4 = f & 15;
-      const int64_t m = t0 + r;
-      pi[u] = m < r1 ? tail_ld4(CIN + m * 64 + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < 4; ++u) pi[u] = tail_ld4(cit + (tid + 256 * u) * 4);  // row f >> 4, float4 f & 15
+    if (tid < CB_ROWS) {  // wave 0 (uniform branch)
+      const int64_t m = t0 + tid, mc = m < M ? m : M - 1;
+      pg = reinterpret_cast<const float4*>(g)[mc];
+      po = *reinterpret_cast<const float4*>(O3 + m * 32);
+      ps = O16[m * 32];
     }
   };
 
@@ -116,14 +124,12 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
     if (tid < CB_ROWS) {
       const int64_t m = t0 + tid;
       float a = 0.f, b = 0.f, c = 0.f, ds = 0.f;
-      if (m < r1 && m < M) {
-        const float4 gg = reinterpret_cast<const float4*>(g)[m];
-        const float* o = O3 + m * 32;
-        const float s0 = sigmoidf_(o[0]), s1 = sigmoidf_(o[1]), s2 = sigmoidf_(o[2]);
-        a = gg.x * (s0 * (1.0f - s0));
-        b = gg.y * (s1 * (1.0f - s1));
-        c = gg.z * (s2 * (1.0f - s2));
-        ds = gg.w * expf(fminf(fmaxf(O16[m * 32], -EXP_MAX), EXP_MAX));
+      if (m < M) {
+        const float s0 = sigmoidf_(po.x), s1 = sigmoidf_(po.y), s2 = sigmoidf_(po.z);
+        a = pg.x * (s0 * (1.0f - s0));
+        b = pg.y * (s1 * (1.0f - s1));
+        c = pg.z * (s2 * (1.0f - s2));
+        ds = pg.w * expf(fminf(fmaxf(ps, -EXP_MAX), EXP_MAX));
       }
       s_do3[tid * 4 + 0] = a;
       s_do3[tid * 4 + 1] = b;
@@ -200,10 +206,10 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
     }
     __syncthreads();
     // ---- dO16 rows: [ds, dgeo (sum of the two halves), 0 x 16]
-    for (int f = tid; f < CB_ROWS * 8; f += 256) {
-      const int r = f >> 3, c4 = f & 7;
+    const int nc4 = ldd / 4;
+    for (int f = tid; f < CB_ROWS * nc4; f += 256) {
+      const int r = f / nc4, c4 = f - r * nc4;
       const int64_t m = t0 + r;
-      if (m >= r1) continue;
       float v[4] = {0.f, 0.f, 0.f, 0.f};
       if (c4 < 4) {
 #pragma unroll
@@ -213,11 +219,11 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
           else if (c <= 15) v[e] = s_geo[r * CB_GEO + c - 1] + s_geo[(CB_ROWS + r) * CB_GEO + c - 1];
         }
       }
-      tail_st4(dO16 + m * 32 + 4 * c4, make_float4(v[0], v[1], v[2], v[3]));
+      tail_st4(dO16 + m * ldd + 4 * c4, make_float4(v[0], v[1], v[2], v[3]));
     }
   }
   // ---- this split's slab: weight sums, bias sums (lane halves combined)
-  float* P = half ? partial2 + sp * cslab - off_w0 : partial + sp * slab;
+  float* P = half ? partial2 + sp * cslab - p2base : partial + sp * slab;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int n = (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -240,6 +246,113 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
   }
   if (tid == 128) P[off_b1 + 2] = b1;
 }
+// ------------------------------------------------------------------ fused head backward (fp32 path)
+// dZ7 = (dO16 Wh) * [Y7 > 0] and the head sums dWh += dO16^T Y7, dbh += colsum(dO16) in ONE pass over Y7: the one
+// read of a Y7 float4 is both the ReLU mask of the lane's own dZ7 float4 and a weight-gradient MFMA operand.  It
+// replaces the head input-gradient GEMM and the head weight-gradient GEMM, which streamed Y7 / dZ7 separately
+// (fine net, round 3: 258 + 216 us; this pass moves 2.1 KB per row: dO16 64 B + Y7 1 KB in, dZ7 1 KB out).
+// Same split walk as color_bwd (workgroup 2s + h, 64-row tiles, sums in registers, half 1 into partial2).  Lane
+// (g, j) of wave w owns columns hc = 64 w + 4 j .. + 3 and, in row group u, row 4 u + g: its dZ7 float4 is a
+// 16-term VALU dot against its register slice of Wh, and its Y7 float4 is the B operand of four 16x16x4 MFMAs
+// (column hc + q, q = 0..3) whose A operand is dO16[4 u + g][n = j] — output lane (g, j) register v then holds
+// dWh[4 g + v][hc + q].  dO16 tiles are double-buffered in LDS (one barrier per tile); Y7 streams in two 32-row
+// halves, each issued one half ahead, from a uniform tile base with 32-bit lane offsets.
+constexpr int HB_ROWS = 64;
+static __global__ __launch_bounds__(256, 2) void head_bwd_kernel(const float* __restrict__ dO16,  // [Mp][16]
+                                                       const float* __restrict__ Y7,    // [Mp][256]
+                                                       const float* __restrict__ Wh,    // [32][256], rows < 16 live
+                                                       float* __restrict__ dZ7,         // [Mp][256]
+                                                       float* __restrict__ partial, int64_t slab,
+                                                       float* __restrict__ partial2, int64_t cslab, int64_t p2base,
+                                                       int64_t off_wh, int64_t off_bh, int64_t rps, int64_t Mp) {
+  __shared__ __attribute__((aligned(16))) float s_d[2][HB_ROWS * 16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, j = lane & 15;
+  const int hc = 64 * wave + 4 * j;
+  const int64_t sp = blockIdx.x >> 1, half = blockIdx.x & 1;
+  const int64_t rph = ((rps + 2 * HB_ROWS - 1) / (2 * HB_ROWS)) * HB_ROWS;  // rows of half 0
+  const int64_t r0 = sp * rps + half * rph;
+  int64_t r1 = half ? sp * rps + rps : r0 + rph;
+  if (r1 > Mp) r1 = Mp;
+  // every tile row is < r1 (r0, r1 multiples of 64, as in color_bwd); "next tile" loads past the last tile re-read it
+  const int64_t last = r1 - HB_ROWS;
+
+  float4 wh[16];
+#pragma unroll
+  for (int n = 0; n < 16; ++n) wh[n] = *reinterpret_cast<const float4*>(Wh + n * 256 + hc);
+  nerf_f32x4 acc[4], accb;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = nerf_f32x4{0.f, 0.f, 0.f, 0.f};
+  accb = nerf_f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float4 dd = make_float4(0.f, 0.f, 0.f, 0.f), ya[8], yb[8];
+  auto load_y = [&](float4 (&y)[8], int64_t t0, int rb) {
+    const float* yt = Y7 + t0 * 256;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) y[u] = *reinterpret_cast<const float4*>(yt + ((rb + 4 * u + g) * 256 + hc));
+  };
+  auto rows = [&](const float4 (&y)[8], int64_t t0, int rb, const float* sd) {
+    float* zt = dZ7 + t0 * 256;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = rb + 4 * u + g;
+      const float* drow = sd + r * 16;
+      float z0 = 0.f, z1 = 0.f, z2 = 0.f, z3 = 0.f;
+#pragma unroll
+      for (int n4 = 0; n4 < 4; ++n4) {
+        const float4 d = *reinterpret_cast<const float4*>(drow + 4 * n4);
+        const float dn[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float4 w4 = wh[4 * n4 + e];
+          z0 = fmaf(dn[e], w4.x, z0);
+          z1 = fmaf(dn[e], w4.y, z1);
+          z2 = fmaf(dn[e], w4.z, z2);
+          z3 = fmaf(dn[e], w4.w, z3);
+        }
+      }
+      const float4 yy = y[u];
+      *reinterpret_cast<float4*>(zt + (r * 256 + hc)) =
+          make_float4(yy.x > 0.f ? z0 : 0.f, yy.y > 0.f ? z1 : 0.f, yy.z > 0.f ? z2 : 0.f, yy.w > 0.f ? z3 : 0.f);
+      const float a = drow[j];
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, yy.x, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, yy.y, acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, yy.z, acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, yy.w, acc[3], 0, 0, 0);
+      if (wave == 0) accb = __builtin_amdgcn_mfma_f32_16x16x4f32(a, 1.0f, accb, 0, 0, 0);
+    }
+  };
+
+  if (r0 < r1) {
+    dd = *reinterpret_cast<const float4*>(dO16 + r0 * 16 + tid * 4);  // 64 rows x 16 = one float4 per thread
+    load_y(ya, r0, 0);
+  }
+  int buf = 0;
+  for (int64_t t0 = r0; t0 < r1; t0 += HB_ROWS) {
+    const int64_t tn = t0 < last ? t0 + HB_ROWS : last;
+    float* sd = s_d[buf];
+    *reinterpret_cast<float4*>(sd + tid * 4) = dd;
+    __syncthreads();  // (the other buffer's readers finished before the previous tile's barrier)
+    dd = *reinterpret_cast<const float4*>(dO16 + tn * 16 + tid * 4);
+    load_y(yb, t0, 32);
+    rows(ya, t0, 0, sd);
+    load_y(ya, tn, 0);
+    rows(yb, t0, 32, sd);
+    buf ^= 1;
+  }
+
+  float* P = half ? partial2 + sp * cslab - p2base : partial + sp * slab;
+#pragma unroll
+  for (int v = 0; v < 4; ++v)
+    *reinterpret_cast<float4*>(P + off_wh + (int64_t)(4 * g + v) * 256 + hc) =
+        make_float4(acc[0][v], acc[1][v], acc[2][v], acc[3][v]);
+  for (int i = tid; i < 16 * 256; i += 256) P[off_wh + 16 * 256 + i] = 0.f;  // head rows 16..31: padding
+  if (wave == 0 && j == 0) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) P[off_bh + 4 * g + v] = accb[v];
+  }
+  if (tid >= 16 && tid < 32) P[off_bh + tid] = 0.f;
+}
+
 // reduce_splits plus the second-half colour sums: float4 i >= c0 of the packed gradient also adds
 // sum_s src2[s][i - c0] after the S slab terms (fixed order: bitwise reproducible)
 static __global__ void reduce_splits2_kernel(const float* __restrict__ src, int64_t slab, int S, float* __restrict__ dst,

@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--train-views", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend (gloo: a rehearsal of N ranks sharing one GPU; RCCL needs one GPU per rank)")
     ap.add_argument("--shard", action="store_true", help="shard FlatAdam over the ranks (reduce-scatter + all-gather)")
     ap.add_argument("--no-bucket", action="store_true",
                     help="one all-reduce of the flat gradient in step() instead of per-table buckets started by the "
@@ -159,10 +161,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local % torch.cuda.device_count())  # a gloo rehearsal may run more ranks than GPUs
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group(a.backend, device_id=dev if a.backend == "nccl" else None)
     from nerf_amd import ngp as G
 
     one, model = build_step(a, dev, rank, world)
