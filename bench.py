@@ -107,6 +107,10 @@ def parse():
     ap.add_argument("--psnr-steps", type=int, default=3000,
                     help="total train steps of each precision's engine before the held-out PSNR renders")
     ap.add_argument("--psnr-views", type=int, default=2, help="held-out 800x800 views rendered for the PSNR")
+    ap.add_argument("--fp32-gemm", default="split", choices=["split", "native"],
+                    help="fp32 trunk GEMMs: bf16 split products at fp32 accuracy (gemm_x6.hpp) or fp32 MFMA kernels")
+    ap.add_argument("--no-native-ref", action="store_true",
+                    help="skip the fp32-MFMA (native) engine leg timed beside the split-GEMM engine")
     return ap.parse_args()
 
 
@@ -364,7 +368,7 @@ def roofline(tm, bf16, overlap, bf16_flags=0):
     return roof
 
 
-def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl):
+def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_gemm=None):
     """The fused train step (NeRFTrainer) timed over a.steps after a.warmup: value, ms/step, the live-event roofline,
     and (N > 1) the per-rank exchange diagnostics.  Returns (record, trainer, (coarse, fine))."""
     from nerf_amd.trainer import NeRFTrainer
@@ -373,7 +377,8 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl):
     coarse, fine = VanillaNeRF().to(dev), VanillaNeRF().to(dev)
     tr = NeRFTrainer(coarse, fine, n_samples=a.samples, n_importance=a.importance, world_size=world, device=dev,
                      overlap=not a.no_overlap, precision=precision,
-                     bf16_flags=a.bf16_flags if precision == "bf16" else 0, split_wgrad=a.split_wgrad)
+                     bf16_flags=a.bf16_flags if precision == "bf16" else 0, split_wgrad=a.split_wgrad,
+                     fp32_gemm=fp32_gemm or a.fp32_gemm)
 
     def one(step):
         rays, gt = _batch(rb, a, step, rank, world, n_local)
@@ -428,6 +433,8 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl):
                             event_pass="the timing_steps steps after the timed region, every launch alone (no "
                                        "side-stream coarse backward, fine weight gradients in line)"),
            "streams": {"coarse_bwd_beside_fine_fwd": tr.overlap, "fine_wgrad_stream": tr.split_wgrad}}
+    if precision == "fp32":
+        rec["fp32_gemm"] = tr.fp32_gemm
     peak = BF16_MFMA_PEAK_TFLOPS if precision == "bf16" else FP32_MFMA_PEAK_TFLOPS
     rec["step_mfma_frac"] = round(rec["value"] * FLOP_PER_RAY / world / 1e12 / peak, 4)
     if dp:
@@ -535,6 +542,9 @@ def main():
             sub["dropin"] = dropin_run(rb, dev, a, world, rank, n_local, other)
             sub["dropin_vs_engine"] = round(sub["dropin"]["value"] / sub["value"], 4)
 
+    native = None
+    if (world == 1 and a.path == "engine" and not bf16 and a.fp32_gemm == "split" and not a.no_native_ref):
+        native, _, _ = engine_run(a, dev, rb, world, rank, n_local, "fp32", barrier, nccl, fp32_gemm="native")
     main_res = drop if a.path == "dropin" else engine
     value = main_res["value"]
     out = {
@@ -550,7 +560,7 @@ def main():
                                (" [drop-in render_rays/autograd path]" if a.path == "dropin" else " [fused engine]"),
                    "global_batch": a.batch if a.strong else a.batch * world, "rays_per_gpu": n_local,
                    "samples": [a.samples, a.importance], "parallelism": f"dp{world}", "precision": a.precision,
-                   "path": a.path},
+                   "path": a.path, "fp32_gemm": None if bf16 else a.fp32_gemm},
         "rccl_ranks": world, "backend": ("nccl (RCCL)" if nccl else "gloo (rehearsal)") if world > 1 else None,
         "roofline": engine["roofline"] if engine else None,
         "step_mfma_frac": round(value * FLOP_PER_RAY / world / 1e12 /
@@ -567,6 +577,9 @@ def main():
         out["dropin_vs_engine"] = round(drop["value"] / engine["value"], 4)
     if sub:
         out[other] = sub
+    if native:
+        out["fp32_native_gemm"] = {k: native[k] for k in ("value", "ms_per_step", "final_loss", "step_mfma_frac")}
+        out["fp32_native_gemm"]["roofline_classes_ms"] = native["roofline"].get("classes_ms")
     progress("timed legs done")
     if not a.no_psnr and rank == 0 and runs and world == 1:
         out["psnr"] = psnr_run(a, rb, scene, runs, rank, world, n_local)

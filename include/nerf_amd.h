@@ -112,7 +112,7 @@ int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* rgb_sigma, 
 int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
                  int64_t ws_bytes, hipEvent_t* events, hipStream_t stream);
 /* events: NULL, or 32 hipEvent_t: events[4i+0/1] bracket the weight-gradient GEMM of trunk.i,
- * events[4i+2/3] its input-gradient GEMM (i >= 1); events[2/3] bracket the head's input-gradient GEMM. */
+ * events[4i+2/3] its input-gradient GEMM (i >= 1); events[2/3] bracket the backward tail (colour branch + head -> dZ7). */
 
 /* nerf_mlp_bwd with the weight-gradient GEMMs on a second stream: the input-gradient chain (colour branch, head and
  * trunk dgrads) stays on `stream`; each weight-gradient GEMM runs on `wgrad_stream` behind an event recorded on
@@ -125,6 +125,22 @@ int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
 int64_t nerf_mlp_workspace_bytes_2s(int64_t M);
 int nerf_mlp_bwd_2s(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
                     int64_t ws_bytes, hipEvent_t* events, hipStream_t stream, hipStream_t wgrad_stream, hipEvent_t* sync);
+
+/* fp32 GEMM engine of the three calls above.  Default (flags 0, and the un-suffixed entry points): the 256-wide
+ * trunk GEMMs (forward, input gradient, weight gradient) run on the bf16 matrix cores as split products — every fp32
+ * operand is cut into three bf16 pieces hi + mid + lo that sum to it exactly, and the six piece products down to
+ * 2^-16 of the leading one are accumulated in fp32 (v_mfma_f32_32x32x16_bf16); measured error against fp64 equals the
+ * fp32 MFMA's and a sequential fp32 fmaf chain's (tools/split_probe.hip).  NERF_MLP_NATIVE_FP32 selects the
+ * v_mfma_f32_16x16x4_f32 kernels instead.  Unknown flag bits: NERF_E_ENUM.  Replaces the same reference interfaces as
+ * nerf_mlp_fwd / nerf_mlp_bwd (MetaNeRF forward / autograd, models/inr/meta_vanilla.py:123-154). */
+#define NERF_MLP_NATIVE_FP32 1
+int nerf_mlp_fwd_ex(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws, int64_t ws_bytes,
+                    int training, int flags, hipEvent_t* events, hipStream_t stream);
+int nerf_mlp_bwd_ex(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
+                    int64_t ws_bytes, int flags, hipEvent_t* events, hipStream_t stream);
+int nerf_mlp_bwd_2s_ex(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
+                       int64_t ws_bytes, int flags, hipEvent_t* events, hipStream_t stream, hipStream_t wgrad_stream,
+                       hipEvent_t* sync);
 
 /* bf16 variants (BASELINE configs[2]: "bf16 MLP with fp32 compositing"): the same network, packed fp32
  * parameters, inputs and outputs as nerf_mlp_fwd/bwd; the layer GEMMs run on bf16 MFMA with fp32

@@ -1,0 +1,380 @@
+// fp32 trunk GEMMs on the bf16 matrix cores: every fp32 operand is split into three bf16 pieces x = hi + mid + lo
+// (round-to-nearest at each step; 3 x 8 significant bits cover fp32's 24, so the split is exact for normal numbers)
+// and A.B^T is accumulated in fp32 from the six piece products whose magnitude is >= 2^-16 of the leading one:
+//   lo.hi + mid.mid + hi.lo + mid.hi + hi.mid + hi.hi     (smallest first, one fp32 accumulator per output)
+// The three dropped products (mid.lo, lo.mid, lo.lo) are <= 2^-24 relative — fp32 rounding size.  Measured on
+// MI355X (tools/split_probe.hip, K = 256, forward- and backward-like data, error / sum_k |a_k b_k| against fp64):
+// max 5.71 / mean 0.347 x 2^-24 for this scheme against 5.78 / 0.307 for the 16x16x4 fp32 MFMA and for a sequential
+// fp32 fmaf chain (the two are bitwise equal) — the same accuracy as the fp32 path, at six `v_mfma_f32_32x32x16_bf16`
+// (16 cycles per 16K MACs each) instead of sixteen `v_mfma_f32_16x16x4_f32` (8 cycles per 1K MACs each): 2.7x the
+// MAC rate of the fp32 matrix cores, which moves the 256x256 trunk layers from MFMA-bound to HBM-bound.
+//
+//   gemm_nt_x6     C[m][n] = epi( sum_k A[m][k] B[n][k] ): A fp32 activations (split while staged into LDS), B the
+//                  layer weights (forward) or their transpose (input gradient) as three pre-split bf16 planes
+//   gemm_wgrad_x6  P[s][n][k] = sum_{m in split s} G[m][n] X[m][k] (+ bias column sums): both operands fp32
+//                  activations, split while staged; fp32 slabs, deterministic reduce as in gemm.hpp
+// Fragment / LDS conventions are gemm_bf16.hpp's (NT: [rows][BK] tiles, ds_read_b128 per fragment, C^T so a lane
+// owns one output row; wgrad: row-major [m][cols] tiles read with ds_read_b64_tr_b16), one image per piece plane.
+#pragma once
+#include "gemm_bf16.hpp"
+
+// four fp32 values -> their hi / mid / lo bf16 pieces, packed in pairs (v_cvt_pk_bf16_f32 rounds to nearest even)
+__device__ __forceinline__ void x6_split4(const float4 v, uint2& h, uint2& m, uint2& l) {
+#ifdef NERF_X6_NOSPLIT  // ablation builds only: split cost probe (wrong results)
+  h = m = l = make_uint2(__float_as_uint(v.x), __float_as_uint(v.y));
+  return;
+#endif
+  const uint32_t h0 = nerf_pack_bf16x2(v.x, v.y), h1 = nerf_pack_bf16x2(v.z, v.w);
+  const float r0 = v.x - nerf_bf16_lo(h0), r1 = v.y - nerf_bf16_hi(h0);
+  const float r2 = v.z - nerf_bf16_lo(h1), r3 = v.w - nerf_bf16_hi(h1);
+  const uint32_t m0 = nerf_pack_bf16x2(r0, r1), m1 = nerf_pack_bf16x2(r2, r3);
+  const uint32_t l0 = nerf_pack_bf16x2(r0 - nerf_bf16_lo(m0), r1 - nerf_bf16_hi(m0));
+  const uint32_t l1 = nerf_pack_bf16x2(r2 - nerf_bf16_lo(m1), r3 - nerf_bf16_hi(m1));
+  h = make_uint2(h0, h1);
+  m = make_uint2(m0, m1);
+  l = make_uint2(l0, l1);
+}
+
+// the six piece products, smallest first: term t multiplies A piece X6_PA[t] by B piece X6_PB[t] (0 = hi, 1 = mid,
+// 2 = lo).  One term is issued for every accumulator of the wave before the next term, so consecutive MFMAs never
+// chain on one accumulator (a dependent 32x32x16 MFMA waits for its predecessor's result).
+__device__ constexpr int X6_PA[6] = {2, 1, 0, 1, 0, 0};
+__device__ constexpr int X6_PB[6] = {0, 1, 2, 0, 1, 0};
+// acc_[TM_][TN_] += over the six terms; MFMA(first_, second_) operands: NT passes (B fragment, A fragment) so the
+// accumulator is C^T (gemm_bf16.hpp); the weight gradient passes (G^T fragment, X fragment)
+#ifndef NERF_X6_TERMS  // ablation builds only (tools/build_exp.sh): fewer terms -> wrong results, MFMA cost probe
+#define NERF_X6_TERMS 6
+#endif
+#define X6_MFMA_BLOCK(acc_, TM_, TN_, FIRST_, SECOND_)                                                      \
+  _Pragma("unroll") for (int t_ = 6 - NERF_X6_TERMS; t_ < 6; ++t_)                                        \
+    _Pragma("unroll") for (int a_ = 0; a_ < TM_; ++a_)                                                    \
+      _Pragma("unroll") for (int b_ = 0; b_ < TN_; ++b_)                                                  \
+        acc_[a_][b_] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(FIRST_, SECOND_, acc_[a_][b_], 0, 0, 0);
+
+// ------------------------------------------------------------------------------------------ weight planes
+// dst plane p (p = hi, mid, lo) of job j: [rows_out][cols_out] bf16 at dst + p * plane, where for a plain job
+// rows_out x cols_out = rows x cols of src (row pitch lds) and for a transposed job dst[c][r] = src[r][c]
+struct X6Job {
+  const float* src;
+  nerf_bf16* dst;
+  int rows, cols, lds, transpose;
+  int64_t plane;
+};
+struct X6Jobs {
+  X6Job j[16];
+};
+static __global__ void x6_planes_kernel(X6Jobs jobs) {
+  const X6Job J = jobs.j[blockIdx.z];
+  __shared__ float tile[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  if (r0 >= J.rows || c0 >= J.cols) return;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int y = ty; y < 32; y += 8) {
+    const int r = r0 + y, c = c0 + tx;
+    tile[y][tx] = (r < J.rows && c < J.cols) ? J.src[(int64_t)r * J.lds + c] : 0.f;
+  }
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) {
+    // plain: element (r0 + y, c0 + tx); transposed: element (r0 + tx, c0 + y) written to row c0 + y
+    const float v = J.transpose ? tile[tx][y] : tile[y][tx];
+    const int orow = J.transpose ? c0 + y : r0 + y, ocol = J.transpose ? r0 + tx : c0 + tx;
+    const int orows = J.transpose ? J.cols : J.rows, ocols = J.transpose ? J.rows : J.cols;
+    if (orow < orows && ocol < ocols) {
+      const nerf_bf16 h = (nerf_bf16)v;
+      const float r1 = v - (float)h;
+      const nerf_bf16 m = (nerf_bf16)r1;
+      const nerf_bf16 l = (nerf_bf16)(r1 - (float)m);
+      const int64_t o = (int64_t)orow * ocols + ocol;
+      J.dst[o] = h;
+      J.dst[J.plane + o] = m;
+      J.dst[2 * J.plane + o] = l;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ gemm_nt_x6
+// 128 x 128 output tile per 256-thread workgroup (four 64 x 64 wave tiles of 2 x 2 MFMA tiles), BK = 32 (two MFMA
+// k-steps per slab).  The activation operand goes HBM -> registers in fragment layout (lane (r, h) of row block a:
+// row r, k = 8 h .. 8 h + 7 of each 16-k step = two float4) and is split there, so only the pre-split weight planes
+// pass through LDS: a first version that staged all six piece images through LDS ran at MFMA busy 0.31 with the LDS
+// pipe as busy as the matrix cores (12 ds_read_b128 + 9 ds_write per 24 MFMAs, PMC 4e7 bank-conflict cycles per
+// launch).  Weight planes: [3][128][40] bf16 per stage (80-B pitch: 16 consecutive rows hit 16 distinct 16-B bank
+// slots), double-buffered, 60 KiB per workgroup -> two workgroups per CU.  The activation loads of slab k + 2 are
+// issued as slab k's registers are consumed (two register sets); the weight slab k + 1 (L2-resident) is staged in
+// registers during slab k and written to LDS after it (one barrier per slab).
+// B: three planes of [N][ldb] bf16, plane stride bplane.  Requirements (host): M % 128 == 0, N % 128 == 0,
+// K % 32 == 0, lda % 4 == 0, ldb % 8 == 0.
+template <int EPI, int BK = 32, int MINW = 2>
+__global__ __launch_bounds__(256, MINW) void gemm_nt_x6_kernel(const float* __restrict__ A, int lda,
+                                                              const nerf_bf16* __restrict__ Bp, int ldb, int64_t bplane,
+                                                              const float* __restrict__ bias, float* __restrict__ C,
+                                                              int ldc, const uint32_t* __restrict__ mbits, int ldmb,
+                                                              uint32_t* __restrict__ mbits_out, int K, int n_ntiles) {
+  constexpr int BM = 128, BN = 128, WTM = 64, WTN = 64, TM = 2, TN = 2;
+  constexpr int KS = BK / 16;   // MFMA k-steps per slab
+  constexpr int CPR = BK / 8;   // 16-B weight chunks per row per slab
+  static_assert(BK == 16 || BK == 32, "slab");
+  constexpr int LS = BK + 8;    // 48 / 80-B pitch: 16 consecutive rows hit 16 distinct 16-B bank slots
+  constexpr int PL = BN * LS;  // one weight piece image
+  __shared__ __attribute__((aligned(16))) nerf_bf16 smem[2 * 3 * PL];
+
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
+  const int64_t m0 = (int64_t)mt * BM;
+  const int n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  const nerf_bf16* Bb = Bp + (int64_t)n0 * ldb;
+  // this lane's activation rows (uniform tile base + 32-bit lane offsets)
+  const float* At = A + (m0 + wm * WTM) * lda;
+  int aoff[TM];
+#pragma unroll
+  for (int a = 0; a < TM; ++a) aoff[a] = (a * 32 + li) * lda + 8 * lh;
+
+  // register sets: ra[set][a][ks] = the 8 fp32 of row block a, k-step ks (two float4)
+  float4 ra[2][TM][KS][2];
+  uint4 rb[3][KS];  // weight slab: 3 planes x 128 rows x CPR chunks of 16 B (thread: chunks t + 256 i)
+#define X6_ALOAD(set_, k0_)                                                                                \
+  _Pragma("unroll") for (int a = 0; a < TM; ++a)                                                          \
+    _Pragma("unroll") for (int ks = 0; ks < KS; ++ks)                                                     \
+      _Pragma("unroll") for (int hf = 0; hf < 2; ++hf)                                                    \
+        ra[set_][a][ks][hf] = *reinterpret_cast<const float4*>(At + aoff[a] + (k0_) + 16 * ks + 4 * hf);
+#define X6_BLOAD(k0_)                                                                                      \
+  _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                           \
+    _Pragma("unroll") for (int i = 0; i < KS; ++i) {                                                      \
+      const int c = tid + 256 * i;                                                                        \
+      rb[p][i] = *reinterpret_cast<const uint4*>(Bb + p * bplane + (int64_t)(c / CPR) * ldb + (k0_) + 8 * (c % CPR)); \
+    }
+#define X6_BSTORE(buf_)                                                                                    \
+  _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                           \
+    _Pragma("unroll") for (int i = 0; i < KS; ++i) {                                                      \
+      const int c = tid + 256 * i;                                                                        \
+      *reinterpret_cast<uint4*>(smem + ((buf_) * 3 + p) * PL + (c / CPR) * LS + 8 * (c % CPR)) = rb[p][i]; \
+    }
+
+  nerf_f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int nk = K / BK;
+  X6_ALOAD(0, 0);
+  X6_ALOAD(1, (nk > 1 ? 1 : 0) * BK);
+  X6_BLOAD(0);
+  X6_BSTORE(0);
+  __syncthreads();
+  for (int kt0 = 0; kt0 < nk; kt0 += 2) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // slab kt = kt0 + j: LDS buffer j, activation register set j
+      const int kt = kt0 + j;
+      if (kt < nk) {
+        X6_BLOAD((kt + 1 < nk ? kt + 1 : kt) * BK);
+        const nerf_bf16* S = smem + j * 3 * PL;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          nerf_bf16x8 af[TM][3], bf[TN][3];
+#pragma unroll
+          for (int a = 0; a < TM; ++a) {
+            uint2 h0, m0_, l0, h1, m1, l1;
+            x6_split4(ra[j][a][ks][0], h0, m0_, l0);
+            x6_split4(ra[j][a][ks][1], h1, m1, l1);
+            af[a][0] = __builtin_bit_cast(nerf_bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+            af[a][1] = __builtin_bit_cast(nerf_bf16x8, make_uint4(m0_.x, m0_.y, m1.x, m1.y));
+            af[a][2] = __builtin_bit_cast(nerf_bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+          }
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+              bf[b][p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + (wn * WTN + b * 32 + li) * LS + 16 * ks +
+                                                               8 * lh);
+          X6_MFMA_BLOCK(acc, TM, TN, bf[b_][X6_PB[t_]], af[a_][X6_PA[t_]])
+        }
+        // set j is consumed: slab kt + 2 streams into it while slab kt + 1 is computed
+        X6_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);
+        X6_BSTORE(j ^ 1);
+        __syncthreads();
+      }
+    }
+  }
+#undef X6_ALOAD
+#undef X6_BLOAD
+#undef X6_BSTORE
+
+#ifdef NERF_X6_NOSTORE  // ablation builds only: the epilogue's cost (outputs left stale)
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) asm volatile("" ::"v"(acc[a][b]));
+#else
+  ntb_epilogue<TM, TN, WTM, WTN, EPI, 0>(acc, m0 + wm * WTM, n0 + wn * WTN, li, lh, bias, C, ldc, mbits, ldmb,
+                                         mbits_out);
+#endif
+}
+
+// ------------------------------------------------------------------------------------------ gemm_wgrad_x6
+// gemm_wgrad_bf16_kernel's tiling with fp32 operands split while staged: 16-row slabs (one MFMA k-step), per stage
+// three G piece images [16][PG] and three X images [16][PX] (pitch = 64 B mod 256 B for the transposing reads),
+// double-buffered: 60 KiB for 128 x 128 tiles -> two workgroups per CU.  Bias column sums (tiles of k-block 0) add
+// the three pieces of every G value, which sum to it exactly.  Requirements: rows_per_split % 16 == 0, M % 16 == 0,
+// ldg / ldx % 4 == 0.
+template <int BN, int BK, int WAVES_N>
+__global__ __launch_bounds__(256, 2) void gemm_wgrad_x6_kernel(const float* __restrict__ G, int ldg,
+                                                              const float* __restrict__ X, int ldx,
+                                                              float* __restrict__ P, int ldp, float* __restrict__ Pb,
+                                                              int64_t slab, int64_t rows_per_split, int64_t M,
+                                                              int n_ktiles, int n_tiles) {
+  constexpr int MR = 16;
+  constexpr int WAVES_K = 4 / WAVES_N;
+  constexpr int WTN = BN / WAVES_N, WTK = BK / WAVES_K;
+  constexpr int TM = WTN / 32, TN = WTK / 32;
+  static_assert(TM >= 1 && TN >= 1, "wave tile");
+  constexpr int PG = ((BN + 127) / 128) * 128 + 32, PX = ((BK + 127) / 128) * 128 + 32;
+  constexpr int IG = MR * PG, IX = MR * PX;       // one piece image
+  constexpr int STAGE = 3 * (IG + IX);
+  constexpr int G_F4 = MR * BN / 4, X_F4 = MR * BK / 4;
+  constexpr int G_PER = (G_F4 + 255) / 256, X_PER = (X_F4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) nerf_bf16 smem[2 * STAGE];
+
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int s = lin / n_tiles;
+  const int tile = lin - s * n_tiles;
+  const int nt = tile / n_ktiles, kt = tile - nt * n_ktiles;
+  const int n0 = nt * BN, k0 = kt * BK;
+  const int64_t r0 = (int64_t)s * rows_per_split;
+  int64_t r1 = r0 + rows_per_split;
+  if (r1 > M) r1 = M;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave / WAVES_K, wk = wave % WAVES_K;
+  const int li = lane & 31, lh = lane >> 5;
+  const bool do_bias = (Pb != nullptr) && kt == 0 && wk == 0;
+
+  constexpr int PF = 4;  // register sets in flight, as in gemm_nt_x6_kernel
+  float4 rg[PF][G_PER], rx[PF][X_PER];
+#define WX6_GLOAD(set_, m_)                                                                                \
+  {                                                                                                        \
+    _Pragma("unroll") for (int i = 0; i < G_PER; ++i) {                                                    \
+      const int f = tid + 256 * i;                                                                         \
+      if (G_F4 % 256 == 0 || f < G_F4)                                                                     \
+        rg[set_][i] = *reinterpret_cast<const float4*>(G + ((m_) + f / (BN / 4)) * ldg + n0 + (f % (BN / 4)) * 4); \
+    }                                                                                                      \
+    _Pragma("unroll") for (int i = 0; i < X_PER; ++i) {                                                    \
+      const int f = tid + 256 * i;                                                                         \
+      if (X_F4 % 256 == 0 || f < X_F4)                                                                     \
+        rx[set_][i] = *reinterpret_cast<const float4*>(X + ((m_) + f / (BK / 4)) * ldx + k0 + (f % (BK / 4)) * 4); \
+    }                                                                                                      \
+  }
+#define WX6_SSTORE(set_, buf_)                                                                             \
+  {                                                                                                        \
+    nerf_bf16* Gs_ = smem + (buf_) * STAGE;                                                                \
+    nerf_bf16* Xs_ = Gs_ + 3 * IG;                                                                         \
+    _Pragma("unroll") for (int i = 0; i < G_PER; ++i) {                                                    \
+      const int f = tid + 256 * i;                                                                         \
+      if (G_F4 % 256 == 0 || f < G_F4) {                                                                   \
+        uint2 h, m, l;                                                                                     \
+        x6_split4(rg[set_][i], h, m, l);                                                                   \
+        const int o = (f / (BN / 4)) * PG + (f % (BN / 4)) * 4;                                            \
+        *reinterpret_cast<uint2*>(Gs_ + o) = h;                                                            \
+        *reinterpret_cast<uint2*>(Gs_ + IG + o) = m;                                                       \
+        *reinterpret_cast<uint2*>(Gs_ + 2 * IG + o) = l;                                                   \
+      }                                                                                                    \
+    }                                                                                                      \
+    _Pragma("unroll") for (int i = 0; i < X_PER; ++i) {                                                    \
+      const int f = tid + 256 * i;                                                                         \
+      if (X_F4 % 256 == 0 || f < X_F4) {                                                                   \
+        uint2 h, m, l;                                                                                     \
+        x6_split4(rx[set_][i], h, m, l);                                                                   \
+        const int o = (f / (BK / 4)) * PX + (f % (BK / 4)) * 4;                                            \
+        *reinterpret_cast<uint2*>(Xs_ + o) = h;                                                            \
+        *reinterpret_cast<uint2*>(Xs_ + IX + o) = m;                                                       \
+        *reinterpret_cast<uint2*>(Xs_ + 2 * IX + o) = l;                                                   \
+      }                                                                                                    \
+    }                                                                                                      \
+  }
+
+  nerf_f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  float bsum[TM];
+#pragma unroll
+  for (int a = 0; a < TM; ++a) bsum[a] = 0.f;
+
+  // transposing-read addressing (gemm_bf16.hpp): lane 4q + p of 16-lane group g reads row 8 (g >> 1) + 4 t + q,
+  // columns 16 (g & 1) + 4 p .. + 3; lane i of the group receives column 16 (g & 1) + i
+  const int grp = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+  const int trow = 8 * (grp >> 1) + q, tcol = 16 * (grp & 1) + 4 * p4;
+  auto tr_frag = [&](const nerf_bf16* base, int pitch) {
+    const nerf_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) nerf_s16x4*)(base));
+    const nerf_s16x4 hi =
+        __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) nerf_s16x4*)(base + 4 * pitch));
+    const short v8 __attribute__((ext_vector_type(8))) = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(nerf_bf16x8, v8);
+  };
+
+  const int64_t nit = (r1 - r0) / MR;
+  if (nit > 0) {
+#pragma unroll
+    for (int j = 0; j < PF; ++j) WX6_GLOAD(j, r0 + (j < nit ? j : nit - 1) * MR);
+    WX6_SSTORE(0, 0);
+  }
+  __syncthreads();
+  for (int64_t it0 = 0; it0 < nit; it0 += PF) {
+#pragma unroll
+   for (int j = 0; j < PF; ++j) {  // slab it = it0 + j: LDS buffer j & 1, register set j
+    const int64_t it = it0 + j;
+    if (it >= nit) break;
+    WX6_GLOAD(j, r0 + (it + PF < nit ? it + PF : nit - 1) * MR);
+    const nerf_bf16* Gs = smem + (j & 1) * STAGE;
+    const nerf_bf16* Xs = Gs + 3 * IG;
+    nerf_bf16x8 af[TM][3], bf[TN][3];
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a) af[a][pc] = tr_frag(Gs + pc * IG + trow * PG + wn * WTN + a * 32 + tcol, PG);
+#pragma unroll
+      for (int b = 0; b < TN; ++b) bf[b][pc] = tr_frag(Xs + pc * IX + trow * PX + wk * WTK + b * 32 + tcol, PX);
+    }
+    if (do_bias) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsum[a] += ((float)af[a][0][j] + (float)af[a][1][j]) + (float)af[a][2][j];
+    }
+    // A = G^T (rows n, piece X6_PA), B = X (columns k, piece X6_PB); P itself is accumulated (not transposed)
+    X6_MFMA_BLOCK(acc, TM, TN, af[a_][X6_PA[t_]], bf[b_][X6_PB[t_]])
+    if (it + 1 < nit) WX6_SSTORE((j + 1) % PF, (j + 1) & 1);
+    __syncthreads();
+   }
+  }
+#undef WX6_GLOAD
+#undef WX6_SSTORE
+
+  float* Ps = P + (int64_t)s * slab;
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int k = k0 + wk * WTK + b * 32 + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + wn * WTN + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        Ps[(int64_t)n * ldp + k] = acc[a][b][r];
+      }
+    }
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const float v = bsum[a] + __shfl_xor(bsum[a], 32, 64);
+      if (lh == 0) Pb[(int64_t)s * slab + n0 + wn * WTN + a * 32 + li] = v;
+    }
+  }
+}

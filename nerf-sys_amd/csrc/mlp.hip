@@ -15,6 +15,7 @@
 //   C0 [Mp][128], O3 [Mp][32].  Backward adds dA/dB [Mp][256], dO16 [Mp][32] (from the fused colour-branch
 //   backward), transposed trunk / head weights, and S split-M partial slabs of the packed gradient.
 #include "gemm.hpp"
+#include "gemm_x6.hpp"
 #include "mlp_common.hpp"
 #include "mlp_tail.hpp"
 #include "mlp_fwd_tail.hpp"
@@ -29,12 +30,21 @@ struct WS {
   // backward
   float *dA, *dB, *dO16, *WT, *partial, *partial2;
   float* dZ[8];  // two-stream backward (training == 2): one input-gradient buffer per trunk layer (dZ_i of trunk.i)
+  nerf_bf16* WPf;  // bf16 piece planes of the trunk weights (split GEMMs): layer i at x6_fwd_off(i), [3][256][KPAD_i]
+  nerf_bf16* WPb;  // ... of the transposed trunk weights (input gradients): layer i >= 1 at 3 * 65536 * (i - 1)
   int S;
   int64_t rps;
   int64_t bytes;
 };
 
 constexpr int64_t WT_FLOATS = 7 * 65536 + 256 * 32;
+// bf16 piece planes (gemm_x6.hpp): forward 3 x 256 x sum(KPAD) bf16, input gradient 7 x 3 x 256 x 256 bf16
+inline int64_t x6_fwd_off(int i) {
+  int64_t o = 0;
+  for (int j = 0; j < i; ++j) o += 3 * 256 * (int64_t)KPAD[j];
+  return o;
+}
+constexpr int64_t X6_BWD_BF16 = 7 * 3 * 65536;
 // the head backward (dZ7, head weight / bias sums) is one pass (head_bwd_kernel) unless NERF_BWD_TAIL_CHAIN keeps the
 // separate head dgrad / wgrad GEMMs for A/B runs; the second-half sums of the split walks start at P2BASE
 #ifndef NERF_BWD_TAIL_CHAIN
@@ -54,6 +64,7 @@ WS carve(void* base, int64_t M, int training) {
     return q;
   };
   w.X3E = take(Mp * 320);
+  w.WPf = reinterpret_cast<nerf_bf16*>(take(x6_fwd_off(8) / 2));
   if (training) {
     for (int i = 0; i < 8; ++i) w.Y[i] = (i == 3) ? w.X3E : take(Mp * 256);
   } else {
@@ -76,6 +87,7 @@ WS carve(void* base, int64_t M, int training) {
     }
     w.dO16 = take(Mp * 32);  // [Mp][16] for the fused head backward, [Mp][32] for the chain
     w.WT = take(WT_FLOATS);
+    w.WPb = reinterpret_cast<nerf_bf16*>(take(X6_BWD_BF16 / 2));
     w.S = n_splits(Mp);
     w.rps = round_up(nerf_cdiv(Mp, w.S), 64);  // whole slabs for every wgrad MR
     w.partial = take((int64_t)w.S * layout().total);
@@ -270,6 +282,49 @@ int wgrad(const float* G, int ldg, const float* X, int ldx, int tensor_w, const 
   return NERF_OK;
 }
 
+// split-product (bf16 x 6) forms of the trunk GEMMs (gemm_x6.hpp)
+template <int EPI>
+int nt_x6(const float* A, int lda, const nerf_bf16* Bp, int ldb, int64_t bplane, const float* bias, float* C, int ldc,
+          const uint32_t* mbits, uint32_t* mbits_out, int64_t M, int N, int K, hipStream_t st) {
+  if (M % 128 || N % 128 || K % 32 || lda % 4 || ldb % 8) return NERF_E_ARG;
+  const int ntn = N / 128;
+#ifndef NERF_X6_NT_BK  // ablation / tuning builds: slab depth and workgroups per CU of the split NT GEMM
+#define NERF_X6_NT_BK 32
+#define NERF_X6_NT_MINW 2
+#endif
+  gemm_nt_x6_kernel<EPI, NERF_X6_NT_BK, NERF_X6_NT_MINW><<<(unsigned)((M / 128) * ntn), 256, 0, st>>>(A, lda, Bp, ldb, bplane, bias, C, ldc, mbits,
+                                                                      N / 32, mbits_out, K, ntn);
+  return NERF_OK;
+}
+
+// trunk weight gradient, N = 256: 128 x 128 tiles over the first 256 input columns, 128 x 64 tiles over K = 64
+// (trunk.0) and the K = 320 remainder of trunk.4 (its encoding columns)
+int wgrad_x6(const float* G, int ldg, const float* X, int ldx, int tensor_w, const WS& w, int N, int K, hipStream_t st) {
+  const Layout& L = layout();
+  float* P = w.partial + L.off[tensor_w];
+  float* Pb = w.partial + L.off[tensor_w + 1];
+  const int ldp = L.cols[tensor_w];
+  const int64_t slab = L.total;
+  if (N != 256 || ldg % 4 || ldx % 4) return NERF_E_ARG;
+  auto t128 = [&](const float* Xk, float* Pk, float* Pbk) {
+    gemm_wgrad_x6_kernel<128, 128, 2><<<4 * w.S, 256, 0, st>>>(G, ldg, Xk, ldx, Pk, ldp, Pbk, slab, w.rps, w.Mp, 2, 4);
+  };
+  auto t64 = [&](const float* Xk, float* Pk, float* Pbk) {
+    gemm_wgrad_x6_kernel<128, 64, 4><<<2 * w.S, 256, 0, st>>>(G, ldg, Xk, ldx, Pk, ldp, Pbk, slab, w.rps, w.Mp, 1, 2);
+  };
+  if (K == 64) {
+    t64(X, P, Pb);
+  } else if (K == 256) {
+    t128(X, P, Pb);
+  } else if (K == 320) {
+    t128(X, P, Pb);
+    t64(X + 256, P + 256, nullptr);
+  } else {
+    return NERF_E_ARG;
+  }
+  return NERF_OK;
+}
+
 }  // namespace
 
 extern "C" int64_t nerf_mlp_layout(int64_t* table) {
@@ -290,9 +345,11 @@ extern "C" int64_t nerf_mlp_workspace_bytes(int64_t M, int training) {
   return carve(nullptr, M, training).bytes + 256;
 }
 
-extern "C" int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws, int64_t ws_bytes,
-                            int training, hipEvent_t* ev, hipStream_t st) {
+extern "C" int nerf_mlp_fwd_ex(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws,
+                               int64_t ws_bytes, int training, int flags, hipEvent_t* ev, hipStream_t st) {
   NERF_CHECK_ARG(w && x_d && rgb_sigma && ws && M >= 0);
+  if (flags & ~NERF_MLP_NATIVE_FP32) return NERF_E_ENUM;
+  const bool native = flags & NERF_MLP_NATIVE_FP32;
   if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(rgb_sigma)) return NERF_E_ALIGN;
   const WS W = carve(ws, M, training);
   if (ws_bytes < W.bytes) return NERF_E_WORKSPACE;
@@ -302,6 +359,12 @@ extern "C" int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* 
   auto Wt = [&](int t) { return w + L.off[t]; };
 
   pe_xyz_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(x_d, M, Mp, W.X3E);
+  if (!native) {  // this call's weights as bf16 piece planes
+    X6Jobs jobs{};
+    for (int i = 0; i < 8; ++i)
+      jobs.j[i] = X6Job{Wt(2 * i), W.WPf + x6_fwd_off(i), 256, KPAD[i], KPAD[i], 0, 256 * (int64_t)KPAD[i]};
+    x6_planes_kernel<<<dim3(10, 8, 8), 256, 0, st>>>(jobs);
+  }
   // trunk
   const float* in = W.X3E + 256;
   int ld_in = 320;
@@ -310,8 +373,12 @@ extern "C" int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* 
     const int ld_out = training ? ld_of(W, i) : ((i % 2 == 0) ? 256 : 320);
     if (i == 4) { in = W.X3E; ld_in = 320; }  // cat([h3, enc]) lives in X3E
     if (ev) (void)hipEventRecord(ev[2 * i], st);
-    TRY(nt<EPI_BIAS_RELU>(in, ld_in, Wt(2 * i), KPAD[i], Wt(2 * i + 1), out, ld_out, nullptr,
-                          training ? W.MB[i] : nullptr, Mp, 256, KPAD[i], st));
+    if (native)
+      TRY(nt<EPI_BIAS_RELU>(in, ld_in, Wt(2 * i), KPAD[i], Wt(2 * i + 1), out, ld_out, nullptr,
+                            training ? W.MB[i] : nullptr, Mp, 256, KPAD[i], st));
+    else
+      TRY(nt_x6<EPI_BIAS_RELU>(in, ld_in, W.WPf + x6_fwd_off(i), KPAD[i], 256 * (int64_t)KPAD[i], Wt(2 * i + 1), out,
+                               ld_out, nullptr, training ? W.MB[i] : nullptr, Mp, 256, KPAD[i], st));
     if (ev) (void)hipEventRecord(ev[2 * i + 1], st);
     in = out;
     ld_in = ld_out;
@@ -350,6 +417,11 @@ extern "C" int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* 
   return nerf_launch_status();
 }
 
+extern "C" int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws, int64_t ws_bytes,
+                            int training, hipEvent_t* ev, hipStream_t st) {
+  return nerf_mlp_fwd_ex(w, x_d, M, rgb_sigma, ws, ws_bytes, training, 0, ev, st);
+}
+
 extern "C" int64_t nerf_mlp_workspace_bytes_2s(int64_t M) {
   if (M < 0) return -1;
   return carve(nullptr, M, 2).bytes + 256;
@@ -362,9 +434,11 @@ namespace {
 // waits for stw (sync[9]) before the split reduce; sync[0] is unused.  The same kernels, grids and slabs: bitwise the
 // one-stream result.
 int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
-                 int64_t ws_bytes, hipEvent_t* ev, hipStream_t st, hipStream_t stw, hipEvent_t* sync) {
+                 int64_t ws_bytes, int flags, hipEvent_t* ev, hipStream_t st, hipStream_t stw, hipEvent_t* sync) {
   NERF_CHECK_ARG(w && d_rgb_sigma && d_w && ws && M >= 0);
   NERF_CHECK_ARG(!stw || sync);
+  if (flags & ~NERF_MLP_NATIVE_FP32) return NERF_E_ENUM;
+  const bool native = flags & NERF_MLP_NATIVE_FP32;
   if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(d_w) || !nerf_aligned16(d_rgb_sigma))
     return NERF_E_ALIGN;
   const bool two = stw != nullptr;
@@ -385,20 +459,27 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
   const int64_t Mp = W.Mp;
   auto Wt = [&](int t) { return w + L.off[t]; };
 
-  // transposed weights for the dgrad GEMMs
+  // transposed weights for the dgrad GEMMs: fp32 (native) or bf16 piece planes (split products)
   float* T = W.WT;
   float* WTi[8] = {nullptr};
   TJobs jobs{};
   int nj = 0;
-  for (int i = 1; i < 8; ++i) {
-    WTi[i] = T;
-    jobs.j[nj++] = TJob{Wt(2 * i), T, 256, 256, KPAD[i]};  // first 256 input cols (h part for trunk.4)
-    T += 65536;
+  if (native) {
+    for (int i = 1; i < 8; ++i) {
+      WTi[i] = T;
+      jobs.j[nj++] = TJob{Wt(2 * i), T, 256, 256, KPAD[i]};  // first 256 input cols (h part for trunk.4)
+      T += 65536;
+    }
+  } else {
+    X6Jobs xj{};
+    for (int i = 1; i < 8; ++i)
+      xj.j[i - 1] = X6Job{Wt(2 * i), W.WPb + 3 * 65536 * (int64_t)(i - 1), 256, 256, KPAD[i], 1, 65536};
+    x6_planes_kernel<<<dim3(8, 8, 7), 256, 0, st>>>(xj);
   }
 #ifdef NERF_BWD_TAIL_CHAIN
-  float* Wht = T;  jobs.j[nj++] = TJob{Wt(16), Wht, 32, 256, 256};  // [256][32]
+  float* Wht = W.WT + 7 * 65536;  jobs.j[nj++] = TJob{Wt(16), Wht, 32, 256, 256};  // [256][32]
 #endif
-  transpose_kernel<<<dim3(8, 8, nj), 256, 0, st>>>(jobs);
+  if (nj) transpose_kernel<<<dim3(8, 8, nj), 256, 0, st>>>(jobs);
 
   // colour branch + head activations in one kernel: dO16 and the colour weight / bias slabs (two workgroups per
   // split; the second halves' colour sums go to W.partial2 and are added by the final reduce)
@@ -432,12 +513,19 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
     const int ldx = (i == 0 || i == 4) ? 320 : ld_of(W, i - 1);
     if (two && i < 7) TRY(handoff(8 - i));  // dZ_i, written by the trunk.(i+1) dgrad: sync[8 - i]
     if (ev) (void)hipEventRecord(ev[4 * i], sw);
-    TRY(wgrad(dcur, 256, X, ldx, 2 * i, W, 256, KPAD[i], sw));
+    if (native)
+      TRY(wgrad(dcur, 256, X, ldx, 2 * i, W, 256, KPAD[i], sw));
+    else
+      TRY(wgrad_x6(dcur, 256, X, ldx, 2 * i, W, 256, KPAD[i], sw));
     if (ev) (void)hipEventRecord(ev[4 * i + 1], sw);
     if (i > 0) {
       if (two) dnext = W.dZ[i - 1];  // never the buffer a trailing weight gradient still reads
       if (ev) (void)hipEventRecord(ev[4 * i + 2], st);
-      TRY(nt<EPI_MASK>(dcur, 256, WTi[i], 256, nullptr, dnext, 256, W.MB[i - 1], nullptr, Mp, 256, 256, st));
+      if (native)
+        TRY(nt<EPI_MASK>(dcur, 256, WTi[i], 256, nullptr, dnext, 256, W.MB[i - 1], nullptr, Mp, 256, 256, st));
+      else
+        TRY(nt_x6<EPI_MASK>(dcur, 256, W.WPb + 3 * 65536 * (int64_t)(i - 1), 256, 65536, nullptr, dnext, 256,
+                            W.MB[i - 1], nullptr, Mp, 256, 256, st));
       if (ev) (void)hipEventRecord(ev[4 * i + 3], st);
       float* t = dcur; dcur = dnext; dnext = t;
     }
@@ -453,14 +541,25 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
 }
 }  // namespace
 
+extern "C" int nerf_mlp_bwd_ex(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate,
+                               void* ws, int64_t ws_bytes, int flags, hipEvent_t* ev, hipStream_t st) {
+  return mlp_bwd_impl(w, M, d_rgb_sigma, d_w, accumulate, ws, ws_bytes, flags, ev, st, nullptr, nullptr);
+}
+
 extern "C" int nerf_mlp_bwd(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
                             int64_t ws_bytes, hipEvent_t* ev, hipStream_t st) {
-  return mlp_bwd_impl(w, M, d_rgb_sigma, d_w, accumulate, ws, ws_bytes, ev, st, nullptr, nullptr);
+  return mlp_bwd_impl(w, M, d_rgb_sigma, d_w, accumulate, ws, ws_bytes, 0, ev, st, nullptr, nullptr);
+}
+
+extern "C" int nerf_mlp_bwd_2s_ex(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate,
+                                  void* ws, int64_t ws_bytes, int flags, hipEvent_t* ev, hipStream_t st,
+                                  hipStream_t wgrad_stream, hipEvent_t* sync) {
+  NERF_CHECK_ARG(wgrad_stream && sync && wgrad_stream != st);
+  return mlp_bwd_impl(w, M, d_rgb_sigma, d_w, accumulate, ws, ws_bytes, flags, ev, st, wgrad_stream, sync);
 }
 
 extern "C" int nerf_mlp_bwd_2s(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
                                int64_t ws_bytes, hipEvent_t* ev, hipStream_t st, hipStream_t wgrad_stream,
                                hipEvent_t* sync) {
-  NERF_CHECK_ARG(wgrad_stream && sync && wgrad_stream != st);
-  return mlp_bwd_impl(w, M, d_rgb_sigma, d_w, accumulate, ws, ws_bytes, ev, st, wgrad_stream, sync);
+  return nerf_mlp_bwd_2s_ex(w, M, d_rgb_sigma, d_w, accumulate, ws, ws_bytes, 0, ev, st, wgrad_stream, sync);
 }

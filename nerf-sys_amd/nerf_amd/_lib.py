@@ -43,6 +43,9 @@ def lib():
             "nerf_mlp_bwd": [P, I64, P, P, I, P, I64, P, P],
             "nerf_mlp_workspace_bytes_2s": [I64],
             "nerf_mlp_bwd_2s": [P, I64, P, P, I, P, I64, P, P, P, P],
+            "nerf_mlp_fwd_ex": [P, P, I64, P, P, I64, I, I, P, P],
+            "nerf_mlp_bwd_ex": [P, I64, P, P, I, P, I64, I, P, P],
+            "nerf_mlp_bwd_2s_ex": [P, I64, P, P, I, P, I64, I, P, P, P, P],
             "nerf_mlp_workspace_bytes_bf16": [I64, I],
             "nerf_mlp_fwd_bf16": [P, P, I64, P, P, I64, I, I, P, P],
             "nerf_mlp_bwd_bf16": [P, I64, P, P, I, P, I64, I, P, P],
@@ -127,7 +130,7 @@ def lib():
 EXPORTS = ("nerf_rays_gen", "nerf_pick_pixels", "nerf_clamp_near_far", "nerf_rays_ndc",
            "nerf_sample_stratified", "nerf_build_xd", "nerf_sample_pdf", "nerf_freq_encode",
            "nerf_mlp_layout", "nerf_mlp_workspace_bytes", "nerf_mlp_fwd", "nerf_mlp_bwd",
-           "nerf_mlp_workspace_bytes_2s", "nerf_mlp_bwd_2s",
+           "nerf_mlp_workspace_bytes_2s", "nerf_mlp_bwd_2s", "nerf_mlp_fwd_ex", "nerf_mlp_bwd_ex", "nerf_mlp_bwd_2s_ex",
            "nerf_mlp_workspace_bytes_bf16", "nerf_mlp_fwd_bf16", "nerf_mlp_bwd_bf16",
            "nerf_composite_fwd", "nerf_composite_bwd", "nerf_grad_sqnorm", "nerf_adam", "nerf_version",
            "nerf_hash_encode", "nerf_hash_encode_bwd", "nerf_sh_encode", "nerf_ngp_layout",

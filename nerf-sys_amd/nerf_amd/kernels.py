@@ -148,7 +148,11 @@ def _events_arg(events):
     return arr
 
 
-def mlp_fwd(w_packed, x_d, ws, training, out=None, events=None, precision="fp32", bf16_flags=0):
+# fp32 GEMM engine flags (include/nerf_amd.h): 0 = bf16 split products (default), NATIVE_FP32 = fp32 MFMA kernels
+MLP_NATIVE_FP32 = 1
+
+
+def mlp_fwd(w_packed, x_d, ws, training, out=None, events=None, precision="fp32", bf16_flags=0, fp32_flags=0):
     need(w_packed, "packed weights"), need(x_d, "x_d")
     _check_precision(precision)
     M = x_d.shape[0]
@@ -158,13 +162,13 @@ def mlp_fwd(w_packed, x_d, ws, training, out=None, events=None, precision="fp32"
         check(lib().nerf_mlp_fwd_bf16(ptr(w_packed), ptr(x_d), M, ptr(out), ptr(ws), ws.numel(), int(training),
                                       int(bf16_flags), _events_arg(events), stream()), "nerf_mlp_fwd_bf16")
         return out
-    check(lib().nerf_mlp_fwd(ptr(w_packed), ptr(x_d), M, ptr(out), ptr(ws), ws.numel(), int(training),
-                             _events_arg(events), stream()), "nerf_mlp_fwd")
+    check(lib().nerf_mlp_fwd_ex(ptr(w_packed), ptr(x_d), M, ptr(out), ptr(ws), ws.numel(), int(training),
+                                int(fp32_flags), _events_arg(events), stream()), "nerf_mlp_fwd_ex")
     return out
 
 
 def mlp_bwd(w_packed, M, d_rgb_sigma, ws, d_w=None, accumulate=False, events=None, precision="fp32", bf16_flags=0,
-            wgrad_stream=None, sync=None):
+            wgrad_stream=None, sync=None, fp32_flags=0):
     """wgrad_stream (fp32 only): run the weight-gradient GEMMs there (nerf_mlp_bwd_2s; sync = 10 torch.cuda.Events,
     ws from mlp_workspace_bytes_2s); d_w is complete in the current stream's order either way."""
     need(w_packed, "packed weights"), need(d_rgb_sigma, "d_rgb_sigma")
@@ -182,12 +186,13 @@ def mlp_bwd(w_packed, M, d_rgb_sigma, ws, d_w=None, accumulate=False, events=Non
         for e in sync:  # torch creates an event's HIP handle at its first record
             if not e.cuda_event:
                 e.record()
-        check(lib().nerf_mlp_bwd_2s(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws), ws.numel(),
-                                    _events_arg(events), stream(), ctypes.c_void_p(wgrad_stream.cuda_stream),
-                                    _events_arg(sync)), "nerf_mlp_bwd_2s")
+        check(lib().nerf_mlp_bwd_2s_ex(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws),
+                                       ws.numel(), int(fp32_flags), _events_arg(events), stream(),
+                                       ctypes.c_void_p(wgrad_stream.cuda_stream), _events_arg(sync)),
+              "nerf_mlp_bwd_2s_ex")
         return d_w
-    check(lib().nerf_mlp_bwd(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws), ws.numel(),
-                             _events_arg(events), stream()), "nerf_mlp_bwd")
+    check(lib().nerf_mlp_bwd_ex(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws), ws.numel(),
+                                int(fp32_flags), _events_arg(events), stream()), "nerf_mlp_bwd_ex")
     return d_w
 
 

@@ -60,7 +60,8 @@ class NeRFTrainer:
                  eps: float = 1e-8, weight_decay: float = 0.0, grad_clip: Optional[float] = 1.0,
                  color_space: str = "linear", bg: str = "white", sigma_scale: float = 1.0,
                  world_size: int = 1, device="cuda", overlap: bool = True, precision: str = "fp32",
-                 overlap_with: str = "fwd", bf16_flags: int = 0, split_wgrad: bool = False):
+                 overlap_with: str = "fwd", bf16_flags: int = 0, split_wgrad: bool = False,
+                 fp32_gemm: str = "split"):
         L = PackedLayout.get()
         self.L = L
         self.P = L.total
@@ -87,6 +88,11 @@ class NeRFTrainer:
             raise ValueError(f"precision must be one of {K.PRECISIONS}")
         self.precision = precision  # MLP GEMMs: fp32 (configs[1]) or bf16 (configs[2]); compositing stays fp32
         self.bf16_flags = int(bf16_flags)  # K.BF16_LAYERED_* (A/B runs of the layered bf16 launches)
+        # fp32 trunk GEMMs: "split" = bf16 piece products at fp32 accuracy (default), "native" = fp32 MFMA kernels
+        if fp32_gemm not in ("split", "native"):
+            raise ValueError(f"fp32_gemm must be 'split' or 'native', got {fp32_gemm!r}")
+        self.fp32_gemm = fp32_gemm
+        self.fp32_flags = K.MLP_NATIVE_FP32 if fp32_gemm == "native" else 0
         self.betas, self.eps, self.wd = betas, eps, weight_decay
         self.grad_clip = grad_clip
         if color_space not in _CS:
@@ -190,7 +196,8 @@ class NeRFTrainer:
         t_c = K.sample_stratified(rays, S, True, u_strat, seed)
         xd_c = K.build_xd(rays, t_c)
         ws_c = self._workspace("c", N * S)
-        rs_c = K.mlp_fwd(self.w(0), xd_c, ws_c, True, precision=self.precision, bf16_flags=self.bf16_flags)
+        rs_c = K.mlp_fwd(self.w(0), xd_c, ws_c, True, precision=self.precision, bf16_flags=self.bf16_flags,
+                          fp32_flags=self.fp32_flags)
         _, _, w_c, _, _, drgb_c = K.composite_fwd(rs_c, t_c, bg, self.sigma_scale, gt=gt,
                                                   color_space=self.color_space, inv_count=inv_count,
                                                   loss_sum=self.loss_buf)
@@ -206,7 +213,8 @@ class NeRFTrainer:
             with torch.cuda.stream(self._side):
                 d_rs_c = K.composite_bwd(rs_c, t_c, bg, drgb_c, sigma_scale=self.sigma_scale)
                 K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=False, precision=self.precision,
-                          bf16_flags=self.bf16_flags)
+                          bf16_flags=self.bf16_flags,
+                          fp32_flags=self.fp32_flags)
                 # bucket 1 of the data-parallel exchange: the coarse net's gradient is final here, so its all-reduce
                 # starts now and runs beside the fine net's forward / backward (bucket 2 trails the backward)
                 self._exchange(self.gbuf[:P], ev_box[0], 0)
@@ -222,7 +230,8 @@ class NeRFTrainer:
             ws_f = self._workspace("f", N * (S + NI), two_stream=self.split_wgrad)
             ev = ev_box[0]
             rs_f = K.mlp_fwd(self.w(fine_k), xd_f, ws_f, True, events=ev["fwd"] if ev else None,
-                             precision=self.precision, bf16_flags=self.bf16_flags)
+                             precision=self.precision, bf16_flags=self.bf16_flags,
+                          fp32_flags=self.fp32_flags)
             if self.overlap and self.overlap_with == "bwd":
                 side_done = coarse_bwd_on_side()
             _, _, _, _, _, drgb_f = K.composite_fwd(rs_f, t_f, bg, self.sigma_scale, gt=gt,
@@ -231,7 +240,7 @@ class NeRFTrainer:
             d_rs_f = K.composite_bwd(rs_f, t_f, bg, drgb_f, sigma_scale=self.sigma_scale)
             K.mlp_bwd(self.w(fine_k), N * (S + NI), d_rs_f, ws_f, d_w=self.g(fine_k), accumulate=False,
                       events=ev["bwd"] if ev else None, precision=self.precision, bf16_flags=self.bf16_flags,
-                      wgrad_stream=self._wg if self.split_wgrad else None,
+                      fp32_flags=self.fp32_flags, wgrad_stream=self._wg if self.split_wgrad else None,
                       sync=self._wg_sync if self.split_wgrad else None)
             if ev:
                 self.timing["M"] = N * (S + NI)
@@ -241,7 +250,8 @@ class NeRFTrainer:
         else:
             d_rs_c = K.composite_bwd(rs_c, t_c, bg, drgb_c, sigma_scale=self.sigma_scale)
             K.mlp_bwd(self.w(0), N * S, d_rs_c, ws_c, d_w=self.g(0), accumulate=(fine_k == 0 and NI > 0),
-                      precision=self.precision, bf16_flags=self.bf16_flags)
+                      precision=self.precision, bf16_flags=self.bf16_flags,
+                          fp32_flags=self.fp32_flags)
             self._exchange(self.gbuf, ev_box[0], 1)
         self.step_count += 1
         if self.grad_clip is not None and self.grad_clip > 0:
