@@ -18,18 +18,26 @@
 #pragma once
 #include "gemm_bf16.hpp"
 
+// two fp32 -> one packed bf16 pair in ONE v_cvt_pk_bf16_f32 (round to nearest even); the scalar-cast form
+// (nerf_pack_bf16x2) compiles to two converts plus a repack
+typedef float x6_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 x6_bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t x6_pack(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(x6_f32x2{a, b}, x6_bf16x2));
+}
+
 // four fp32 values -> their hi / mid / lo bf16 pieces, packed in pairs (v_cvt_pk_bf16_f32 rounds to nearest even)
 __device__ __forceinline__ void x6_split4(const float4 v, uint2& h, uint2& m, uint2& l) {
 #ifdef NERF_X6_NOSPLIT  // ablation builds only: split cost probe (wrong results)
   h = m = l = make_uint2(__float_as_uint(v.x), __float_as_uint(v.y));
   return;
 #endif
-  const uint32_t h0 = nerf_pack_bf16x2(v.x, v.y), h1 = nerf_pack_bf16x2(v.z, v.w);
+  const uint32_t h0 = x6_pack(v.x, v.y), h1 = x6_pack(v.z, v.w);
   const float r0 = v.x - nerf_bf16_lo(h0), r1 = v.y - nerf_bf16_hi(h0);
   const float r2 = v.z - nerf_bf16_lo(h1), r3 = v.w - nerf_bf16_hi(h1);
-  const uint32_t m0 = nerf_pack_bf16x2(r0, r1), m1 = nerf_pack_bf16x2(r2, r3);
-  const uint32_t l0 = nerf_pack_bf16x2(r0 - nerf_bf16_lo(m0), r1 - nerf_bf16_hi(m0));
-  const uint32_t l1 = nerf_pack_bf16x2(r2 - nerf_bf16_lo(m1), r3 - nerf_bf16_hi(m1));
+  const uint32_t m0 = x6_pack(r0, r1), m1 = x6_pack(r2, r3);
+  const uint32_t l0 = x6_pack(r0 - nerf_bf16_lo(m0), r1 - nerf_bf16_hi(m0));
+  const uint32_t l1 = x6_pack(r2 - nerf_bf16_lo(m1), r3 - nerf_bf16_hi(m1));
   h = make_uint2(h0, h1);
   m = make_uint2(m0, m1);
   l = make_uint2(l0, l1);
@@ -214,6 +222,110 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_x6_kernel(const float* __re
   ntb_epilogue<TM, TN, WTM, WTN, EPI, 0>(acc, m0 + wm * WTM, n0 + wn * WTN, li, lh, bias, C, ldc, mbits, ldmb,
                                          mbits_out);
 #endif
+}
+
+// ------------------------------------------------------------------------------------------ gemm_nt_x6w
+// Wide-wave form of gemm_nt_x6: a 256 x 128 workgroup tile whose four waves each own 64 rows x ALL 128 columns
+// (2 x 4 MFMA tiles), so every activation row is loaded and split by exactly one wave (gemm_nt_x6's 64 x 64 waves
+// split each row twice) and the split VALU work per MFMA halves.  BK = 16 (one k-step per slab), weight planes
+// [3][128][24] bf16 double-buffered in LDS (36 KiB per workgroup); B fragments are read per pair of column blocks
+// so that at most 24 VGPRs of them are live.  Requirements as gemm_nt_x6 with M % 256 == 0.
+template <int EPI, int MINW = 2>
+__global__ __launch_bounds__(256, MINW) void gemm_nt_x6w_kernel(const float* __restrict__ A, int lda,
+                                                               const nerf_bf16* __restrict__ Bp, int ldb, int64_t bplane,
+                                                               const float* __restrict__ bias, float* __restrict__ C,
+                                                               int ldc, const uint32_t* __restrict__ mbits, int ldmb,
+                                                               uint32_t* __restrict__ mbits_out, int K, int n_ntiles) {
+  constexpr int BM = 256, BN = 128, BK = 16, WTM = 64, WTN = 128, TM = 2, TN = 4;
+  constexpr int LS = BK + 8;
+  constexpr int PL = BN * LS;
+  __shared__ __attribute__((aligned(16))) nerf_bf16 smem[2 * 3 * PL];
+
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
+  const int64_t m0 = (int64_t)mt * BM;
+  const int n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const nerf_bf16* Bb = Bp + (int64_t)n0 * ldb;
+  const float* At = A + (m0 + wave * WTM) * lda;
+  int aoff[TM];
+#pragma unroll
+  for (int a = 0; a < TM; ++a) aoff[a] = (a * 32 + li) * lda + 8 * lh;
+
+  float4 ra[2][TM][2];
+  uint4 rb[3];  // weight slab: 3 planes x 128 rows x 2 chunks of 16 B = 3 x 256 chunks (thread: chunk t)
+  const int brow = tid >> 1, bch = tid & 1;
+#define X6W_ALOAD(set_, k0_)                                                                              \
+  _Pragma("unroll") for (int a = 0; a < TM; ++a)                                                         \
+    _Pragma("unroll") for (int hf = 0; hf < 2; ++hf)                                                     \
+      ra[set_][a][hf] = *reinterpret_cast<const float4*>(At + aoff[a] + (k0_) + 4 * hf);
+#define X6W_BLOAD(k0_)                                                                                    \
+  _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                          \
+    rb[p] = *reinterpret_cast<const uint4*>(Bb + p * bplane + (int64_t)brow * ldb + (k0_) + 8 * bch);
+#define X6W_BSTORE(buf_)                                                                                  \
+  _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                          \
+    *reinterpret_cast<uint4*>(smem + ((buf_) * 3 + p) * PL + brow * LS + 8 * bch) = rb[p];
+
+  nerf_f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int nk = K / BK;
+  X6W_ALOAD(0, 0);
+  X6W_ALOAD(1, (nk > 1 ? 1 : 0) * BK);
+  X6W_BLOAD(0);
+  X6W_BSTORE(0);
+  __syncthreads();
+  for (int kt0 = 0; kt0 < nk; kt0 += 2) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // slab kt = kt0 + j: LDS buffer j, activation register set j
+      const int kt = kt0 + j;
+      if (kt < nk) {
+        X6W_BLOAD((kt + 1 < nk ? kt + 1 : kt) * BK);
+        const nerf_bf16* S = smem + j * 3 * PL;
+        nerf_bf16x8 af[TM][3];
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+          uint2 h0, m0_, l0, h1, m1, l1;
+          x6_split4(ra[j][a][0], h0, m0_, l0);
+          x6_split4(ra[j][a][1], h1, m1, l1);
+          af[a][0] = __builtin_bit_cast(nerf_bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+          af[a][1] = __builtin_bit_cast(nerf_bf16x8, make_uint4(m0_.x, m0_.y, m1.x, m1.y));
+          af[a][2] = __builtin_bit_cast(nerf_bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+        }
+        X6W_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);  // set j consumed: slab kt + 2 streams into it
+#pragma unroll
+        for (int bp = 0; bp < TN / 2; ++bp) {  // column-block pairs: 2 x 3 B fragments live
+          nerf_bf16x8 bf[2][3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+              bf[b][p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + ((2 * bp + b) * 32 + li) * LS + 8 * lh);
+#pragma unroll
+          for (int t = 0; t < 6; ++t)
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+              for (int b = 0; b < 2; ++b)
+                acc[a][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[b][X6_PB[t]], af[a][X6_PA[t]],
+                                                                           acc[a][2 * bp + b], 0, 0, 0);
+        }
+        X6W_BSTORE(j ^ 1);
+        __syncthreads();
+      }
+    }
+  }
+#undef X6W_ALOAD
+#undef X6W_BLOAD
+#undef X6W_BSTORE
+
+  ntb_epilogue<TM, TN, WTM, WTN, EPI, 0>(acc, m0 + wave * WTM, n0, li, lh, bias, C, ldc, mbits, ldmb, mbits_out);
 }
 
 // ------------------------------------------------------------------------------------------ gemm_wgrad_x6

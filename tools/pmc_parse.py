@@ -58,6 +58,12 @@ def upper(vals):
 
 fetch = per_kernel(load("FETCH_SIZE"))
 write = per_kernel(load("WRITE_SIZE"))
+if len(sys.argv) <= 2 and any("gemm_nt_x6_kernel" in k[0] for k in fetch):  # fp32 split-product GEMMs (gemm_x6.hpp)
+    CLASSES = {
+        "fwd": ("gemm_nt_x6_kernel<1,", 0),
+        "dgrad": ("gemm_nt_x6_kernel<2,", 0),
+        "wgrad": ("gemm_wgrad_x6_kernel<128, 128, 2>", 0),
+    }
 res, detail = {}, {}
 for cls, (pat, _) in CLASSES.items():
     # the fine-net trunk launches are the ones with the largest grid of that kernel
