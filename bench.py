@@ -276,8 +276,9 @@ def _batch(rb, a, step, rank, world, n_local):
     return rb.batch(n_local, seed=shard_seed(step, rank, world))  # disjoint per-rank streams
 
 
-def _traffic(bf16, key):
-    tpath = os.path.join(ROOT, "profiles", "traffic_bf16.json" if bf16 else "traffic.json")
+def _traffic(bf16, key, split=False):
+    tpath = os.path.join(ROOT, "profiles", "traffic_bf16.json" if bf16 else
+                         ("traffic_split.json" if split else "traffic.json"))
     if os.path.exists(tpath):
         try:
             return json.load(open(tpath)).get(key)
@@ -326,7 +327,13 @@ def roofline_bf16(tm):
             "classes": cls, "rule": "largest total time per step (mean launch x launches) among the fused MLP kernels"}
 
 
-def roofline(tm, bf16, overlap, bf16_flags=0):
+X6_PRODUCTS = 6  # bf16 piece products per fp32 product in the split GEMMs (nerf-sys_amd/csrc/gemm_x6.hpp)
+
+
+def roofline(tm, bf16, overlap, bf16_flags=0, split=False):
+    """fp32 (native): the fine net's 256x256 trunk GEMMs on the fp32 MFMA (peak 157.3 TFLOP/s).  fp32 (split, the
+    default): the same GEMMs run X6_PRODUCTS bf16 MFMA products per fp32 product, so the matrix-core work per launch is
+    6 x 2*M*256*256 bf16 FLOP against the dense bf16 peak; the fp32-equivalent rate is listed beside it."""
     if bf16 and not bf16_flags:
         return roofline_bf16(tm)
     M = tm["M"]
@@ -355,14 +362,22 @@ def roofline(tm, bf16, overlap, bf16_flags=0):
         roof = {"bound": "hbm", "kernel": kern, "achieved": round(ach_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": by, "mfma_tflops": round(ach, 1),
                 "mfma_frac_bf16": round(ach / BF16_MFMA_PEAK_TFLOPS, 4)}
+    elif split:
+        names = {"fwd": "gemm_nt_x6w fwd (fp32 as 6 bf16 split products, 32x32x16, bias+ReLU)",
+                 "wgrad": "gemm_wgrad_x6 (fp32 as 6 bf16 split products, split-M, 128x128 tiles)",
+                 "dgrad": "gemm_nt_x6w dgrad (fp32 as 6 bf16 split products, ReLU mask)"}
+        kern = f"{names[dom]}, fine net M={M}: trunk 256x256 layers {K256}"
+        roof = {"bound": "mfma", "kernel": kern, "achieved": round(X6_PRODUCTS * ach, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(X6_PRODUCTS * ach / BF16_MFMA_PEAK_TFLOPS, 4),
+                "flop_per_launch": X6_PRODUCTS * flop256, "fp32_flop_per_launch": flop256,
+                "fp32_equiv_tflops": round(ach, 2), "fp32_equiv_frac_of_fp32_peak": round(ach / FP32_MFMA_PEAK_TFLOPS, 4)}
     else:
         roof = {"bound": "mfma", "kernel": kern, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "flop_per_launch": flop256}
-    roof.update({"traffic": _traffic(bf16, dom), "class": dom, "mean_launch_ms": round(ms, 4),
+    peak_c = BF16_MFMA_PEAK_TFLOPS if bf16 else (BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS if split else FP32_MFMA_PEAK_TFLOPS)
+    roof.update({"traffic": _traffic(bf16, dom, split), "class": dom, "mean_launch_ms": round(ms, 4),
                  "classes_ms": {k: round(v, 4) for k, v in cls.items()},
-                 "classes_frac": {k: round(flop256 / (v * 1e-3) / 1e12 / (BF16_MFMA_PEAK_TFLOPS if bf16 else
-                                                                       FP32_MFMA_PEAK_TFLOPS), 4)
-                                  for k, v in cls.items()},
+                 "classes_frac": {k: round(flop256 / (v * 1e-3) / 1e12 / peak_c, 4) for k, v in cls.items()},
                  "rule": "largest mean launch time among classes that run alone" +
                          (" (fine fwd overlaps the coarse backward: excluded)" if overlap else "")})
     return roof
@@ -429,7 +444,8 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_
               "bytes_per_step": int(tr.gbuf.numel() * 4)}
     rec = {"value": round(n_local * world * a.steps / el, 1), "ms_per_step": round(el / a.steps * 1e3, 3),
            "final_loss": round(float(loss.item()), 6),
-           "roofline": dict(roofline(tm, precision == "bf16", False, tr.bf16_flags), event_steps=n_ev,
+           "roofline": dict(roofline(tm, precision == "bf16", False, tr.bf16_flags,
+                                     split=precision == "fp32" and tr.fp32_gemm == "split"), event_steps=n_ev,
                             event_pass="the timing_steps steps after the timed region, every launch alone (no "
                                        "side-stream coarse backward, fine weight gradients in line)"),
            "streams": {"coarse_bwd_beside_fine_fwd": tr.overlap, "fine_wgrad_stream": tr.split_wgrad}}
@@ -437,6 +453,9 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_
         rec["fp32_gemm"] = tr.fp32_gemm
     peak = BF16_MFMA_PEAK_TFLOPS if precision == "bf16" else FP32_MFMA_PEAK_TFLOPS
     rec["step_mfma_frac"] = round(rec["value"] * FLOP_PER_RAY / world / 1e12 / peak, 4)
+    if precision == "fp32" and tr.fp32_gemm == "split":  # the trunk's fp32 FLOPs ran as 6 bf16 products each
+        rec["step_mfma_frac_note"] = ("fp32 FLOPs of the step / fp32 MFMA peak (157.3 TFLOP/s); the split GEMMs execute "
+                                      "them on the bf16 matrix cores, so a value above 1 is possible")
     if dp:
         rec["dp"] = dp
     return rec, tr, (coarse, fine)

@@ -490,3 +490,147 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_x6_kernel(const float* __re
     }
   }
 }
+
+// ------------------------------------------------------------------------------------------ gemm_wgrad_x6w
+// The 256 x 256 weight gradient of one split in ONE 512-thread workgroup: G and X are each read once per split (the
+// 128 x 128-tile form reads them twice, PMC 2.30 GB against 1.68 GB algorithmic per fine launch) and every element is
+// split once; eight waves of 64 (n) x 128 (k) (2 x 4 MFMA tiles) amortise each G fragment over four X fragments.
+// 16-row slabs, six piece images [16][288] bf16 per stage, double-buffered (108 KiB: one workgroup per CU, two waves
+// per SIMD); the loads of slab it + 2 are issued at iteration it (two register sets).  The tiles of waves wk == 0 also
+// sum the bias columns.  Requirements: rows_per_split % 16 == 0, M % 16 == 0, ldg / ldx % 4 == 0, K >= 256 (the first
+// 256 columns of X).
+__global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __restrict__ G, int ldg,
+                                                               const float* __restrict__ X, int ldx,
+                                                               float* __restrict__ P, int ldp, float* __restrict__ Pb,
+                                                               int64_t slab, int64_t rows_per_split, int64_t M) {
+  constexpr int MR = 16, TM = 2, TN = 4, WTN = 64, WTK = 128;
+  constexpr int PT = 256 + 32;                   // pitch = 64 B mod 256 B (transposing reads, gemm_bf16.hpp)
+  constexpr int IMG = MR * PT;                   // one piece image
+  constexpr int STAGE = 6 * IMG;                 // G hi / mid / lo, X hi / mid / lo
+  __shared__ __attribute__((aligned(16))) nerf_bf16 smem[2 * STAGE];
+
+  const int s = blockIdx.x;
+  const int64_t r0 = (int64_t)s * rows_per_split;
+  int64_t r1 = r0 + rows_per_split;
+  if (r1 > M) r1 = M;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  const bool do_bias = (Pb != nullptr) && wk == 0;
+
+  // staging: a 16 x 256 fp32 slab = 1024 float4, thread f = tid + 512 i: row f >> 6, float4 f & 63
+  float4 rg[2][2], rx[2][2];
+#define WX6W_GLOAD(set_, m_)                                                                               \
+  _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                          \
+    const int f = tid + 512 * i;                                                                           \
+    rg[set_][i] = *reinterpret_cast<const float4*>(G + ((m_) + (f >> 6)) * ldg + 4 * (f & 63));            \
+    rx[set_][i] = *reinterpret_cast<const float4*>(X + ((m_) + (f >> 6)) * ldx + 4 * (f & 63));            \
+  }
+#define WX6W_SSTORE(set_, buf_)                                                                            \
+  _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                          \
+    const int f = tid + 512 * i;                                                                           \
+    const int o = (f >> 6) * PT + 4 * (f & 63);                                                            \
+    nerf_bf16* S_ = smem + (buf_) * STAGE;                                                                 \
+    uint2 h, m, l;                                                                                         \
+    x6_split4(rg[set_][i], h, m, l);                                                                       \
+    *reinterpret_cast<uint2*>(S_ + o) = h;                                                                 \
+    *reinterpret_cast<uint2*>(S_ + IMG + o) = m;                                                           \
+    *reinterpret_cast<uint2*>(S_ + 2 * IMG + o) = l;                                                       \
+    x6_split4(rx[set_][i], h, m, l);                                                                       \
+    *reinterpret_cast<uint2*>(S_ + 3 * IMG + o) = h;                                                       \
+    *reinterpret_cast<uint2*>(S_ + 4 * IMG + o) = m;                                                       \
+    *reinterpret_cast<uint2*>(S_ + 5 * IMG + o) = l;                                                       \
+  }
+
+  nerf_f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  float bsum[TM];
+#pragma unroll
+  for (int a = 0; a < TM; ++a) bsum[a] = 0.f;
+
+  const int grp = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+  const int trow = 8 * (grp >> 1) + q, tcol = 16 * (grp & 1) + 4 * p4;
+  auto tr_frag = [&](const nerf_bf16* base) {
+    const nerf_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) nerf_s16x4*)(base));
+    const nerf_s16x4 hi =
+        __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) nerf_s16x4*)(base + 4 * PT));
+    const short v8 __attribute__((ext_vector_type(8))) = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(nerf_bf16x8, v8);
+  };
+
+  const int64_t nit = (r1 - r0) / MR;
+  if (nit > 0) {
+    WX6W_GLOAD(0, r0);
+    WX6W_GLOAD(1, r0 + (nit > 1 ? 1 : 0) * MR);
+    WX6W_SSTORE(0, 0);
+  }
+  __syncthreads();
+  for (int64_t it0 = 0; it0 < nit; it0 += 2) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // slab it = it0 + j: LDS buffer j, register set j
+      const int64_t it = it0 + j;
+      if (it >= nit) break;
+      WX6W_GLOAD(j, r0 + (it + 2 < nit ? it + 2 : nit - 1) * MR);
+      const nerf_bf16* Gs = smem + j * STAGE;
+      const nerf_bf16* Xs = Gs + 3 * IMG;
+      nerf_bf16x8 af[TM][3];
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc)
+#pragma unroll
+        for (int a = 0; a < TM; ++a) af[a][pc] = tr_frag(Gs + pc * IMG + trow * PT + wn * WTN + a * 32 + tcol);
+      if (do_bias) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) bsum[a] += ((float)af[a][0][jj] + (float)af[a][1][jj]) + (float)af[a][2][jj];
+      }
+#pragma unroll
+      for (int bp = 0; bp < TN / 2; ++bp) {  // column-block pairs: 2 x 3 X fragments live
+        nerf_bf16x8 bf[2][3];
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            bf[b][pc] = tr_frag(Xs + pc * IMG + trow * PT + wk * WTK + (2 * bp + b) * 32 + tcol);
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+          for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+              acc[a][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][X6_PA[t]], bf[b][X6_PB[t]],
+                                                                         acc[a][2 * bp + b], 0, 0, 0);
+      }
+      if (it + 1 < nit) WX6W_SSTORE((j + 1) & 1, (j + 1) & 1);
+      __syncthreads();
+    }
+  }
+#undef WX6W_GLOAD
+#undef WX6W_SSTORE
+
+  float* Ps = P + (int64_t)s * slab;
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int k = wk * WTK + b * 32 + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = wn * WTN + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        Ps[(int64_t)n * ldp + k] = acc[a][b][r];
+      }
+    }
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const float v = bsum[a] + __shfl_xor(bsum[a], 32, 64);
+      if (lh == 0) Pb[(int64_t)s * slab + wn * WTN + a * 32 + li] = v;
+    }
+  }
+}

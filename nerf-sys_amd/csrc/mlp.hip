@@ -314,7 +314,11 @@ int wgrad_x6(const float* G, int ldg, const float* X, int ldx, int tensor_w, con
   const int64_t slab = L.total;
   if (N != 256 || ldg % 4 || ldx % 4) return NERF_E_ARG;
   auto t128 = [&](const float* Xk, float* Pk, float* Pbk) {
+#ifndef NERF_X6_WGRAD_TILES  // one 512-thread workgroup per split (gemm_wgrad_x6w); the A/B form: 4 x 128x128 tiles
+    gemm_wgrad_x6w_kernel<<<w.S, 512, 0, st>>>(G, ldg, Xk, ldx, Pk, ldp, Pbk, slab, w.rps, w.Mp);
+#else
     gemm_wgrad_x6_kernel<128, 128, 2><<<4 * w.S, 256, 0, st>>>(G, ldg, Xk, ldx, Pk, ldp, Pbk, slab, w.rps, w.Mp, 2, 4);
+#endif
   };
   auto t64 = [&](const float* Xk, float* Pk, float* Pbk) {
     gemm_wgrad_x6_kernel<128, 64, 4><<<2 * w.S, 256, 0, st>>>(G, ldg, Xk, ldx, Pk, ldp, Pbk, slab, w.rps, w.Mp, 1, 2);

@@ -46,9 +46,9 @@ inline const Layout& layout() {
 
 inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
-// split-M partial slabs of the weight gradient: one per 2048 rows, at most 256
-#ifndef NERF_SPLIT_ROWS
-#define NERF_SPLIT_ROWS 2048
+// split-M partial slabs of the weight gradient: one per NERF_SPLIT_ROWS rows, at most 256
+#ifndef NERF_SPLIT_ROWS  // 1024: the split weight-gradient GEMM runs one workgroup per split, so the coarse net
+#define NERF_SPLIT_ROWS 1024  // (Mp = 262,144) needs 256 splits to fill the CUs
 #endif
 inline int n_splits(int64_t Mp) {
   int64_t s = Mp / NERF_SPLIT_ROWS;
