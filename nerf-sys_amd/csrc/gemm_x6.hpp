@@ -225,18 +225,25 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_x6_kernel(const float* __re
 }
 
 // ------------------------------------------------------------------------------------------ gemm_nt_x6w
-// Wide-wave form of gemm_nt_x6: a 256 x 128 workgroup tile whose four waves each own 64 rows x ALL 128 columns
+// Wide-wave form of gemm_nt_x6: a (64 NW) x 128 workgroup tile whose NW waves each own 64 rows x ALL 128 columns
 // (2 x 4 MFMA tiles), so every activation row is loaded and split by exactly one wave (gemm_nt_x6's 64 x 64 waves
-// split each row twice) and the split VALU work per MFMA halves.  BK = 16 (one k-step per slab), weight planes
-// [3][128][24] bf16 double-buffered in LDS (36 KiB per workgroup); B fragments are read per pair of column blocks
-// so that at most 24 VGPRs of them are live.  Requirements as gemm_nt_x6 with M % 256 == 0.
-template <int EPI, int MINW = 2>
-__global__ __launch_bounds__(256, MINW) void gemm_nt_x6w_kernel(const float* __restrict__ A, int lda,
-                                                               const nerf_bf16* __restrict__ Bp, int ldb, int64_t bplane,
-                                                               const float* __restrict__ bias, float* __restrict__ C,
-                                                               int ldc, const uint32_t* __restrict__ mbits, int ldmb,
-                                                               uint32_t* __restrict__ mbits_out, int K, int n_ntiles) {
-  constexpr int BM = 256, BN = 128, BK = 16, WTM = 64, WTN = 128, TM = 2, TN = 4;
+// split each row twice) and the split VALU work per MFMA halves.  Weight planes [3][128][BK + 8] bf16
+// double-buffered in LDS; B fragments are read per pair of column blocks so that at most 24 VGPRs of them are live.
+// Requirements as gemm_nt_x6 with M % (64 NW) == 0 and K % BK == 0.  Default BK = 32, NW = 8 (512 x 128 tiles, one
+// workgroup per CU): C2 step 204.0k -> 207.5-209.0k rays/s over BK = 16, NW = 4 (fwd / dgrad 0.65 -> 0.63 ms).
+template <int EPI, int BK = 32, int NW = 8>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_nt_x6w_kernel(const float* __restrict__ A, int lda,
+                                                                     const nerf_bf16* __restrict__ Bp, int ldb,
+                                                                     int64_t bplane, const float* __restrict__ bias,
+                                                                     float* __restrict__ C, int ldc,
+                                                                     const uint32_t* __restrict__ mbits, int ldmb,
+                                                                     uint32_t* __restrict__ mbits_out, int K,
+                                                                     int n_ntiles) {
+  constexpr int NT = 64 * NW;                     // threads
+  constexpr int BM = 64 * NW, BN = 128, WTM = 64, WTN = 128, TM = 2, TN = 4;
+  constexpr int KS = BK / 16, CPR = BK / 8;       // MFMA k-steps / 16-B weight chunks per row, per slab
+  constexpr int BCH = 3 * BN * CPR / NT;          // weight chunks per thread per slab
+  static_assert((3 * BN * CPR) % NT == 0 && (BN * CPR) % NT == 0, "weight staging");
   constexpr int LS = BK + 8;
   constexpr int PL = BN * LS;
   __shared__ __attribute__((aligned(16))) nerf_bf16 smem[2 * 3 * PL];
@@ -253,19 +260,23 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_x6w_kernel(const float* __r
 #pragma unroll
   for (int a = 0; a < TM; ++a) aoff[a] = (a * 32 + li) * lda + 8 * lh;
 
-  float4 ra[2][TM][2];
-  uint4 rb[3];  // weight slab: 3 planes x 128 rows x 2 chunks of 16 B = 3 x 256 chunks (thread: chunk t)
-  const int brow = tid >> 1, bch = tid & 1;
+  float4 ra[2][TM][KS][2];
+  uint4 rb[BCH];  // chunk c = tid + NT i: plane c / (BN CPR), row (c / CPR) % BN, chunk c % CPR
 #define X6W_ALOAD(set_, k0_)                                                                              \
   _Pragma("unroll") for (int a = 0; a < TM; ++a)                                                         \
-    _Pragma("unroll") for (int hf = 0; hf < 2; ++hf)                                                     \
-      ra[set_][a][hf] = *reinterpret_cast<const float4*>(At + aoff[a] + (k0_) + 4 * hf);
+    _Pragma("unroll") for (int ks = 0; ks < KS; ++ks)                                                    \
+      _Pragma("unroll") for (int hf = 0; hf < 2; ++hf)                                                   \
+        ra[set_][a][ks][hf] = *reinterpret_cast<const float4*>(At + aoff[a] + (k0_) + 16 * ks + 4 * hf);
 #define X6W_BLOAD(k0_)                                                                                    \
-  _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                          \
-    rb[p] = *reinterpret_cast<const uint4*>(Bb + p * bplane + (int64_t)brow * ldb + (k0_) + 8 * bch);
+  _Pragma("unroll") for (int i = 0; i < BCH; ++i) {                                                      \
+    const int c = tid + NT * i, p = c / (BN * CPR), r = (c / CPR) % BN, q = c % CPR;                     \
+    rb[i] = *reinterpret_cast<const uint4*>(Bb + p * bplane + (int64_t)r * ldb + (k0_) + 8 * q);         \
+  }
 #define X6W_BSTORE(buf_)                                                                                  \
-  _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                          \
-    *reinterpret_cast<uint4*>(smem + ((buf_) * 3 + p) * PL + brow * LS + 8 * bch) = rb[p];
+  _Pragma("unroll") for (int i = 0; i < BCH; ++i) {                                                      \
+    const int c = tid + NT * i, p = c / (BN * CPR), r = (c / CPR) % BN, q = c % CPR;                     \
+    *reinterpret_cast<uint4*>(smem + ((buf_) * 3 + p) * PL + r * LS + 8 * q) = rb[i];                    \
+  }
 
   nerf_f32x16 acc[TM][TN];
 #pragma unroll
@@ -288,34 +299,38 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_x6w_kernel(const float* __r
       if (kt < nk) {
         X6W_BLOAD((kt + 1 < nk ? kt + 1 : kt) * BK);
         const nerf_bf16* S = smem + j * 3 * PL;
-        nerf_bf16x8 af[TM][3];
 #pragma unroll
-        for (int a = 0; a < TM; ++a) {
-          uint2 h0, m0_, l0, h1, m1, l1;
-          x6_split4(ra[j][a][0], h0, m0_, l0);
-          x6_split4(ra[j][a][1], h1, m1, l1);
-          af[a][0] = __builtin_bit_cast(nerf_bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
-          af[a][1] = __builtin_bit_cast(nerf_bf16x8, make_uint4(m0_.x, m0_.y, m1.x, m1.y));
-          af[a][2] = __builtin_bit_cast(nerf_bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
-        }
-        X6W_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);  // set j consumed: slab kt + 2 streams into it
+        for (int ks = 0; ks < KS; ++ks) {
+          nerf_bf16x8 af[TM][3];
 #pragma unroll
-        for (int bp = 0; bp < TN / 2; ++bp) {  // column-block pairs: 2 x 3 B fragments live
-          nerf_bf16x8 bf[2][3];
+          for (int a = 0; a < TM; ++a) {
+            uint2 h0, m0_, l0, h1, m1, l1;
+            x6_split4(ra[j][a][ks][0], h0, m0_, l0);
+            x6_split4(ra[j][a][ks][1], h1, m1, l1);
+            af[a][0] = __builtin_bit_cast(nerf_bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+            af[a][1] = __builtin_bit_cast(nerf_bf16x8, make_uint4(m0_.x, m0_.y, m1.x, m1.y));
+            af[a][2] = __builtin_bit_cast(nerf_bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+          }
 #pragma unroll
-          for (int p = 0; p < 3; ++p)
+          for (int bp = 0; bp < TN / 2; ++bp) {  // column-block pairs: 2 x 3 B fragments live
+            nerf_bf16x8 bf[2][3];
 #pragma unroll
-            for (int b = 0; b < 2; ++b)
-              bf[b][p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + ((2 * bp + b) * 32 + li) * LS + 8 * lh);
-#pragma unroll
-          for (int t = 0; t < 6; ++t)
-#pragma unroll
-            for (int a = 0; a < TM; ++a)
+            for (int p = 0; p < 3; ++p)
 #pragma unroll
               for (int b = 0; b < 2; ++b)
-                acc[a][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[b][X6_PB[t]], af[a][X6_PA[t]],
-                                                                           acc[a][2 * bp + b], 0, 0, 0);
+                bf[b][p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + ((2 * bp + b) * 32 + li) * LS + 16 * ks +
+                                                                 8 * lh);
+#pragma unroll
+            for (int t = 0; t < 6; ++t)
+#pragma unroll
+              for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                  acc[a][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[b][X6_PB[t]], af[a][X6_PA[t]],
+                                                                             acc[a][2 * bp + b], 0, 0, 0);
+          }
         }
+        X6W_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);  // set j consumed: slab kt + 2 streams into it
         X6W_BSTORE(j ^ 1);
         __syncthreads();
       }

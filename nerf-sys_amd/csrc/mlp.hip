@@ -288,10 +288,17 @@ int nt_x6(const float* A, int lda, const nerf_bf16* Bp, int ldb, int64_t bplane,
           const uint32_t* mbits, uint32_t* mbits_out, int64_t M, int N, int K, hipStream_t st) {
   if (M % 128 || N % 128 || K % 32 || lda % 4 || ldb % 8) return NERF_E_ARG;
   const int ntn = N / 128;
-#ifndef NERF_X6_SQUARE  // 256 x 128 tiles of 64 x 128 waves (gemm_nt_x6w); NERF_X6_SQUARE: 128 x 128 (A/B builds)
-  if (M % 256 == 0) {
-    gemm_nt_x6w_kernel<EPI><<<(unsigned)((M / 256) * ntn), 256, 0, st>>>(A, lda, Bp, ldb, bplane, bias, C, ldc, mbits,
-                                                                        N / 32, mbits_out, K, ntn);
+#ifndef NERF_X6_SQUARE  // (64 NW) x 128 tiles of 64 x 128 waves (gemm_nt_x6w); NERF_X6_SQUARE: 128 x 128 (A/B builds)
+#ifndef NERF_X6W_BK
+#define NERF_X6W_BK 32
+#endif
+#ifndef NERF_X6W_NW
+#define NERF_X6W_NW 8
+#endif
+  if (M % (64 * NERF_X6W_NW) == 0 && K % NERF_X6W_BK == 0) {
+    gemm_nt_x6w_kernel<EPI, NERF_X6W_BK, NERF_X6W_NW><<<(unsigned)((M / (64 * NERF_X6W_NW)) * ntn), 64 * NERF_X6W_NW, 0,
+                                                        st>>>(A, lda, Bp, ldb, bplane, bias, C, ldc, mbits, N / 32,
+                                                              mbits_out, K, ntn);
     return NERF_OK;
   }
 #endif
