@@ -107,8 +107,9 @@ def parse():
     ap.add_argument("--psnr-steps", type=int, default=3000,
                     help="total train steps of each precision's engine before the held-out PSNR renders")
     ap.add_argument("--psnr-views", type=int, default=2, help="held-out 800x800 views rendered for the PSNR")
-    ap.add_argument("--fp32-gemm", default="split", choices=["split", "native"],
-                    help="fp32 trunk GEMMs: bf16 split products at fp32 accuracy (gemm_x6.hpp) or fp32 MFMA kernels")
+    ap.add_argument("--fp32-gemm", default="split", choices=["split", "split_dgrad", "native"],
+                    help="fp32 trunk GEMMs: forward + weight gradient as bf16 split products (gemm_x6.hpp, default), "
+                         "input gradients split too (split_dgrad), or all on the fp32 MFMA kernels (native)")
     ap.add_argument("--no-native-ref", action="store_true",
                     help="skip the fp32-MFMA (native) engine leg timed beside the split-GEMM engine")
     return ap.parse_args()
@@ -331,9 +332,11 @@ X6_PRODUCTS = 6  # bf16 piece products per fp32 product in the split GEMMs (nerf
 
 
 def roofline(tm, bf16, overlap, bf16_flags=0, split=False):
-    """fp32 (native): the fine net's 256x256 trunk GEMMs on the fp32 MFMA (peak 157.3 TFLOP/s).  fp32 (split, the
-    default): the same GEMMs run X6_PRODUCTS bf16 MFMA products per fp32 product, so the matrix-core work per launch is
-    6 x 2*M*256*256 bf16 FLOP against the dense bf16 peak; the fp32-equivalent rate is listed beside it."""
+    """fp32 native: the fine net's 256x256 trunk GEMMs on the fp32 MFMA (peak 157.3 TFLOP/s).  fp32 split (``split`` =
+    the trainer's fp32_gemm, "split" by default): the forward and weight-gradient GEMMs run X6_PRODUCTS bf16 MFMA
+    products per fp32 product, so their matrix-core work per launch is 6 x 2*M*256*256 bf16 FLOP against the dense
+    bf16 peak (fp32-equivalent rate listed beside it); the input gradients stay on the fp32 MFMA unless
+    split == "split_dgrad"."""
     if bf16 and not bf16_flags:
         return roofline_bf16(tm)
     M = tm["M"]
@@ -346,13 +349,10 @@ def roofline(tm, bf16, overlap, bf16_flags=0, split=False):
     }
     eligible = [k for k in cls if not (overlap and k == "fwd")]
     dom = max(eligible, key=lambda k: cls[k])
-    names = {"fwd": "gemm_nt16 fwd (16x16x4, bias+ReLU)", "wgrad": "gemm_wgrad (32x32x2, split-M, 128x128 tiles)",
-             "dgrad": "gemm_nt16 dgrad (16x16x4, ReLU mask)"}
     ms = cls[dom]
     ach = flop256 / (ms * 1e-3) / 1e12
-    kern = f"{names[dom]}, fine net M={M}: trunk 256x256 layers {K256}"
     if bf16:  # the layered bf16 path (--bf16-flags A/B runs)
-        names = {k: v.replace("gemm_nt", "gemm_nt_bf16").replace("gemm_wgrad", "gemm_wgrad_bf16") for k, v in names.items()}
+        names = {"fwd": "gemm_nt_bf16 fwd", "wgrad": "gemm_wgrad_bf16", "dgrad": "gemm_nt_bf16 dgrad"}
         kern = f"{names[dom]}, fine net M={M}: trunk 256x256 layers {K256}"
         # bf16 layers are HBM-bound: algorithmic bytes per launch per sample row = bf16 rows in (256 * 2 B) +
         # bf16 rows out (256 * 2 B) [+ the 32-B ReLU bitmask word row of dgrad]; wgrad reads two bf16 rows
@@ -362,22 +362,35 @@ def roofline(tm, bf16, overlap, bf16_flags=0, split=False):
         roof = {"bound": "hbm", "kernel": kern, "achieved": round(ach_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": by, "mfma_tflops": round(ach, 1),
                 "mfma_frac_bf16": round(ach / BF16_MFMA_PEAK_TFLOPS, 4)}
-    elif split:
-        names = {"fwd": "gemm_nt_x6w fwd (fp32 as 6 bf16 split products, 32x32x16, bias+ReLU)",
-                 "wgrad": "gemm_wgrad_x6 (fp32 as 6 bf16 split products, split-M, 128x128 tiles)",
-                 "dgrad": "gemm_nt_x6w dgrad (fp32 as 6 bf16 split products, ReLU mask)"}
-        kern = f"{names[dom]}, fine net M={M}: trunk 256x256 layers {K256}"
-        roof = {"bound": "mfma", "kernel": kern, "achieved": round(X6_PRODUCTS * ach, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(X6_PRODUCTS * ach / BF16_MFMA_PEAK_TFLOPS, 4),
-                "flop_per_launch": X6_PRODUCTS * flop256, "fp32_flop_per_launch": flop256,
-                "fp32_equiv_tflops": round(ach, 2), "fp32_equiv_frac_of_fp32_peak": round(ach / FP32_MFMA_PEAK_TFLOPS, 4)}
+        peak_c = {k: BF16_MFMA_PEAK_TFLOPS for k in cls}
+        split_cls = set()
     else:
-        roof = {"bound": "mfma", "kernel": kern, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "flop_per_launch": flop256}
-    peak_c = BF16_MFMA_PEAK_TFLOPS if bf16 else (BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS if split else FP32_MFMA_PEAK_TFLOPS)
-    roof.update({"traffic": _traffic(bf16, dom, split), "class": dom, "mean_launch_ms": round(ms, 4),
+        split_cls = set() if not split else ({"fwd", "wgrad", "dgrad"} if split == "split_dgrad" else {"fwd", "wgrad"})
+        names = {"fwd": "gemm_nt16 fwd (fp32 16x16x4, bias+ReLU)", "wgrad": "gemm_wgrad (fp32 32x32x2, split-M)",
+                 "dgrad": "gemm_nt16 dgrad (fp32 16x16x4, ReLU mask)"}
+        if "fwd" in split_cls:
+            names["fwd"] = "gemm_nt_x6w fwd (fp32 as 6 bf16 split products, 32x32x16, bias+ReLU)"
+        if "wgrad" in split_cls:
+            names["wgrad"] = "gemm_wgrad_x6w (fp32 as 6 bf16 split products, one 512-thread workgroup per split)"
+        if "dgrad" in split_cls:
+            names["dgrad"] = "gemm_nt_x6w dgrad (fp32 as 6 bf16 split products, ReLU mask)"
+        kern = f"{names[dom]}, fine net M={M}: trunk 256x256 layers {K256}"
+        peak_c = {k: (BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS if k in split_cls else FP32_MFMA_PEAK_TFLOPS) for k in cls}
+        if dom in split_cls:
+            roof = {"bound": "mfma", "kernel": kern, "achieved": round(X6_PRODUCTS * ach, 1),
+                    "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(X6_PRODUCTS * ach / BF16_MFMA_PEAK_TFLOPS, 4),
+                    "flop_per_launch": X6_PRODUCTS * flop256, "fp32_flop_per_launch": flop256,
+                    "fp32_equiv_tflops": round(ach, 2),
+                    "fp32_equiv_frac_of_fp32_peak": round(ach / FP32_MFMA_PEAK_TFLOPS, 4)}
+        else:
+            roof = {"bound": "mfma", "kernel": kern, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "flop_per_launch": flop256}
+    roof.update({"traffic": _traffic(bf16, dom, dom in split_cls), "class": dom, "mean_launch_ms": round(ms, 4),
                  "classes_ms": {k: round(v, 4) for k, v in cls.items()},
-                 "classes_frac": {k: round(flop256 / (v * 1e-3) / 1e12 / peak_c, 4) for k, v in cls.items()},
+                 "classes_frac": {k: round(flop256 / (v * 1e-3) / 1e12 / peak_c[k], 4) for k, v in cls.items()},
+                 "classes_engine": {k: ("split x6" if k in split_cls else ("bf16" if bf16 else "fp32 MFMA"))
+                                    for k in cls},
                  "rule": "largest mean launch time among classes that run alone" +
                          (" (fine fwd overlaps the coarse backward: excluded)" if overlap else "")})
     return roof
@@ -445,7 +458,8 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_
     rec = {"value": round(n_local * world * a.steps / el, 1), "ms_per_step": round(el / a.steps * 1e3, 3),
            "final_loss": round(float(loss.item()), 6),
            "roofline": dict(roofline(tm, precision == "bf16", False, tr.bf16_flags,
-                                     split=precision == "fp32" and tr.fp32_gemm == "split"), event_steps=n_ev,
+                                     split=(tr.fp32_gemm if precision == "fp32" and tr.fp32_gemm != "native"
+                                            else False)), event_steps=n_ev,
                             event_pass="the timing_steps steps after the timed region, every launch alone (no "
                                        "side-stream coarse backward, fine weight gradients in line)"),
            "streams": {"coarse_bwd_beside_fine_fwd": tr.overlap, "fine_wgrad_stream": tr.split_wgrad}}
@@ -453,7 +467,7 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_
         rec["fp32_gemm"] = tr.fp32_gemm
     peak = BF16_MFMA_PEAK_TFLOPS if precision == "bf16" else FP32_MFMA_PEAK_TFLOPS
     rec["step_mfma_frac"] = round(rec["value"] * FLOP_PER_RAY / world / 1e12 / peak, 4)
-    if precision == "fp32" and tr.fp32_gemm == "split":  # the trunk's fp32 FLOPs ran as 6 bf16 products each
+    if precision == "fp32" and tr.fp32_gemm != "native":  # most of the trunk's fp32 FLOPs ran as 6 bf16 products
         rec["step_mfma_frac_note"] = ("fp32 FLOPs of the step / fp32 MFMA peak (157.3 TFLOP/s); the split GEMMs execute "
                                       "them on the bf16 matrix cores, so a value above 1 is possible")
     if dp:
@@ -562,7 +576,7 @@ def main():
             sub["dropin_vs_engine"] = round(sub["dropin"]["value"] / sub["value"], 4)
 
     native = None
-    if (world == 1 and a.path == "engine" and not bf16 and a.fp32_gemm == "split" and not a.no_native_ref):
+    if (world == 1 and a.path == "engine" and not bf16 and a.fp32_gemm != "native" and not a.no_native_ref):
         native, _, _ = engine_run(a, dev, rb, world, rank, n_local, "fp32", barrier, nccl, fp32_gemm="native")
     main_res = drop if a.path == "dropin" else engine
     value = main_res["value"]

@@ -472,8 +472,12 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_x6_kernel(const float* __re
     if (do_bias) {
 #pragma unroll
       for (int a = 0; a < TM; ++a)
+        {  // the slab's 8 rows summed first, then added to the running sum (64x fewer additions to the large sum)
+          float t8 = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) bsum[a] += ((float)af[a][0][j] + (float)af[a][1][j]) + (float)af[a][2][j];
+          for (int j = 0; j < 8; ++j) t8 += ((float)af[a][0][j] + (float)af[a][1][j]) + (float)af[a][2][j];
+          bsum[a] += t8;
+        }
     }
     // A = G^T (rows n, piece X6_PA), B = X (columns k, piece X6_PB); P itself is accumulated (not transposed)
     X6_MFMA_BLOCK(acc, TM, TN, af[a_][X6_PA[t_]], bf[b_][X6_PB[t_]])
@@ -601,8 +605,12 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
       if (do_bias) {
 #pragma unroll
         for (int a = 0; a < TM; ++a)
+          {  // the slab's 8 rows summed first, then added to the running sum
+            float t8 = 0.f;
 #pragma unroll
-          for (int jj = 0; jj < 8; ++jj) bsum[a] += ((float)af[a][0][jj] + (float)af[a][1][jj]) + (float)af[a][2][jj];
+            for (int jj = 0; jj < 8; ++jj) t8 += ((float)af[a][0][jj] + (float)af[a][1][jj]) + (float)af[a][2][jj];
+            bsum[a] += t8;
+          }
       }
 #pragma unroll
       for (int bp = 0; bp < TN / 2; ++bp) {  // column-block pairs: 2 x 3 X fragments live

@@ -455,8 +455,12 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
                  int64_t ws_bytes, int flags, hipEvent_t* ev, hipStream_t st, hipStream_t stw, hipEvent_t* sync) {
   NERF_CHECK_ARG(w && d_rgb_sigma && d_w && ws && M >= 0);
   NERF_CHECK_ARG(!stw || sync);
-  if (flags & ~NERF_MLP_NATIVE_FP32) return NERF_E_ENUM;
+  if (flags & ~(NERF_MLP_NATIVE_FP32 | NERF_MLP_SPLIT_DGRAD)) return NERF_E_ENUM;
   const bool native = flags & NERF_MLP_NATIVE_FP32;
+  // input gradients: fp32 MFMA unless NERF_MLP_SPLIT_DGRAD (the split form's accumulator rounding — one guard bit on
+  // each MFMA update, tools/mfma_round_probe.hip — biases the long signed input-gradient sums: 1.3-20x the native
+  // engine's weight-gradient error, tests/test_gpu_split_gemm.py)
+  const bool split_dgrad = !native && (flags & NERF_MLP_SPLIT_DGRAD);
   if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(d_w) || !nerf_aligned16(d_rgb_sigma))
     return NERF_E_ALIGN;
   const bool two = stw != nullptr;
@@ -477,12 +481,12 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
   const int64_t Mp = W.Mp;
   auto Wt = [&](int t) { return w + L.off[t]; };
 
-  // transposed weights for the dgrad GEMMs: fp32 (native) or bf16 piece planes (split products)
+  // transposed weights for the dgrad GEMMs: fp32, or bf16 piece planes (NERF_MLP_SPLIT_DGRAD)
   float* T = W.WT;
   float* WTi[8] = {nullptr};
   TJobs jobs{};
   int nj = 0;
-  if (native) {
+  if (!split_dgrad) {
     for (int i = 1; i < 8; ++i) {
       WTi[i] = T;
       jobs.j[nj++] = TJob{Wt(2 * i), T, 256, 256, KPAD[i]};  // first 256 input cols (h part for trunk.4)
@@ -539,7 +543,7 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
     if (i > 0) {
       if (two) dnext = W.dZ[i - 1];  // never the buffer a trailing weight gradient still reads
       if (ev) (void)hipEventRecord(ev[4 * i + 2], st);
-      if (native)
+      if (!split_dgrad)
         TRY(nt<EPI_MASK>(dcur, 256, WTi[i], 256, nullptr, dnext, 256, W.MB[i - 1], nullptr, Mp, 256, 256, st));
       else
         TRY(nt_x6<EPI_MASK>(dcur, 256, W.WPb + 3 * 65536 * (int64_t)(i - 1), 256, 65536, nullptr, dnext, 256,

@@ -170,7 +170,7 @@ def hierarchical_t_vals(t_coarse, weights_coarse, n_importance, u=None, det=Fals
 
 def freq_encode(x, n_freq, include_input=True):
     """models/encodings.py:437-444 — per input dim [cos f0..f_{L-1}, sin f0..f_{L-1}], dim-major."""
-    bands = 2.0 ** torch.arange(n_freq, dtype=torch.float32).to(x.dtype)
+    bands = 2.0 ** torch.arange(n_freq, dtype=torch.float32).to(device=x.device, dtype=x.dtype)
     xe = x[..., None] * bands
     pe = torch.cat([torch.cos(xe), torch.sin(xe)], -1).reshape(*x.shape[:-1], -1)
     return torch.cat([x, pe], -1) if include_input else pe

@@ -1,0 +1,116 @@
+"""The fp32 MLP's split-product GEMMs (-m gpu; nerf-sys_amd/csrc/gemm_x6.hpp): the trunk's fp32 products run as six
+bf16 piece products with fp32 accumulation, and must be as accurate as the fp32 MFMA kernels they replace.  Both
+engines (flags 0 and NERF_MLP_NATIVE_FP32) are compared with an fp64 evaluation of the same network (the oracle's
+vanilla_forward / autograd, run on the GPU in float64 as the checker) at a size that takes the 128x128-tile kernels
+(M = 40,001) and at the coarse-net C2 size that takes the 512x128 wide-wave kernels (M = 262,144):
+  * forward: the split engine's max and mean error against fp64 stay within 2x / 1.5x of the native engine's (the
+    probe, tools/split_probe.hip, measures the two at the same size of error at the GEMM level);
+  * weight gradients (default engine: split forward and weight gradients, fp32-MFMA input gradients): the relative
+    error norm of every tensor within 2x of the native engine's; NERF_MLP_SPLIT_DGRAD (input gradients split too)
+    reported beside them and held to the parity tolerance only (see the comment in the test); rows with a ReLU
+    pre-activation within 2e-6 of 0 excluded (a flip there moves a whole row's term in either engine, see
+    test_gpu_parity.test_mlp_backward_multi_split_ragged);
+  * both at the north-star tolerance 1e-4 of scale, and the split engine bitwise reproducible run to run."""
+import pytest
+import torch
+
+from oracle import nerf_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def K():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from nerf_amd import kernels
+    return kernels
+
+
+def _params(seed):
+    from nerf_amd.vanilla import VanillaNeRF
+    net = VanillaNeRF().load_reference_state(O.init_vanilla_params(seed)).to(DEV)
+    return net, {k: v.detach() for k, v in net.named_parameters()}
+
+
+def _kink_rows(p64, x64, eps):
+    seen = []
+    relu = torch.relu
+
+    def rec(x):
+        seen.append(x.detach().abs().amin(dim=-1))
+        return relu(x)
+
+    torch.relu = rec
+    try:
+        O.vanilla_forward(p64, x64)
+    finally:
+        torch.relu = relu
+    return torch.stack(seen, 0).amin(0) < eps
+
+
+@pytest.mark.parametrize("M", [40001, 262144])
+def test_split_forward_as_accurate_as_native(K, M):
+    net, p = _params(5)
+    w = net.packed().detach().contiguous()
+    g = torch.Generator().manual_seed(M)
+    x = torch.cat([torch.rand(M, 3, generator=g) * 3 - 1.5,
+                   torch.nn.functional.normalize(torch.randn(M, 3, generator=g), dim=-1)], -1).to(DEV)
+    ref = O.vanilla_forward({k: v.double() for k, v in p.items()}, x.double())
+    outs = {}
+    for name, flags in (("split", 0), ("native", K.MLP_NATIVE_FP32)):
+        ws = K.mlp_workspace(M, True, DEV)
+        outs[name] = K.mlp_fwd(w, x, ws, True, fp32_flags=flags)
+    again = K.mlp_fwd(w, x, K.mlp_workspace(M, True, DEV), True)
+    assert torch.equal(outs["split"], again), "split forward not bitwise reproducible"
+    err = {k: (v.double() - ref).abs() for k, v in outs.items()}
+    scale = max(1.0, ref.abs().max().item())
+    for k, e in err.items():
+        assert e.max().item() <= 1e-4 * scale, f"{k}: max err {e.max().item():.3e}"
+    assert err["split"].max().item() <= 2.0 * err["native"].max().item() + 1e-7, \
+        (err["split"].max().item(), err["native"].max().item())
+    assert err["split"].mean().item() <= 1.5 * err["native"].mean().item() + 1e-9, \
+        (err["split"].mean().item(), err["native"].mean().item())
+
+
+@pytest.mark.parametrize("M", [40001, 262144])
+def test_split_backward_as_accurate_as_native(K, M):
+    net, p = _params(6)
+    w = net.packed().detach().contiguous()
+    g = torch.Generator().manual_seed(M + 1)
+    x = torch.cat([torch.rand(M, 3, generator=g) * 3 - 1.5,
+                   torch.nn.functional.normalize(torch.randn(M, 3, generator=g), dim=-1)], -1).to(DEV)
+    gup = torch.randn(M, 4, generator=g).to(DEV) * 1e-3
+    p64 = {k: v.double().requires_grad_(True) for k, v in p.items()}
+    kink = _kink_rows({k: v.detach() for k, v in p64.items()}, x.double(), 2e-6)
+    gup[kink] = 0.0
+    ref = O.vanilla_forward(p64, x.double())
+    gr = torch.autograd.grad((ref * gup.double()).sum(), list(p64.values()))
+    dws = {}
+    for name, flags in (("split", 0), ("native", K.MLP_NATIVE_FP32), ("split_dgrad", K.MLP_SPLIT_DGRAD)):
+        ws = K.mlp_workspace(M, True, DEV)
+        K.mlp_fwd(w, x, ws, True, fp32_flags=flags & K.MLP_NATIVE_FP32)
+        dws[name] = K.mlp_bwd(w, M, gup, ws, fp32_flags=flags)
+    # the fp64 gradients in the packed layout (PackedLayout's index map of the reference-named tensors)
+    from nerf_amd.vanilla import PackedLayout
+    L = PackedLayout.get()
+    ref_packed = torch.zeros(L.total, dtype=torch.float64, device=DEV)
+    for name, gk in zip(p64.keys(), gr):
+        ref_packed[L.index[name].to(DEV)] = gk.reshape(-1)
+    errs = {}
+    for t, (off, rows, cols, creal) in enumerate(L.table):
+        n = rows * cols
+        r = ref_packed[off:off + n]
+        if r.abs().max().item() == 0.0:
+            continue
+        errs[t] = {k: (v[off:off + n].double() - r).norm().item() / r.norm().item() for k, v in dws.items()}
+        print(f"M={M} tensor {t}: relative error split {errs[t]['split']:.3e} native {errs[t]['native']:.3e} "
+              f"split_dgrad {errs[t]['split_dgrad']:.3e}")
+    for t, e in errs.items():
+        for k, v in e.items():
+            assert v <= 1e-4, f"tensor {t} {k}: relative error {v:.3e}"
+        # default engine (split forward + weight gradient, fp32 input gradients): as accurate as native
+        assert e["split"] <= 2.0 * e["native"] + 1e-7, f"tensor {t}: split {e['split']:.3e} native {e['native']:.3e}"
+        # NERF_MLP_SPLIT_DGRAD: the bf16 MFMA's one-guard-bit accumulator updates (tools/mfma_round_probe.hip) bias the
+        # long signed input-gradient chain — measured 1.3-20x the native error; held to the parity tolerance above
