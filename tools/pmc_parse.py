@@ -58,11 +58,13 @@ def upper(vals):
 
 fetch = per_kernel(load("FETCH_SIZE"))
 write = per_kernel(load("WRITE_SIZE"))
-if len(sys.argv) <= 2 and any("gemm_nt_x6_kernel" in k[0] for k in fetch):  # fp32 split-product GEMMs (gemm_x6.hpp)
+if len(sys.argv) <= 2 and any("_x6" in k[0] for k in fetch):  # fp32 split-product GEMMs (gemm_x6.hpp)
+    split_dgrad = any("gemm_nt_x6w_kernel<2," in k[0] for k in fetch)
     CLASSES = {
-        "fwd": ("gemm_nt_x6_kernel<1,", 0),
-        "dgrad": ("gemm_nt_x6_kernel<2,", 0),
-        "wgrad": ("gemm_wgrad_x6_kernel<128, 128, 2>", 0),
+        "fwd": ("gemm_nt_x6w_kernel<1,", 0),
+        # default engine: input gradients on the fp32 16x16x4 kernel; NERF_MLP_SPLIT_DGRAD: the split form
+        "dgrad": ("gemm_nt_x6w_kernel<2," if split_dgrad else "gemm_nt16_kernel<128, 128, 2, 2,", 0),
+        "wgrad": ("gemm_wgrad_x6w_kernel", 0),
     }
 res, detail = {}, {}
 for cls, (pat, _) in CLASSES.items():
