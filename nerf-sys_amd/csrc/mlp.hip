@@ -295,6 +295,13 @@ int nt_x6(const float* A, int lda, const nerf_bf16* Bp, int ldb, int64_t bplane,
 #ifndef NERF_X6W_NW
 #define NERF_X6W_NW 8
 #endif
+#ifdef NERF_X6_PIPE
+  if (M % 512 == 0 && K % 16 == 0) {
+    gemm_nt_x6p_kernel<EPI><<<(unsigned)((M / 512) * ntn), 512, 0, st>>>(A, lda, Bp, ldb, bplane, bias, C, ldc, mbits,
+                                                                        N / 32, mbits_out, K, ntn);
+    return NERF_OK;
+  }
+#endif
   if (M % (64 * NERF_X6W_NW) == 0 && K % NERF_X6W_BK == 0) {
     gemm_nt_x6w_kernel<EPI, NERF_X6W_BK, NERF_X6W_NW><<<(unsigned)((M / (64 * NERF_X6W_NW)) * ntn), 64 * NERF_X6W_NW, 0,
                                                         st>>>(A, lda, Bp, ldb, bplane, bias, C, ldc, mbits, N / 32,

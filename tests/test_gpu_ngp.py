@@ -494,4 +494,6 @@ def test_bwd_hash_fused_vs_pair(N, levels, M, interp):
     torch.cuda.synchronize()
     assert torch.equal(dw_f.cpu(), dw_p.cpu())
     scale = float(dt_p.abs().max())
-    assert float((dt_f - dt_p).abs().max()) <= 1e-6 * scale
+    # the same fp32 terms added by atomics in two different orders: a coarse-level entry takes thousands of adds, so the
+    # two sums can differ by tens of ulps of the largest entry (measured up to 1.1e-6 of scale at M = 40,000)
+    assert float((dt_f - dt_p).abs().max()) <= 4e-6 * scale
