@@ -107,9 +107,9 @@ def parse():
     ap.add_argument("--psnr-steps", type=int, default=3000,
                     help="total train steps of each precision's engine before the held-out PSNR renders")
     ap.add_argument("--psnr-views", type=int, default=2, help="held-out 800x800 views rendered for the PSNR")
-    ap.add_argument("--fp32-gemm", default="split", choices=["split", "split_dgrad", "native"],
-                    help="fp32 trunk GEMMs: forward + weight gradient as bf16 split products (gemm_x6.hpp, default), "
-                         "input gradients split too (split_dgrad), or all on the fp32 MFMA kernels (native)")
+    ap.add_argument("--fp32-gemm", default="split", choices=["split", "native_dgrad", "native"],
+                    help="fp32 trunk GEMMs: all as bf16 split products (gemm_x6.hpp, default), input gradients on the "
+                         "fp32 MFMA (native_dgrad), or all on the fp32 MFMA kernels (native)")
     ap.add_argument("--no-native-ref", action="store_true",
                     help="skip the fp32-MFMA (native) engine leg timed beside the split-GEMM engine")
     return ap.parse_args()
@@ -335,8 +335,8 @@ def roofline(tm, bf16, overlap, bf16_flags=0, split=False):
     """fp32 native: the fine net's 256x256 trunk GEMMs on the fp32 MFMA (peak 157.3 TFLOP/s).  fp32 split (``split`` =
     the trainer's fp32_gemm, "split" by default): the forward and weight-gradient GEMMs run X6_PRODUCTS bf16 MFMA
     products per fp32 product, so their matrix-core work per launch is 6 x 2*M*256*256 bf16 FLOP against the dense
-    bf16 peak (fp32-equivalent rate listed beside it); the input gradients stay on the fp32 MFMA unless
-    split == "split_dgrad"."""
+    bf16 peak (fp32-equivalent rate listed beside it); split == "native_dgrad" keeps the input gradients on the fp32
+    MFMA."""
     if bf16 and not bf16_flags:
         return roofline_bf16(tm)
     M = tm["M"]
@@ -365,7 +365,7 @@ def roofline(tm, bf16, overlap, bf16_flags=0, split=False):
         peak_c = {k: BF16_MFMA_PEAK_TFLOPS for k in cls}
         split_cls = set()
     else:
-        split_cls = set() if not split else ({"fwd", "wgrad", "dgrad"} if split == "split_dgrad" else {"fwd", "wgrad"})
+        split_cls = set() if not split else ({"fwd", "wgrad"} if split == "native_dgrad" else {"fwd", "wgrad", "dgrad"})
         names = {"fwd": "gemm_nt16 fwd (fp32 16x16x4, bias+ReLU)", "wgrad": "gemm_wgrad (fp32 32x32x2, split-M)",
                  "dgrad": "gemm_nt16 dgrad (fp32 16x16x4, ReLU mask)"}
         if "fwd" in split_cls:
@@ -373,7 +373,7 @@ def roofline(tm, bf16, overlap, bf16_flags=0, split=False):
         if "wgrad" in split_cls:
             names["wgrad"] = "gemm_wgrad_x6w (fp32 as 6 bf16 split products, one 512-thread workgroup per split)"
         if "dgrad" in split_cls:
-            names["dgrad"] = "gemm_nt_x6w dgrad (fp32 as 6 bf16 split products, ReLU mask)"
+            names["dgrad"] = "gemm_nt_x6w<BIGSMALL> dgrad (fp32 as 6 bf16 split products, small-term accumulators)"
         kern = f"{names[dom]}, fine net M={M}: trunk 256x256 layers {K256}"
         peak_c = {k: (BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS if k in split_cls else FP32_MFMA_PEAK_TFLOPS) for k in cls}
         if dom in split_cls:

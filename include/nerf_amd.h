@@ -130,16 +130,17 @@ int nerf_mlp_bwd_2s(const float* w, int64_t M, const float* d_rgb_sigma, float* 
  * trunk GEMMs (forward, input gradient, weight gradient) run on the bf16 matrix cores as split products — every fp32
  * operand is cut into three bf16 pieces hi + mid + lo that sum to it exactly, and the six piece products down to
  * 2^-16 of the leading one are accumulated in fp32 (v_mfma_f32_32x32x16_bf16); measured error against fp64 equals the
- * fp32 MFMA's and a sequential fp32 fmaf chain's (tools/split_probe.hip).  NERF_MLP_NATIVE_FP32 selects the
+ * fp32 MFMA's and a sequential fp32 fmaf chain's (tools/split_probe.hip); the input-gradient GEMMs keep the small
+ * products in separate accumulators (see NERF_MLP_NATIVE_DGRAD).  NERF_MLP_NATIVE_FP32 selects the
  * v_mfma_f32_16x16x4_f32 kernels instead.  Unknown flag bits: NERF_E_ENUM.  Replaces the same reference interfaces as
  * nerf_mlp_fwd / nerf_mlp_bwd (MetaNeRF forward / autograd, models/inr/meta_vanilla.py:123-154). */
 #define NERF_MLP_NATIVE_FP32 1
-/* NERF_MLP_SPLIT_DGRAD (backward, with the split engine): the input-gradient GEMMs as split products too.  Faster
- * (0.63 vs 0.82 ms per C2 fine layer) but the bf16 MFMA adds each 16-product sum to its fp32 accumulator with one
- * guard bit (tools/mfma_round_probe.hip), which biases the long signed input-gradient chain: weight gradients carry
- * 1.3-20x the fp32 engine's error (<= 1.5e-5 relative at M = 262,144).  Off by default: the input gradients run on the
- * fp32 MFMA kernels. */
-#define NERF_MLP_SPLIT_DGRAD 2
+/* NERF_MLP_NATIVE_DGRAD (backward, with the split engine): the input-gradient GEMMs on the fp32 MFMA kernels.  By
+ * default they are split products too, with the five small products in accumulators of their own: the bf16 MFMA adds
+ * each 16-product sum to its fp32 accumulator with one guard bit (tools/mfma_round_probe.hip), and with ONE accumulator
+ * that biased the long signed input-gradient chain (weight gradients 1.3-20x the fp32 engine's error); with separate
+ * small-term accumulators they are as accurate as the fp32 engine's (tests/test_gpu_split_gemm.py). */
+#define NERF_MLP_NATIVE_DGRAD 2
 int nerf_mlp_fwd_ex(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws, int64_t ws_bytes,
                     int training, int flags, hipEvent_t* events, hipStream_t stream);
 int nerf_mlp_bwd_ex(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,

@@ -231,8 +231,8 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_x6_kernel(const float* __re
 // double-buffered in LDS; B fragments are read per pair of column blocks so that at most 24 VGPRs of them are live.
 // Requirements as gemm_nt_x6 with M % (64 NW) == 0 and K % BK == 0.  Default BK = 32, NW = 8 (512 x 128 tiles, one
 // workgroup per CU): C2 step 204.0k -> 207.5-209.0k rays/s over BK = 16, NW = 4 (fwd / dgrad 0.65 -> 0.63 ms).
-template <int EPI, int BK = 32, int NW = 8>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_nt_x6w_kernel(const float* __restrict__ A, int lda,
+template <int EPI, int BK = 32, int NW = 8, bool BIGSMALL = false>
+__global__ __launch_bounds__(64 * NW, BIGSMALL ? 1 : 8 / NW) void gemm_nt_x6w_kernel(const float* __restrict__ A, int lda,
                                                                      const nerf_bf16* __restrict__ Bp, int ldb,
                                                                      int64_t bplane, const float* __restrict__ bias,
                                                                      float* __restrict__ C, int ldc,
@@ -278,13 +278,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_nt_x6w_kernel(const floa
     *reinterpret_cast<uint4*>(smem + ((buf_) * 3 + p) * PL + r * LS + 8 * q) = rb[i];                    \
   }
 
-  nerf_f32x16 acc[TM][TN];
+  // BIGSMALL: the five small piece products accumulate in their own registers (2^-8 of the hi.hi sum, so the bf16
+  // MFMA's one-guard-bit accumulator update loses 2^8 less there) and hi.hi gets 1 update per k-step instead of 6
+  nerf_f32x16 acc[TM][TN], accs[BIGSMALL ? TM : 1][BIGSMALL ? TN : 1];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
     for (int b = 0; b < TN; ++b)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+      for (int r = 0; r < 16; ++r) {
+        acc[a][b][r] = 0.f;
+        if constexpr (BIGSMALL) accs[a][b][r] = 0.f;
+      }
 
   const int nk = K / BK;
   X6W_ALOAD(0, 0);
@@ -325,9 +330,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_nt_x6w_kernel(const floa
 #pragma unroll
               for (int a = 0; a < TM; ++a)
 #pragma unroll
-                for (int b = 0; b < 2; ++b)
-                  acc[a][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[b][X6_PB[t]], af[a][X6_PA[t]],
-                                                                             acc[a][2 * bp + b], 0, 0, 0);
+                for (int b = 0; b < 2; ++b) {
+                  if constexpr (BIGSMALL) {
+                    if (t < 5)
+                      accs[a][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                          bf[b][X6_PB[t]], af[a][X6_PA[t]], accs[a][2 * bp + b], 0, 0, 0);
+                    else
+                      acc[a][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                          bf[b][X6_PB[t]], af[a][X6_PA[t]], acc[a][2 * bp + b], 0, 0, 0);
+                  } else {
+                    acc[a][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[b][X6_PB[t]], af[a][X6_PA[t]],
+                                                                               acc[a][2 * bp + b], 0, 0, 0);
+                  }
+                }
           }
         }
         X6W_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);  // set j consumed: slab kt + 2 streams into it
@@ -340,124 +355,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_nt_x6w_kernel(const floa
 #undef X6W_BLOAD
 #undef X6W_BSTORE
 
+  if constexpr (BIGSMALL) {
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) acc[a][b] += accs[a][b];
+  }
   ntb_epilogue<TM, TN, WTM, WTN, EPI, 0>(acc, m0 + wave * WTM, n0, li, lh, bias, C, ldc, mbits, ldmb, mbits_out);
-}
-
-// ------------------------------------------------------------------------------------------ gemm_nt_x6p
-// Software-pipelined form of gemm_nt_x6w (A/B build NERF_X6_PIPE): the eight waves of a workgroup pass the slab
-// barrier together, so in gemm_nt_x6w both waves of a SIMD split their activation fragments (VALU) at the same time and
-// then issue their MFMAs at the same time.  Here a wave splits the fragments of k-step s + 1 between the two MFMA
-// groups of k-step s (the MFMAs run asynchronously beside the VALU work), so the split leaves the critical path.
-// 16-deep slabs (one k-step per slab) keep the extra fragment registers within two waves per SIMD.
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm_nt_x6p_kernel(const float* __restrict__ A, int lda,
-                                                            const nerf_bf16* __restrict__ Bp, int ldb, int64_t bplane,
-                                                            const float* __restrict__ bias, float* __restrict__ C,
-                                                            int ldc, const uint32_t* __restrict__ mbits, int ldmb,
-                                                            uint32_t* __restrict__ mbits_out, int K, int n_ntiles) {
-  constexpr int NW = 8, NT = 512, BK = 16;
-  constexpr int BM = 64 * NW, BN = 128, WTM = 64, TM = 2, TN = 4;
-  constexpr int CPR = BK / 8;                     // 2 weight chunks of 16 B per row per slab
-  constexpr int NCH = 3 * BN * CPR;               // 768 weight chunks per slab
-  constexpr int BCH = (NCH + NT - 1) / NT;        // 2 (threads >= 256: one; wave-uniform)
-  constexpr int LS = BK + 8;
-  constexpr int PL = BN * LS;
-  __shared__ __attribute__((aligned(16))) nerf_bf16 smem[2 * 3 * PL];
-
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
-  const int64_t m0 = (int64_t)mt * BM;
-  const int n0 = nt * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int li = lane & 31, lh = lane >> 5;
-  const nerf_bf16* Bb = Bp + (int64_t)n0 * ldb;
-  const float* At = A + (m0 + wave * WTM) * lda;
-  int aoff[TM];
-#pragma unroll
-  for (int a = 0; a < TM; ++a) aoff[a] = (a * 32 + li) * lda + 8 * lh;
-
-  float4 ra[2][TM][2];
-  uint4 rb[BCH];
-#define X6P_ALOAD(set_, k0_)                                                                              \
-  _Pragma("unroll") for (int a = 0; a < TM; ++a)                                                         \
-    _Pragma("unroll") for (int hf = 0; hf < 2; ++hf)                                                     \
-      ra[set_][a][hf] = *reinterpret_cast<const float4*>(At + aoff[a] + (k0_) + 4 * hf);
-#define X6P_BLOAD(k0_)                                                                                    \
-  _Pragma("unroll") for (int i = 0; i < BCH; ++i) {                                                      \
-    const int c = tid + NT * i, p = c / (BN * CPR), r = (c / CPR) % BN, q = c % CPR;                     \
-    if (NCH % NT == 0 || c < NCH)                                                                        \
-      rb[i] = *reinterpret_cast<const uint4*>(Bb + p * bplane + (int64_t)r * ldb + (k0_) + 8 * q);       \
-  }
-#define X6P_BSTORE(buf_)                                                                                  \
-  _Pragma("unroll") for (int i = 0; i < BCH; ++i) {                                                      \
-    const int c = tid + NT * i, p = c / (BN * CPR), r = (c / CPR) % BN, q = c % CPR;                     \
-    if (NCH % NT == 0 || c < NCH) *reinterpret_cast<uint4*>(smem + ((buf_) * 3 + p) * PL + r * LS + 8 * q) = rb[i]; \
-  }
-  auto split_frags = [&](const float4 (&r)[TM][2], nerf_bf16x8 (&af)[TM][3]) {
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
-      uint2 h0, m0_, l0, h1, m1, l1;
-      x6_split4(r[a][0], h0, m0_, l0);
-      x6_split4(r[a][1], h1, m1, l1);
-      af[a][0] = __builtin_bit_cast(nerf_bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
-      af[a][1] = __builtin_bit_cast(nerf_bf16x8, make_uint4(m0_.x, m0_.y, m1.x, m1.y));
-      af[a][2] = __builtin_bit_cast(nerf_bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
-    }
-  };
-
-  nerf_f32x16 acc[TM][TN];
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-
-  const int nk = K / BK;
-  X6P_ALOAD(0, 0);
-  X6P_ALOAD(1, (nk > 1 ? 1 : 0) * BK);
-  X6P_BLOAD(0);
-  X6P_BSTORE(0);
-  nerf_bf16x8 af[2][TM][3];  // [cur / next]
-  split_frags(ra[0], af[0]);
-  __syncthreads();
-  for (int kt0 = 0; kt0 < nk; kt0 += 2) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {  // slab kt = kt0 + j: LDS buffer j, activation register set j, fragments af[j]
-      const int kt = kt0 + j;
-      if (kt < nk) {
-        X6P_BLOAD((kt + 1 < nk ? kt + 1 : kt) * BK);
-        X6P_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);  // set j was split into af[j] one slab ago
-        const nerf_bf16* S = smem + j * 3 * PL;
-#pragma unroll
-        for (int bp = 0; bp < TN / 2; ++bp) {
-          nerf_bf16x8 bf[2][3];
-#pragma unroll
-          for (int p = 0; p < 3; ++p)
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-              bf[b][p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + ((2 * bp + b) * 32 + li) * LS + 8 * lh);
-#pragma unroll
-          for (int t = 0; t < 6; ++t)
-#pragma unroll
-            for (int a = 0; a < TM; ++a)
-#pragma unroll
-              for (int b = 0; b < 2; ++b)
-                acc[a][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[b][X6_PB[t]], af[j][a][X6_PA[t]],
-                                                                           acc[a][2 * bp + b], 0, 0, 0);
-          // between the two MFMA groups: the next slab's fragments (its activations landed one slab ago)
-          if (bp == 0) split_frags(ra[j ^ 1], af[j ^ 1]);
-        }
-        X6P_BSTORE(j ^ 1);
-        __syncthreads();
-      }
-    }
-  }
-#undef X6P_ALOAD
-#undef X6P_BLOAD
-#undef X6P_BSTORE
-
-  ntb_epilogue<TM, TN, WTM, 128, EPI, 0>(acc, m0 + wave * WTM, n0, li, lh, bias, C, ldc, mbits, ldmb, mbits_out);
 }
 
 // ------------------------------------------------------------------------------------------ gemm_wgrad_x6

@@ -295,13 +295,14 @@ int nt_x6(const float* A, int lda, const nerf_bf16* Bp, int ldb, int64_t bplane,
 #ifndef NERF_X6W_NW
 #define NERF_X6W_NW 8
 #endif
-#ifdef NERF_X6_PIPE
-  if (M % 512 == 0 && K % 16 == 0) {
-    gemm_nt_x6p_kernel<EPI><<<(unsigned)((M / 512) * ntn), 512, 0, st>>>(A, lda, Bp, ldb, bplane, bias, C, ldc, mbits,
-                                                                        N / 32, mbits_out, K, ntn);
-    return NERF_OK;
+  if constexpr (EPI == EPI_MASK) {  // input gradients: split accumulators, one wave per SIMD (gemm_x6.hpp BIGSMALL)
+    if (M % 256 == 0 && K % 32 == 0) {
+      gemm_nt_x6w_kernel<EPI, 32, 4, true><<<(unsigned)((M / 256) * ntn), 256, 0, st>>>(A, lda, Bp, ldb, bplane, bias,
+                                                                                    C, ldc, mbits, N / 32, mbits_out,
+                                                                                    K, ntn);
+      return NERF_OK;
+    }
   }
-#endif
   if (M % (64 * NERF_X6W_NW) == 0 && K % NERF_X6W_BK == 0) {
     gemm_nt_x6w_kernel<EPI, NERF_X6W_BK, NERF_X6W_NW><<<(unsigned)((M / (64 * NERF_X6W_NW)) * ntn), 64 * NERF_X6W_NW, 0,
                                                         st>>>(A, lda, Bp, ldb, bplane, bias, C, ldc, mbits, N / 32,
@@ -462,12 +463,11 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
                  int64_t ws_bytes, int flags, hipEvent_t* ev, hipStream_t st, hipStream_t stw, hipEvent_t* sync) {
   NERF_CHECK_ARG(w && d_rgb_sigma && d_w && ws && M >= 0);
   NERF_CHECK_ARG(!stw || sync);
-  if (flags & ~(NERF_MLP_NATIVE_FP32 | NERF_MLP_SPLIT_DGRAD)) return NERF_E_ENUM;
+  if (flags & ~(NERF_MLP_NATIVE_FP32 | NERF_MLP_NATIVE_DGRAD)) return NERF_E_ENUM;
   const bool native = flags & NERF_MLP_NATIVE_FP32;
-  // input gradients: fp32 MFMA unless NERF_MLP_SPLIT_DGRAD (the split form's accumulator rounding — one guard bit on
-  // each MFMA update, tools/mfma_round_probe.hip — biases the long signed input-gradient sums: 1.3-20x the native
-  // engine's weight-gradient error, tests/test_gpu_split_gemm.py)
-  const bool split_dgrad = !native && (flags & NERF_MLP_SPLIT_DGRAD);
+  // input gradients: split products with the small terms in their own accumulators (gemm_nt_x6w BIGSMALL) unless
+  // NERF_MLP_NATIVE_DGRAD keeps them on the fp32 MFMA
+  const bool split_dgrad = !native && !(flags & NERF_MLP_NATIVE_DGRAD);
   if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(d_w) || !nerf_aligned16(d_rgb_sigma))
     return NERF_E_ALIGN;
   const bool two = stw != nullptr;
@@ -488,7 +488,7 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
   const int64_t Mp = W.Mp;
   auto Wt = [&](int t) { return w + L.off[t]; };
 
-  // transposed weights for the dgrad GEMMs: fp32, or bf16 piece planes (NERF_MLP_SPLIT_DGRAD)
+  // transposed weights for the dgrad GEMMs: bf16 piece planes (split) or fp32 (NERF_MLP_NATIVE_DGRAD / native)
   float* T = W.WT;
   float* WTi[8] = {nullptr};
   TJobs jobs{};

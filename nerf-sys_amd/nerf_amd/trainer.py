@@ -88,10 +88,10 @@ class NeRFTrainer:
             raise ValueError(f"precision must be one of {K.PRECISIONS}")
         self.precision = precision  # MLP GEMMs: fp32 (configs[1]) or bf16 (configs[2]); compositing stays fp32
         self.bf16_flags = int(bf16_flags)  # K.BF16_LAYERED_* (A/B runs of the layered bf16 launches)
-        # fp32 trunk GEMMs: "split" = forward + weight-gradient GEMMs as bf16 piece products (gemm_x6.hpp), input
-        # gradients on the fp32 MFMA (default); "split_dgrad" = the input gradients split too (faster, 1.3-20x the
-        # weight-gradient error); "native" = every GEMM on the fp32 MFMA kernels
-        flags = {"split": 0, "split_dgrad": K.MLP_SPLIT_DGRAD, "native": K.MLP_NATIVE_FP32}
+        # fp32 trunk GEMMs: "split" = every trunk GEMM as bf16 piece products (gemm_x6.hpp; the input gradients with
+        # separate small-term accumulators), the default; "native_dgrad" = input gradients on the fp32 MFMA;
+        # "native" = every GEMM on the fp32 MFMA kernels
+        flags = {"split": 0, "native_dgrad": K.MLP_NATIVE_DGRAD, "native": K.MLP_NATIVE_FP32}
         if fp32_gemm not in flags:
             raise ValueError(f"fp32_gemm must be one of {sorted(flags)}, got {fp32_gemm!r}")
         self.fp32_gemm = fp32_gemm

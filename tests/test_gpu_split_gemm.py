@@ -5,9 +5,8 @@ vanilla_forward / autograd, run on the GPU in float64 as the checker) at a size 
 (M = 40,001) and at the coarse-net C2 size that takes the 512x128 wide-wave kernels (M = 262,144):
   * forward: the split engine's max and mean error against fp64 stay within 2x / 1.5x of the native engine's (the
     probe, tools/split_probe.hip, measures the two at the same size of error at the GEMM level);
-  * weight gradients (default engine: split forward and weight gradients, fp32-MFMA input gradients): the relative
-    error norm of every tensor within 2x of the native engine's; NERF_MLP_SPLIT_DGRAD (input gradients split too)
-    reported beside them and held to the parity tolerance only (see the comment in the test); rows with a ReLU
+  * weight gradients (default engine, and with NERF_MLP_NATIVE_DGRAD): the relative error norm of every tensor within
+    2x of the native engine's (see the comment in the test); rows with a ReLU
     pre-activation within 2e-6 of 0 excluded (a flip there moves a whole row's term in either engine, see
     test_gpu_parity.test_mlp_backward_multi_split_ragged);
   * both at the north-star tolerance 1e-4 of scale, and the split engine bitwise reproducible run to run."""
@@ -88,7 +87,7 @@ def test_split_backward_as_accurate_as_native(K, M):
     ref = O.vanilla_forward(p64, x.double())
     gr = torch.autograd.grad((ref * gup.double()).sum(), list(p64.values()))
     dws = {}
-    for name, flags in (("split", 0), ("native", K.MLP_NATIVE_FP32), ("split_dgrad", K.MLP_SPLIT_DGRAD)):
+    for name, flags in (("split", 0), ("native", K.MLP_NATIVE_FP32), ("native_dgrad", K.MLP_NATIVE_DGRAD)):
         ws = K.mlp_workspace(M, True, DEV)
         K.mlp_fwd(w, x, ws, True, fp32_flags=flags & K.MLP_NATIVE_FP32)
         dws[name] = K.mlp_bwd(w, M, gup, ws, fp32_flags=flags)
@@ -106,11 +105,12 @@ def test_split_backward_as_accurate_as_native(K, M):
             continue
         errs[t] = {k: (v[off:off + n].double() - r).norm().item() / r.norm().item() for k, v in dws.items()}
         print(f"M={M} tensor {t}: relative error split {errs[t]['split']:.3e} native {errs[t]['native']:.3e} "
-              f"split_dgrad {errs[t]['split_dgrad']:.3e}")
+              f"native_dgrad {errs[t]['native_dgrad']:.3e}")
     for t, e in errs.items():
         for k, v in e.items():
             assert v <= 1e-4, f"tensor {t} {k}: relative error {v:.3e}"
-        # default engine (split forward + weight gradient, fp32 input gradients): as accurate as native
+        # default engine (every trunk GEMM split; input gradients with separate small-term accumulators): as
+        # accurate as native.  (With ONE accumulator the bf16 MFMA's one-guard-bit update, tools/mfma_round_probe.hip,
+        # biased the signed input-gradient chain: 1.3-20x the native error — round 3)
         assert e["split"] <= 2.0 * e["native"] + 1e-7, f"tensor {t}: split {e['split']:.3e} native {e['native']:.3e}"
-        # NERF_MLP_SPLIT_DGRAD: the bf16 MFMA's one-guard-bit accumulator updates (tools/mfma_round_probe.hip) bias the
-        # long signed input-gradient chain — measured 1.3-20x the native error; held to the parity tolerance above
+        assert e["native_dgrad"] <= 2.0 * e["native"] + 1e-7, (t, e)

@@ -62,7 +62,7 @@ if len(sys.argv) <= 2 and any("_x6" in k[0] for k in fetch):  # fp32 split-produ
     split_dgrad = any("gemm_nt_x6w_kernel<2," in k[0] for k in fetch)
     CLASSES = {
         "fwd": ("gemm_nt_x6w_kernel<1,", 0),
-        # default engine: input gradients on the fp32 16x16x4 kernel; NERF_MLP_SPLIT_DGRAD: the split form
+        # default engine: the split input-gradient kernel (small-term accumulators); NERF_MLP_NATIVE_DGRAD: fp32 16x16x4
         "dgrad": ("gemm_nt_x6w_kernel<2," if split_dgrad else "gemm_nt16_kernel<128, 128, 2, 2,", 0),
         "wgrad": ("gemm_wgrad_x6w_kernel", 0),
     }
