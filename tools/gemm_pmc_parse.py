@@ -43,8 +43,13 @@ for d, c in disp.items():
         a["busy"].append(c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (1024 * g / 8))
     if c.get("SQ_WAVE_CYCLES"):
         a["wait"].append(c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"])
+        for k, n in (("SQ_WAIT_INST_ANY", "winst"), ("SQ_ACTIVE_INST_ANY", "active"), ("SQ_WAIT_INST_LDS", "wlds")):
+            if k in c:
+                a[n].append(c[k] / c["SQ_WAVE_CYCLES"])
     a["lds"].append(c.get("SQ_LDS_BANK_CONFLICT", 0.0))
 med = lambda xs: statistics.median(xs) if xs else float("nan")
 for (name, grid), a in sorted(agg.items()):
     print(f"{name:70s} grid {grid:>15s} n {len(a['wall']):3d}  wall {med(a['wall']) * 1e3:7.3f} ms  clock {med(a['clock']):5.2f} GHz  "
-          f"MFMA busy {med(a['busy']):5.3f}  waits/wave-cycles {med(a['wait']):5.3f}  LDS conflicts {med(a['lds']):.3g}")
+          f"MFMA busy {med(a['busy']):5.3f}  waits/wave-cycles {med(a['wait']):5.3f}  LDS conflicts {med(a['lds']):.3g}" +
+          (f"  issue-stall {med(a['winst']):5.3f}  active {med(a['active']):5.3f}  lds-issue-stall {med(a['wlds']):5.3f}"
+           if a["winst"] else ""))
