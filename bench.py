@@ -107,7 +107,7 @@ def parse():
     ap.add_argument("--psnr-steps", type=int, default=3000,
                     help="total train steps of each precision's engine before the held-out PSNR renders")
     ap.add_argument("--psnr-views", type=int, default=2, help="held-out 800x800 views rendered for the PSNR")
-    ap.add_argument("--fp32-gemm", default="split", choices=["split", "native_dgrad", "native", "split_tiled"],
+    ap.add_argument("--fp32-gemm", default="split", choices=["split", "native_dgrad", "native"],
                     help="fp32 trunk GEMMs: all as bf16 split products (gemm_x6.hpp, default), input gradients on the "
                          "fp32 MFMA (native_dgrad), or all on the fp32 MFMA kernels (native)")
     ap.add_argument("--no-native-ref", action="store_true",
@@ -368,13 +368,8 @@ def roofline(tm, bf16, overlap, bf16_flags=0, split=False):
         split_cls = set() if not split else ({"fwd", "wgrad"} if split == "native_dgrad" else {"fwd", "wgrad", "dgrad"})
         names = {"fwd": "gemm_nt16 fwd (fp32 16x16x4, bias+ReLU)", "wgrad": "gemm_wgrad (fp32 32x32x2, split-M)",
                  "dgrad": "gemm_nt16 dgrad (fp32 16x16x4, ReLU mask)"}
-        if split == "split_tiled":  # the register-staged tiled NT kernels (A/B reference of the ring kernels)
-            nt_f, nt_d = "gemm_nt_x6w fwd (fp32 as 6 bf16 split products, 512x128 tiles, bias+ReLU)", \
-                "gemm_nt_x6w<BIGSMALL> dgrad (fp32 as 6 bf16 split products, small-term accumulators)"
-        else:
-            nt_f, nt_d = "gemm_nt_x6r fwd (fp32 as 6 bf16 split products, persistent LDS-DMA ring, bias+ReLU)", \
-                "gemm_nt_x6r<BIGSMALL> dgrad (fp32 as 6 bf16 split products, persistent LDS-DMA ring, " \
-                "small-term accumulators)"
+        nt_f, nt_d = "gemm_nt_x6w fwd (fp32 as 6 bf16 split products, 512x128 tiles, bias+ReLU)", \
+            "gemm_nt_x6w<BIGSMALL> dgrad (fp32 as 6 bf16 split products, small-term accumulators)"
         if "fwd" in split_cls:
             names["fwd"] = nt_f
         if "wgrad" in split_cls:

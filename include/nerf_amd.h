@@ -141,10 +141,6 @@ int nerf_mlp_bwd_2s(const float* w, int64_t M, const float* d_rgb_sigma, float* 
  * that biased the long signed input-gradient chain (weight gradients 1.3-20x the fp32 engine's error); with separate
  * small-term accumulators they are as accurate as the fp32 engine's (tests/test_gpu_split_gemm.py). */
 #define NERF_MLP_NATIVE_DGRAD 2
-/* NERF_MLP_X6_TILED (forward and backward, with the split engine): the 256-wide split forward / input-gradient GEMMs
- * as one launch of 512 x 128 (input gradients: 256 x 128) register-staged tiles (gemm_nt_x6w) instead of the
- * persistent LDS-DMA ring kernel (gemm_nt_x6r).  Same MFMA order per output: bitwise equal results. */
-#define NERF_MLP_X6_TILED 4
 int nerf_mlp_fwd_ex(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws, int64_t ws_bytes,
                     int training, int flags, hipEvent_t* events, hipStream_t stream);
 int nerf_mlp_bwd_ex(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,

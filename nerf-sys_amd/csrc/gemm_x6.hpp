@@ -16,8 +16,6 @@
 // Fragment / LDS conventions are gemm_bf16.hpp's (NT: [rows][BK] tiles, ds_read_b128 per fragment, C^T so a lane
 // owns one output row; wgrad: row-major [m][cols] tiles read with ds_read_b64_tr_b16), one image per piece plane.
 #pragma once
-#include <type_traits>
-
 #include "gemm_bf16.hpp"
 
 // two fp32 -> one packed bf16 pair in ONE v_cvt_pk_bf16_f32 (round to nearest even); the scalar-cast form
@@ -726,218 +724,3 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
   }
 }
 
-// ------------------------------------------------------------------------------------------ gemm_nt_x6r
-// Persistent split NT GEMM for the 256-wide trunk layers (N = 256) with an LDS-DMA ring.  gemm_nt_x6w loads the
-// activation operand straight into registers in fragment shape (every wave-load touches 32 rows x 32 B), keeps one
-// slab of cover, and restarts its pipeline for every 512 x 128 tile at one workgroup per CU (prologue latency and the
-// epilogue's stores exposed): PMC MFMA busy 0.43, 2.8 TB/s.  Here one workgroup per CU walks a strided list of
-// BM x 256 tiles as ONE stream of 16-deep k-slabs; the DMA engine (global_load_lds_dwordx4, full 64-B row pieces of
-// the fp32 activations and of the three bf16 weight planes, no VGPR staging) keeps STAGES - 1 slabs in flight across
-// the tile boundaries; a counted `s_waitcnt vmcnt` + raw barrier retire one slab per iteration.  Every activation row
-// is split by exactly one wave (wave tile 32 rows x 256 columns, 8 accumulators).
-//   NW = 8 waves (forward, BM = 256, two waves per SIMD): stage = 16 KiB activations + 24 KiB weights, 4 stages.
-//   NW = 4 waves (BIGSMALL input gradients, 256 accumulator registers: one wave per SIMD, BM = 128): 32 KiB, 5 stages.
-// LDS images (64-B pseudo-rows of four 16-B chunks, chunk c of pseudo-row r in slot c ^ ((r >> 2) & 3); the DMA writes
-// lane-linear pieces of 16 pseudo-rows, so the swizzle is applied to the SOURCE address):
-//   activations [BM][16] fp32: pseudo-row = row, chunk c = k 4c .. 4c + 3;
-//   weight plane p [256][16] bf16: pseudo-row r holds rows n = 2r, 2r + 1, chunk q = 2 (n & 1) + (k >> 3).
-// Both fragment reads (16 lanes: 16 rows, one chunk) hit 16 distinct 16-B bank slots.  Fragment reads are inline asm:
-// a compiler-visible LDS read of a DMA target is preceded by `s_waitcnt vmcnt(0)`, which would drain the ring.
-// MFMA order per accumulator = gemm_nt_x6w's (k-steps in order, the six terms smallest first): bitwise its results.
-// Requirements (host): N == 256, M % BM == 0, K % 16 == 0, lda % 4 == 0, ldb % 8 == 0, 16-B aligned operands.
-__device__ __forceinline__ x6_f32x4 x6r_lds_f4(uint32_t a) {
-  x6_f32x4 v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
-  return v;
-}
-template <int OFF>
-__device__ __forceinline__ nerf_bf16x8 x6r_lds_b8(uint32_t a) {
-  nerf_bf16x8 v;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF) : "memory");
-  return v;
-}
-
-template <int I, int N, typename F>
-__device__ __forceinline__ void x6r_static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    x6r_static_for<I + 1, N>(f);
-  }
-}
-
-template <int EPI, int NW, bool BIGSMALL>
-__global__ __launch_bounds__(64 * NW, 1) void gemm_nt_x6r_kernel(const float* __restrict__ A, int lda,
-                                                                const nerf_bf16* __restrict__ Bp, int ldb,
-                                                                int64_t bplane, const float* __restrict__ bias,
-                                                                float* __restrict__ C, int ldc,
-                                                                const uint32_t* __restrict__ mbits, int ldmb,
-                                                                uint32_t* __restrict__ mbits_out, int K, int n_tiles) {
-  constexpr int BM = 32 * NW, BN = 256, TN = 8, BK = 16;
-  constexpr int A_BYTES = BM * 64;                 // [BM][16] fp32
-  constexpr int B_PLANE = BN * 32;                 // [256][16] bf16
-  constexpr int STAGE = A_BYTES + 3 * B_PLANE;
-#ifdef NERF_X6R_PAIR  // A/B builds: retire two slabs per barrier (4 stages: one pair read, the next pair in flight)
-  constexpr int STAGES = 4;
-#else
-  constexpr int STAGES = 163840 / STAGE;
-#endif
-  constexpr int NPIECE = STAGE / 1024, NA = A_BYTES / 1024;
-  constexpr int PPW = NPIECE / NW;                 // DMA pieces per wave per slab
-  static_assert(NPIECE % NW == 0 && NA % NW == 0, "pieces of one kind per wave-step");
-  static_assert(STAGES >= 3 && (STAGES - 2) * PPW <= 32, "ring depth");
-  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
-
-  const int grid = gridDim.x;
-  const int t0 = blockIdx.x;
-  if (t0 >= n_tiles) return;
-  const int my_tiles = (n_tiles - t0 + grid - 1) / grid;
-  const int nk = K / BK;
-  const int total = my_tiles * nk;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int li = lane & 31, lh = lane >> 5;
-
-  // DMA sources at tile row 0, k 0 (element offsets): piece pc = wave + NW j; pieces [0, NA) activations, then the
-  // weight planes (8 pieces each)
-  int soff[PPW];
-#pragma unroll
-  for (int j = 0; j < PPW; ++j) {
-    const int pc = wave + NW * j;
-    const int pr = (pc < NA ? pc : (pc - NA) & 7) * 16 + (lane >> 2);  // pseudo-row within the image
-    const int q = (lane & 3) ^ ((pr >> 2) & 3);                         // source chunk of this lane's slot
-    if (pc < NA) soff[j] = pr * lda + 4 * q;
-    else soff[j] = ((pc - NA) >> 3) * (int)bplane + (2 * pr + (q >> 1)) * ldb + 8 * (q & 1);
-  }
-  const uint32_t sbase = (uint32_t)(uintptr_t)smem;
-  auto issue = [&](int g) {
-    const int ti = g / nk, kt = g - ti * nk;
-    const int64_t m0 = (int64_t)(t0 + ti * grid) * BM;
-    char* st = smem + (g % STAGES) * STAGE;
-    const float* Ak = A + m0 * lda + kt * BK;
-    const nerf_bf16* Bk = Bp + kt * BK;
-#pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-      const int pc = wave + NW * j;
-      const void* src = (pc < NA) ? (const void*)(Ak + soff[j]) : (const void*)(Bk + soff[j]);
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(st + pc * 1024), 16, 0, 0);
-    }
-  };
-
-  // fragment addresses (bytes within a stage): activation row 32 wave + li, chunks 2 lh, 2 lh + 1; weight row
-  // n = 32 b + li of plane p: pseudo-row 16 b + (li >> 1), chunk 2 (li & 1) + lh
-  const int asw = (li >> 2) & 3;
-  const uint32_t a_off0 = (uint32_t)((32 * wave + li) * 64 + 16 * ((2 * lh) ^ asw));
-  const uint32_t a_off1 = (uint32_t)((32 * wave + li) * 64 + 16 * ((2 * lh + 1) ^ asw));
-  const uint32_t b_off = (uint32_t)(A_BYTES + (li >> 1) * 64 + 16 * ((2 * (li & 1) + lh) ^ ((li >> 3) & 3)));
-
-#ifdef NERF_X6R_PAIR
-  issue(0);
-  if (1 < total) issue(1);
-#else
-#pragma unroll
-  for (int s0 = 0; s0 < STAGES - 1; ++s0)
-    if (s0 < total) issue(s0);
-#endif
-
-  for (int ti = 0; ti < my_tiles; ++ti) {
-  nerf_f32x16 acc[1][TN], accs[BIGSMALL ? TN : 1];
-#pragma unroll
-  for (int b = 0; b < TN; ++b)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      acc[0][b][r] = 0.f;
-      if constexpr (BIGSMALL) accs[b][r] = 0.f;
-    }
-  for (int g = ti * nk; g < (ti + 1) * nk; ++g) {
-    // retire slab g: this wave's pieces of the younger in-flight slabs (at most STAGES - 2) may stay outstanding
-#ifdef NERF_X6R_PAIR
-    if ((g & 1) == 0) {  // nk is even: a pair never straddles two tiles
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // slabs g, g + 1 landed; every wave is done reading slabs g - 2, g - 1
-      if (g + 2 < total) issue(g + 2);
-      if (g + 3 < total) issue(g + 3);
-    }
-#else
-    const int younger = (total - 1 - g) < (STAGES - 2) ? (total - 1 - g) : (STAGES - 2);
-    ntb_wait_vmcnt(younger * PPW);
-    __builtin_amdgcn_s_barrier();  // every wave's pieces of slab g landed; every wave is done reading slab g - 1
-    if (g + STAGES - 1 < total) issue(g + STAGES - 1);
-#endif
-    const uint32_t st = sbase + (uint32_t)((g % STAGES) * STAGE);
-    const uint32_t bst = st + b_off;
-    // activation fragment (8 fp32) + the first two column pairs' weight fragments
-    x6_f32x4 a0 = x6r_lds_f4(st + a_off0), a1 = x6r_lds_f4(st + a_off1);
-    nerf_bf16x8 bf[2][2][3];  // [buffer][column block of the pair][plane]
-    auto read_pair = [&](auto BP, nerf_bf16x8 (&d)[2][3]) {
-      constexpr int bp = decltype(BP)::value;
-      x6r_static_for<0, 2>([&](auto B) {
-        constexpr int b = 2 * bp + decltype(B)::value;
-        d[decltype(B)::value][0] = x6r_lds_b8<b * 1024>(bst);
-        d[decltype(B)::value][1] = x6r_lds_b8<B_PLANE + b * 1024>(bst);
-        d[decltype(B)::value][2] = x6r_lds_b8<2 * B_PLANE + b * 1024>(bst);
-      });
-    };
-    read_pair(std::integral_constant<int, 0>{}, bf[0]);
-    read_pair(std::integral_constant<int, 1>{}, bf[1]);
-    asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(a0), "+v"(a1)::"memory");
-    nerf_bf16x8 af[3];
-    {
-      uint2 h0, m0_, l0, h1, m1, l1;
-      x6_split4(__builtin_bit_cast(float4, a0), h0, m0_, l0);
-      x6_split4(__builtin_bit_cast(float4, a1), h1, m1, l1);
-      af[0] = __builtin_bit_cast(nerf_bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
-      af[1] = __builtin_bit_cast(nerf_bf16x8, make_uint4(m0_.x, m0_.y, m1.x, m1.y));
-      af[2] = __builtin_bit_cast(nerf_bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
-    }
-    auto mfma_pair = [&](auto BP, nerf_bf16x8 (&d)[2][3]) {
-      constexpr int bp = decltype(BP)::value;
-#pragma unroll
-      for (int t = 0; t < 6; ++t)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          if constexpr (BIGSMALL) {
-            if (t < 5)
-              accs[2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(d[b][X6_PB[t]], af[X6_PA[t]], accs[2 * bp + b], 0, 0, 0);
-            else
-              acc[0][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(d[b][X6_PB[t]], af[X6_PA[t]], acc[0][2 * bp + b], 0, 0, 0);
-          } else {
-            acc[0][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(d[b][X6_PB[t]], af[X6_PA[t]], acc[0][2 * bp + b], 0, 0, 0);
-          }
-        }
-    };
-    auto touch = [&](nerf_bf16x8 (&d)[2][3]) {
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(d[b][p]));
-    };
-    asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
-    touch(bf[0]);
-    mfma_pair(std::integral_constant<int, 0>{}, bf[0]);
-    read_pair(std::integral_constant<int, 2>{}, bf[0]);
-    asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
-    touch(bf[1]);
-    mfma_pair(std::integral_constant<int, 1>{}, bf[1]);
-    read_pair(std::integral_constant<int, 3>{}, bf[1]);
-    asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
-    touch(bf[0]);
-    mfma_pair(std::integral_constant<int, 2>{}, bf[0]);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    touch(bf[1]);
-    mfma_pair(std::integral_constant<int, 3>{}, bf[1]);
-
-  }
-  {  // the tile's epilogue
-      const int64_t m0 = (int64_t)(t0 + ti * grid) * BM + 32 * wave;
-      if constexpr (BIGSMALL) {  // one column block at a time: the two accumulator sets fill the AGPRs
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          nerf_f32x16 v[1][1] = {{acc[0][b] + accs[b]}};
-          ntb_epilogue<1, 1, 32, 32, EPI, 0>(v, m0, 32 * b, li, lh, bias, C, ldc, mbits, ldmb, mbits_out);
-        }
-      } else {
-        ntb_epilogue<1, TN, 32, 32 * TN, EPI, 0>(acc, m0, 0, li, lh, bias, C, ldc, mbits, ldmb, mbits_out);
-      }
-  }
-  }
-}

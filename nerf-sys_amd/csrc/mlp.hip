@@ -285,31 +285,9 @@ int wgrad(const float* G, int ldg, const float* X, int ldx, int tensor_w, const 
 // split-product (bf16 x 6) forms of the trunk GEMMs (gemm_x6.hpp)
 template <int EPI>
 int nt_x6(const float* A, int lda, const nerf_bf16* Bp, int ldb, int64_t bplane, const float* bias, float* C, int ldc,
-          const uint32_t* mbits, uint32_t* mbits_out, int64_t M, int N, int K, hipStream_t st, bool ring) {
+          const uint32_t* mbits, uint32_t* mbits_out, int64_t M, int N, int K, hipStream_t st) {
   if (M % 128 || N % 128 || K % 32 || lda % 4 || ldb % 8) return NERF_E_ARG;
   const int ntn = N / 128;
-  if (ring && N == 256 && K % 32 == 0 && lda % 4 == 0 && ldb % 8 == 0) {  // K % 32: whole slab pairs
-    // persistent LDS-DMA ring (gemm_x6.hpp gemm_nt_x6r): one workgroup per CU
-    static int n_cu = 0;
-    if (!n_cu) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
-    }
-    if constexpr (EPI == EPI_MASK) {  // input gradients: split accumulators, one wave per SIMD
-      if (M % 128 == 0) {
-        const int nt = (int)(M / 128);
-        gemm_nt_x6r_kernel<EPI, 4, true><<<nt < n_cu ? nt : n_cu, 256, 0, st>>>(A, lda, Bp, ldb, bplane, bias, C, ldc,
-                                                                               mbits, N / 32, mbits_out, K, nt);
-        return NERF_OK;
-      }
-    } else if (M % 256 == 0) {
-      const int nt = (int)(M / 256);
-      gemm_nt_x6r_kernel<EPI, 8, false><<<nt < n_cu ? nt : n_cu, 512, 0, st>>>(A, lda, Bp, ldb, bplane, bias, C, ldc,
-                                                                              mbits, N / 32, mbits_out, K, nt);
-      return NERF_OK;
-    }
-  }
 #ifndef NERF_X6_SQUARE  // (64 NW) x 128 tiles of 64 x 128 waves (gemm_nt_x6w); NERF_X6_SQUARE: 128 x 128 (A/B builds)
 #ifndef NERF_X6W_BK
 #define NERF_X6W_BK 32
@@ -396,9 +374,8 @@ extern "C" int64_t nerf_mlp_workspace_bytes(int64_t M, int training) {
 extern "C" int nerf_mlp_fwd_ex(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws,
                                int64_t ws_bytes, int training, int flags, hipEvent_t* ev, hipStream_t st) {
   NERF_CHECK_ARG(w && x_d && rgb_sigma && ws && M >= 0);
-  if (flags & ~(NERF_MLP_NATIVE_FP32 | NERF_MLP_X6_TILED)) return NERF_E_ENUM;
+  if (flags & ~NERF_MLP_NATIVE_FP32) return NERF_E_ENUM;
   const bool native = flags & NERF_MLP_NATIVE_FP32;
-  const bool ring = !(flags & NERF_MLP_X6_TILED);
   if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(rgb_sigma)) return NERF_E_ALIGN;
   const WS W = carve(ws, M, training);
   if (ws_bytes < W.bytes) return NERF_E_WORKSPACE;
@@ -427,7 +404,7 @@ extern "C" int nerf_mlp_fwd_ex(const float* w, const float* x_d, int64_t M, floa
                             training ? W.MB[i] : nullptr, Mp, 256, KPAD[i], st));
     else
       TRY(nt_x6<EPI_BIAS_RELU>(in, ld_in, W.WPf + x6_fwd_off(i), KPAD[i], 256 * (int64_t)KPAD[i], Wt(2 * i + 1), out,
-                               ld_out, nullptr, training ? W.MB[i] : nullptr, Mp, 256, KPAD[i], st, ring));
+                               ld_out, nullptr, training ? W.MB[i] : nullptr, Mp, 256, KPAD[i], st));
     if (ev) (void)hipEventRecord(ev[2 * i + 1], st);
     in = out;
     ld_in = ld_out;
@@ -486,9 +463,8 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
                  int64_t ws_bytes, int flags, hipEvent_t* ev, hipStream_t st, hipStream_t stw, hipEvent_t* sync) {
   NERF_CHECK_ARG(w && d_rgb_sigma && d_w && ws && M >= 0);
   NERF_CHECK_ARG(!stw || sync);
-  if (flags & ~(NERF_MLP_NATIVE_FP32 | NERF_MLP_NATIVE_DGRAD | NERF_MLP_X6_TILED)) return NERF_E_ENUM;
+  if (flags & ~(NERF_MLP_NATIVE_FP32 | NERF_MLP_NATIVE_DGRAD)) return NERF_E_ENUM;
   const bool native = flags & NERF_MLP_NATIVE_FP32;
-  const bool ring = !(flags & NERF_MLP_X6_TILED);
   // input gradients: split products with the small terms in their own accumulators (gemm_nt_x6w BIGSMALL) unless
   // NERF_MLP_NATIVE_DGRAD keeps them on the fp32 MFMA
   const bool split_dgrad = !native && !(flags & NERF_MLP_NATIVE_DGRAD);
@@ -578,7 +554,7 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
         TRY(nt<EPI_MASK>(dcur, 256, WTi[i], 256, nullptr, dnext, 256, W.MB[i - 1], nullptr, Mp, 256, 256, st));
       else
         TRY(nt_x6<EPI_MASK>(dcur, 256, W.WPb + 3 * 65536 * (int64_t)(i - 1), 256, 65536, nullptr, dnext, 256,
-                            W.MB[i - 1], nullptr, Mp, 256, 256, st, ring));
+                            W.MB[i - 1], nullptr, Mp, 256, 256, st));
       if (ev) (void)hipEventRecord(ev[4 * i + 3], st);
       float* t = dcur; dcur = dnext; dnext = t;
     }

@@ -151,7 +151,6 @@ def _events_arg(events):
 # fp32 GEMM engine flags (include/nerf_amd.h): 0 = bf16 split products (default), NATIVE_FP32 = fp32 MFMA kernels
 MLP_NATIVE_FP32 = 1
 MLP_NATIVE_DGRAD = 2  # backward only: input-gradient GEMMs on the fp32 MFMA (default: split, small-term accumulators)
-MLP_X6_TILED = 4  # split forward / input-gradient GEMMs as register-staged tiles instead of the persistent DMA ring
 
 
 def mlp_fwd(w_packed, x_d, ws, training, out=None, events=None, precision="fp32", bf16_flags=0, fp32_flags=0):
@@ -165,7 +164,7 @@ def mlp_fwd(w_packed, x_d, ws, training, out=None, events=None, precision="fp32"
                                       int(bf16_flags), _events_arg(events), stream()), "nerf_mlp_fwd_bf16")
         return out
     check(lib().nerf_mlp_fwd_ex(ptr(w_packed), ptr(x_d), M, ptr(out), ptr(ws), ws.numel(), int(training),
-                                int(fp32_flags) & (MLP_NATIVE_FP32 | MLP_X6_TILED),  # MLP_NATIVE_DGRAD: backward only
+                                int(fp32_flags) & MLP_NATIVE_FP32,  # MLP_NATIVE_DGRAD is a backward-only flag
                                 _events_arg(events), stream()), "nerf_mlp_fwd_ex")
     return out
 

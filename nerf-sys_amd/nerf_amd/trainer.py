@@ -90,10 +90,8 @@ class NeRFTrainer:
         self.bf16_flags = int(bf16_flags)  # K.BF16_LAYERED_* (A/B runs of the layered bf16 launches)
         # fp32 trunk GEMMs: "split" = every trunk GEMM as bf16 piece products (gemm_x6.hpp; the input gradients with
         # separate small-term accumulators), the default; "native_dgrad" = input gradients on the fp32 MFMA;
-        # "native" = every GEMM on the fp32 MFMA kernels; "split_tiled" = the split engine with the register-staged
-        # tiled forward / input-gradient kernels instead of the persistent DMA ring (bitwise the same results)
-        flags = {"split": 0, "native_dgrad": K.MLP_NATIVE_DGRAD, "native": K.MLP_NATIVE_FP32,
-                 "split_tiled": K.MLP_X6_TILED}
+        # "native" = every GEMM on the fp32 MFMA kernels
+        flags = {"split": 0, "native_dgrad": K.MLP_NATIVE_DGRAD, "native": K.MLP_NATIVE_FP32}
         if fp32_gemm not in flags:
             raise ValueError(f"fp32_gemm must be one of {sorted(flags)}, got {fp32_gemm!r}")
         self.fp32_gemm = fp32_gemm

@@ -115,28 +115,3 @@ def test_split_backward_as_accurate_as_native(K, M):
         assert e["split"] <= 2.0 * e["native"] + 1e-7, f"tensor {t}: split {e['split']:.3e} native {e['native']:.3e}"
         assert e["native_dgrad"] <= 2.0 * e["native"] + 1e-7, (t, e)
 
-
-@pytest.mark.parametrize("M", [1, 300, 40001, 262144, 786432])
-def test_ring_kernels_match_tiled_bitwise(K, M):
-    """The persistent LDS-DMA ring kernels (gemm_nt_x6r: forward, and the input gradients with small-term accumulators)
-    run every output's MFMAs in the register-staged tiled kernels' order (gemm_nt_x6w; NERF_MLP_X6_TILED): the forward
-    output, every saved activation and the packed weight gradient are bitwise equal.  M covers one partial tile
-    (M = 1, 300), fewer tiles than CUs (40001) and several tiles per workgroup (the C2 coarse / fine sizes)."""
-    net, p = _params(7)
-    w = net.packed().detach().contiguous()
-    g = torch.Generator().manual_seed(M + 7)
-    x = torch.cat([torch.rand(M, 3, generator=g) * 3 - 1.5,
-                   torch.nn.functional.normalize(torch.randn(M, 3, generator=g), dim=-1)], -1).to(DEV)
-    gup = torch.randn(M, 4, generator=g).to(DEV) * 1e-3
-    res = {}
-    for name, flags in (("ring", 0), ("tiled", K.MLP_X6_TILED)):
-        ws = K.mlp_workspace(M, True, DEV)
-        ws.fill_(0)
-        out = K.mlp_fwd(w, x, ws, True, fp32_flags=flags).clone()
-        acts = ws.clone()
-        dw = K.mlp_bwd(w, M, gup, ws, fp32_flags=flags).clone()
-        res[name] = (out, acts, dw)
-    assert torch.equal(res["ring"][0], res["tiled"][0]), "forward output differs"
-    assert torch.equal(res["ring"][1], res["tiled"][1]), "saved activations differ"
-    assert torch.equal(res["ring"][2], res["tiled"][2]), "weight gradient differs"
-    assert torch.isfinite(res["ring"][2]).all()

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Where the split NT GEMMs' wave cycles go: one PMC pass per fp32 engine (ring = default, split_tiled) over a short C2
+# Where the split NT GEMMs' wave cycles go: one PMC pass per fp32 engine (--fp32-gemm: split = default, native_dgrad, native) over a short C2
 # bench: parked (SQ_WAIT_ANY: s_waitcnt / barrier), issue-stalled (SQ_WAIT_INST_ANY, LDS part SQ_WAIT_INST_LDS),
 # issuing (SQ_ACTIVE_INST_ANY), MFMA busy and clock per kernel (tools/gemm_pmc_parse.py).
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-for v in ${VARIANTS:-split split_tiled}; do
+for v in ${VARIANTS:-split}; do
   OUT=gpurun_out/pmc_split_$v
   mkdir -p $OUT
   timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE \
