@@ -362,9 +362,6 @@ __global__ __launch_bounds__(64 * NW, BIGSMALL ? 1 : 8 / NW) void gemm_nt_x6w_ke
               for (int b = 0; b < 2; ++b)
                 bf[b][p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + ((2 * bp + b) * 32 + li) * LS + 16 * ks +
                                                                  8 * lh);
-#ifdef NERF_X6_PRIO
-            __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
             for (int t = 0; t < 6; ++t)
 #pragma unroll
@@ -383,9 +380,6 @@ __global__ __launch_bounds__(64 * NW, BIGSMALL ? 1 : 8 / NW) void gemm_nt_x6w_ke
                                                                                acc[a][2 * bp + b], 0, 0, 0);
                   }
                 }
-#ifdef NERF_X6_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
           }
         }
         X6W_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);  // set j consumed: slab kt + 2 streams into it
