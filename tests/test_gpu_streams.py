@@ -69,7 +69,8 @@ def test_trainer_split_wgrad_equals_inline(K):
         res[split] = out
     for s in range(3):
         a, b = res[False][s], res[True][s]
-        # the loss scalar is summed by per-ray atomics (order not fixed run to run); the gradients do not depend on it
-        assert abs(a[0] - b[0]) <= 1e-6 * abs(a[0]), (s, a[0], b[0])
+        # the loss scalar is summed by per-ray float atomics (order not fixed run to run: 512 rays of ~5e-4 each, so
+        # a few fp32 ulps of the sum apart, 2.7e-7 relative seen on MI355X); the gradients do not depend on it
+        assert abs(a[0] - b[0]) <= 1e-5 * abs(a[0]), (s, a[0], b[0])
         assert torch.equal(a[1], b[1]), f"step {s}: gradient buffers differ"
         assert torch.equal(a[2], b[2]), f"step {s}: parameters differ"
