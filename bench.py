@@ -369,7 +369,7 @@ def roofline(tm, bf16, overlap, bf16_flags=0, split=False):
         names = {"fwd": "gemm_nt16 fwd (fp32 16x16x4, bias+ReLU)", "wgrad": "gemm_wgrad (fp32 32x32x2, split-M)",
                  "dgrad": "gemm_nt16 dgrad (fp32 16x16x4, ReLU mask)"}
         nt_f, nt_d = "gemm_nt_x6w fwd (fp32 as 6 bf16 split products, 512x128 tiles, bias+ReLU)", \
-            "gemm_nt_x6w<BIGSMALL> dgrad (fp32 as 6 bf16 split products, small-term accumulators)"
+            "gemm_nt_x6w<BIGSMALL, 32-row waves> dgrad (fp32 as 6 bf16 split products, small-term accumulators, 256x128 tiles)"
         if "fwd" in split_cls:
             names["fwd"] = nt_f
         if "wgrad" in split_cls:

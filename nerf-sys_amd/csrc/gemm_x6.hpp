@@ -230,9 +230,11 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_x6_kernel(const float* __re
 // (2 x 4 MFMA tiles), so every activation row is loaded and split by exactly one wave (gemm_nt_x6's 64 x 64 waves
 // split each row twice) and the split VALU work per MFMA halves.  Weight planes [3][128][BK + 8] bf16
 // double-buffered in LDS; B fragments are read per pair of column blocks so that at most 24 VGPRs of them are live.
-// Requirements as gemm_nt_x6 with M % (64 NW) == 0 and K % BK == 0.  Default BK = 32, NW = 8 (512 x 128 tiles, one
+// Requirements as gemm_nt_x6 with M % (32 TM NW) == 0 and K % BK == 0.  Default BK = 32, NW = 8 (512 x 128 tiles, one
 // workgroup per CU): C2 step 204.0k -> 207.5-209.0k rays/s over BK = 16, NW = 4 (fwd / dgrad 0.65 -> 0.63 ms).
-template <int EPI, int BK = 32, int NW = 8, bool BIGSMALL = false>
+// TM = 1 (32-row waves; the BIGSMALL input gradients, whose 256 accumulator registers per 64-row wave allowed only one
+// wave per SIMD): 256 x 128 tiles at two waves per SIMD.
+template <int EPI, int BK = 32, int NW = 8, bool BIGSMALL = false, int TM = 2>
 __global__ __launch_bounds__(64 * NW, BIGSMALL ? 1 : 8 / NW) void gemm_nt_x6w_kernel(const float* __restrict__ A, int lda,
                                                                      const nerf_bf16* __restrict__ Bp, int ldb,
                                                                      int64_t bplane, const float* __restrict__ bias,
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(64 * NW, BIGSMALL ? 1 : 8 / NW) void gemm_nt_x6w_ke
                                                                      uint32_t* __restrict__ mbits_out, int K,
                                                                      int n_ntiles) {
   constexpr int NT = 64 * NW;                     // threads
-  constexpr int BM = 64 * NW, BN = 128, WTM = 64, WTN = 128, TM = 2, TN = 4;
+  constexpr int WTM = 32 * TM, BM = WTM * NW, BN = 128, WTN = 128, TN = 4;
   constexpr int KS = BK / 16, CPR = BK / 8;       // MFMA k-steps / 16-B weight chunks per row, per slab
   constexpr int BCH = 3 * BN * CPR / NT;          // weight chunks per thread per slab
   static_assert((3 * BN * CPR) % NT == 0 && (BN * CPR) % NT == 0, "weight staging");
@@ -269,8 +271,8 @@ __global__ __launch_bounds__(64 * NW, BIGSMALL ? 1 : 8 / NW) void gemm_nt_x6w_ke
       _Pragma("unroll") for (int hf = 0; hf < 2; ++hf)                                                   \
         ra[set_][a][ks][hf] = *reinterpret_cast<const float4*>(At + aoff[a] + (k0_) + 16 * ks + 4 * hf);
   // ASMB: the weight-slab loads as inline asm.  The compiler sinks plain loads to just before their LDS writes, which
-  // exposes an L2 round trip per slab; at one wave per SIMD (BIGSMALL) nothing else covers it (input-gradient GEMM
-  // 0.78 -> 0.72 ms per fine layer on MI355X).  Issued after the wave's activation registers of the slab have landed
+  // exposes an L2 round trip per slab; in the BIGSMALL input-gradient kernel that cost 0.78 -> 0.72 ms per fine layer
+  // (64-row waves, one per SIMD; measured on MI355X).  Issued after the wave's activation registers of the slab have landed
   // (the touch below), so the compiler's counted waits on its own activation loads never wait on these as well.  At two
   // waves per SIMD the extra live registers spill (fwd 0.62 -> 0.65 ms): plain loads there.
   constexpr bool ASMB = BIGSMALL;
@@ -295,8 +297,9 @@ __global__ __launch_bounds__(64 * NW, BIGSMALL ? 1 : 8 / NW) void gemm_nt_x6w_ke
   }
 #define X6W_BWAIT()                                                                                       \
   if constexpr (ASMB) {                                                                                   \
-    static_assert(TM * KS * 2 == 8, "vmcnt below counts the 8 activation loads issued after the weight loads"); \
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                                                     \
+    static_assert(TM * KS * 2 == 8 || TM * KS * 2 == 4, "vmcnt: the activation loads after the weight loads"); \
+    if constexpr (TM * KS * 2 == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                    \
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                                                \
     _Pragma("unroll") for (int i = 0; i < BCH; ++i) {                                                    \
       x6_f32x4 v_ = __builtin_bit_cast(x6_f32x4, rb[i]);                                                  \
       asm volatile("" : "+v"(v_));                                                                        \
