@@ -234,8 +234,8 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_x6_kernel(const float* __re
 // workgroup per CU): C2 step 204.0k -> 207.5-209.0k rays/s over BK = 16, NW = 4 (fwd / dgrad 0.65 -> 0.63 ms).
 // TM = 1 (32-row waves; the BIGSMALL input gradients, whose 256 accumulator registers per 64-row wave allowed only one
 // wave per SIMD): 256 x 128 tiles at two waves per SIMD.
-template <int EPI, int BK = 32, int NW = 8, bool BIGSMALL = false, int TM = 2>
-__global__ __launch_bounds__(64 * NW, BIGSMALL ? 1 : 8 / NW) void gemm_nt_x6w_kernel(const float* __restrict__ A, int lda,
+template <int EPI, int BK = 32, int NW = 8, bool BIGSMALL = false, int TM = 2, int MINW = (BIGSMALL ? 1 : 8 / NW)>
+__global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float* __restrict__ A, int lda,
                                                                      const nerf_bf16* __restrict__ Bp, int ldb,
                                                                      int64_t bplane, const float* __restrict__ bias,
                                                                      float* __restrict__ C, int ldc,
@@ -274,8 +274,9 @@ __global__ __launch_bounds__(64 * NW, BIGSMALL ? 1 : 8 / NW) void gemm_nt_x6w_ke
   // exposes an L2 round trip per slab; in the BIGSMALL input-gradient kernel that cost 0.78 -> 0.72 ms per fine layer
   // (64-row waves, one per SIMD; measured on MI355X).  Issued after the wave's activation registers of the slab have landed
   // (the touch below), so the compiler's counted waits on its own activation loads never wait on these as well.  At two
-  // waves per SIMD the extra live registers spill (fwd 0.62 -> 0.65 ms): plain loads there.
-  constexpr bool ASMB = BIGSMALL;
+  // waves per SIMD the extra live registers spill (fwd 0.62 -> 0.65 ms): plain loads there.  32-row waves (TM = 1) have
+  // the registers: a forward of that shape went 0.76 -> 0.655 ms with them, still behind 0.63 ms for 64-row waves.
+  constexpr bool ASMB = BIGSMALL || TM == 1;
 #define X6W_BLOAD(k0_)                                                                                    \
   if constexpr (ASMB) {                                                                                   \
     _Pragma("unroll") for (int a = 0; a < TM; ++a)                                                       \
@@ -339,9 +340,9 @@ __global__ __launch_bounds__(64 * NW, BIGSMALL ? 1 : 8 / NW) void gemm_nt_x6w_ke
 #pragma unroll
     for (int j = 0; j < 2; ++j) {  // slab kt = kt0 + j: LDS buffer j, activation register set j
       const int kt = kt0 + j;
-      // BIGSMALL: nk is even (host: K % (2 BK) == 0), so no guard — every path into the loop header then has the same
+      // ASMB: nk is even (host: K % (2 BK) == 0), so no guard — every path into the loop header then has the same
       // loads in flight and the compiler's counted wait there stays vmcnt(8) instead of draining to vmcnt(0)
-      if (BIGSMALL || kt < nk) {
+      if (ASMB || kt < nk) {
         X6W_BLOAD((kt + 1 < nk ? kt + 1 : kt) * BK);
         const nerf_bf16* S = smem + j * 3 * PL;
 #pragma unroll
