@@ -25,4 +25,4 @@ done
 PMC_OUT=$O/pmc_fp32 PMC_BENCH_ARGS="--no-dropin --no-other-precision --no-native-ref" bash tools/pmc_traffic.sh > $O/pmc_fp32.txt 2>&1 || { tail -20 $O/pmc_fp32.txt; exit 1; }
 PMC_OUT=$O/pmc_bf16 PMC_PRECISION=bf16fused PMC_BENCH_ARGS="--precision bf16 --no-dropin --no-other-precision" bash tools/pmc_traffic.sh > $O/pmc_bf16.txt 2>&1 || { tail -20 $O/pmc_bf16.txt; exit 1; }
 PMC_OUT=$O/pmc_mfma PMC_BENCH_ARGS="--no-other-precision --no-native-ref" bash tools/pmc_mfma_bench.sh > $O/pmc_mfma.txt 2>&1 || { tail -20 $O/pmc_mfma.txt; exit 1; }
-tail -3 $O/pmc_fp32.txt $O/pmc_bf16.txt $O/pmc_mfma.txt
+for f in $O/pmc_fp32.txt $O/pmc_bf16.txt $O/pmc_mfma.txt; do tail -n 3 $f; done
