@@ -678,6 +678,11 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
       }
 #pragma unroll
       for (int bp = 0; bp < TN / 2; ++bp) {  // column-block pairs: 2 x 3 X fragments live
+        // the next slab's split + LDS stores go between the two column-block pairs (unconditionally: past the last
+        // slab they fill the free buffer), and the group barriers below interleave their VALU work one MFMA at a time
+        // with the second pair's MFMAs instead of leaving it between the last MFMA and the barrier: 0.52 -> 0.47 ms
+        // per fine layer on MI355X (profiles/r03/x6_wgrad_interleave_ab.txt), bitwise the same results
+        if (bp == 1) WX6W_SSTORE((j + 1) & 1, (j + 1) & 1);
         nerf_bf16x8 bf[2][3];
 #pragma unroll
         for (int pc = 0; pc < 3; ++pc)
@@ -692,8 +697,16 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
             for (int b = 0; b < 2; ++b)
               acc[a][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][X6_PA[t]], bf[b][X6_PB[t]],
                                                                          acc[a][2 * bp + b], 0, 0, 0);
+        if (bp == 1) {  // the pair's fragment reads first, then one MFMA per ~4 VALU of the split, LDS writes spread
+          __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+          for (int q = 0; q < 24; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+            if (q & 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+          }
+        }
       }
-      if (it + 1 < nit) WX6W_SSTORE((j + 1) & 1, (j + 1) & 1);
       __syncthreads();
     }
   }
