@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_x6_kernel(const float* __re
             for (int b = 0; b < TN; ++b)
               bf[b][p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + (wn * WTN + b * 32 + li) * LS + 16 * ks +
                                                                8 * lh);
-          X6_MFMA_BLOCK(acc, TM, TN, bf[b_][X6_PB[t_]], af[a_][X6_PA[t_]])
+          X6_MFMA_BLOCK(acc, TM, TN, bf[b_][X6F_PB[t_]], af[a_][X6F_PA[t_]])  // the forward order (as gemm_nt_x6w)
         }
         // set j is consumed: slab kt + 2 streams into it while slab kt + 1 is computed
         X6_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);
