@@ -49,12 +49,11 @@ __device__ __forceinline__ void x6_split4(const float4 v, uint2& h, uint2& m, ui
 // chain on one accumulator (a dependent 32x32x16 MFMA waits for its predecessor's result).
 __device__ constexpr int X6_PA[6] = {2, 1, 0, 1, 0, 0};
 __device__ constexpr int X6_PB[6] = {0, 1, 2, 0, 1, 0};
-// gemm_nt_x6w without small-term accumulators (the forward): the same six terms, still the three 2^-16 products first,
-// but hi.lo leading, so a k-step's first MFMAs need only the activation's hi piece (the first product of its split
-// chain) and start while mid / lo are still being computed: 0.635 -> 0.629 ms per fine layer on MI355X
-// (profiles/r03/x6_fwd_term_order_ab.txt; tests/test_gpu_split_gemm.py accuracy unchanged)
-__device__ constexpr int X6F_PA[6] = {0, 2, 1, 1, 0, 0};
-__device__ constexpr int X6F_PB[6] = {2, 0, 1, 0, 1, 0};
+// the forward kernels' order: the same as X6_PA / X6_PB (lo.hi first).  A hi.lo-first order let a k-step's first
+// MFMAs overlap the rest of the activation split (0.635 -> 0.629 ms per fine layer) but moved the C2 trajectory's
+// 3000-step PSNR from 28.20 to 27.74 dB; the probe-characterised order is kept (profiles/r03/x6_fwd_term_order_ab.txt)
+__device__ constexpr int X6F_PA[6] = {2, 1, 0, 1, 0, 0};
+__device__ constexpr int X6F_PB[6] = {0, 1, 2, 0, 1, 0};
 // acc_[TM_][TN_] += over the six terms; MFMA(first_, second_) operands: NT passes (B fragment, A fragment) so the
 // accumulator is C^T (gemm_bf16.hpp); the weight gradient passes (G^T fragment, X fragment)
 #ifndef NERF_X6_TERMS  // ablation builds only (tools/build_exp.sh): fewer terms -> wrong results, MFMA cost probe
