@@ -549,8 +549,17 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_x6_kernel(const float* __re
         }
     }
     // A = G^T (rows n, piece X6_PA), B = X (columns k, piece X6_PB); P itself is accumulated (not transposed)
+    // the next slab's split + LDS stores interleaved with this slab's MFMAs (as gemm_wgrad_x6w; unconditional: past the
+    // last slab they fill the free buffer): C2 208.8k -> 209.6k rays/s on one box, bitwise the same
+    // (profiles/r03/x6_wgrad_interleave_ab.txt)
+    WX6_SSTORE((j + 1) % PF, (j + 1) & 1);
     X6_MFMA_BLOCK(acc, TM, TN, af[a_][X6_PA[t_]], bf[b_][X6_PB[t_]])
-    if (it + 1 < nit) WX6_SSTORE((j + 1) % PF, (j + 1) & 1);
+#pragma unroll
+    for (int q = 0; q < 6 * TM * TN; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+    }
     __syncthreads();
    }
   }
