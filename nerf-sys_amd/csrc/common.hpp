@@ -12,6 +12,10 @@ static inline int nerf_launch_status() {
   return e == hipSuccess ? NERF_OK : (int)e;
 }
 
+// A HIP runtime call's result as the C-ABI int convention (include/nerf_amd.h: 0 ok, <0 NERF_E_*, >0 the hipError_t
+// passed through — hipError_t values are positive, so they never collide with a NERF_E_* code).
+static inline int nerf_hip_status(hipError_t e) { return e == hipSuccess ? NERF_OK : (int)e; }
+
 #define NERF_CHECK_ARG(cond) \
   do {                       \
     if (!(cond)) return NERF_E_ARG; \

@@ -477,10 +477,10 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
   if (ws_bytes < W.bytes) return NERF_E_WORKSPACE;
   hipStream_t sw = two ? stw : st;  // the weight-gradient stream
   auto handoff = [&](int k) -> int {  // sw waits for everything issued on st so far
-    if (!two) return hipSuccess;
+    if (!two) return NERF_OK;
     hipError_t e = hipEventRecord(sync[k], st);
     if (e == hipSuccess) e = hipStreamWaitEvent(stw, sync[k], 0);
-    return (int)e;
+    return nerf_hip_status(e);
   };
   const Layout& L = layout();
   if (M == 0) {
@@ -562,8 +562,8 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
     }
   }
   if (two) {  // join: the split reduce reads every weight-gradient slab
-    TRY((int)hipEventRecord(sync[9], stw));
-    TRY((int)hipStreamWaitEvent(st, sync[9], 0));
+    TRY(nerf_hip_status(hipEventRecord(sync[9], stw)));
+    TRY(nerf_hip_status(hipStreamWaitEvent(st, sync[9], 0)));
   }
   const int64_t n4 = L.total / 4;
   reduce_splits2_kernel<<<(unsigned)nerf_cdiv(n4, 256), 256, 0, st>>>(W.partial, L.total, W.S, d_w, n4, accumulate,

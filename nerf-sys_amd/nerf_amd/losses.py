@@ -55,6 +55,24 @@ def compute_mse_loss(P, model, data, params=None, active_module=None, reduction=
     return loss
 
 
+def compute_fim_loss(P, model, data, params=None, active_module=None, *, grad_buffer=None, update_fisher=False,
+                     clamp_factor=5, **_):
+    """nerfs/losses.py:35-151 as the reference runs it: one render_rays pass (P.ray_samples, no importance pass) and
+    the per-ray MSE mean (:67-73) — which the reference returns, because no module defines ``fisher_store`` /
+    ``fim_loss`` (:75-78).  ``model.submodules[active_module]`` is resolved first, as the reference
+    does (:75), so a call without an active module fails there too.  A model that does carry a Fisher store is refused:
+    the Fisher-weighted branch (:79-151) is out of scope."""
+    gt_rgb, rays = data["rgbs"], data["rays"]
+    pred = render_rays(model, rays, ray_samples=P.ray_samples, params=params, active_module=active_module,
+                       chunk=P.chunk_points)[0]
+    a, b = color_space_transformer(pred, gt_rgb, getattr(P, "color_space", "linear"))
+    base_loss = F.mse_loss(a, b, reduction="none").mean(dim=-1).mean()
+    expert_module = model.submodules[active_module]  # noqa: F841  (losses.py:75)
+    if not hasattr(model, "fisher_store") or not hasattr(model, "fim_loss"):
+        return base_loss
+    raise NotImplementedError("the Fisher-weighted loss (nerfs/losses.py:79-151) is out of scope (SURVEY §2 row 4)")
+
+
 def psnr(mse: float) -> float:
     import math
     return -10.0 * math.log10(max(float(mse), 1e-8))

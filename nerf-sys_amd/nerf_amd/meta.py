@@ -21,7 +21,7 @@ from typing import List, Optional
 import torch
 
 from ._lib import check, lib, ptr, stream
-from .losses import compute_mse_loss
+from .losses import compute_fim_loss, compute_mse_loss
 
 
 def _ptr_array(tensors):
@@ -66,10 +66,10 @@ def sgd_update(fast: "OrderedDict[str, torch.Tensor]", grads, inner_lr: float) -
 
 
 def compute_loss(P, model, data, params=None, active_module=None, **kwargs):
-    """nerfs/losses.py:154-166 dispatcher.  The Fisher-information loss (nerfs/losses.py:35-151) is dead code in the
-    reference (no module defines ``fisher_store``; SURVEY §2 row 4, out of scope) and is refused."""
+    """nerfs/losses.py:154-166 dispatcher.  P.fim routes to compute_fim_loss, which (as in the reference, where no
+    module defines ``fisher_store``) returns the per-ray MSE mean of one render; kwargs go to it only, as there."""
     if getattr(P, "fim", False):
-        raise NotImplementedError("compute_fim_loss is out of scope (SURVEY §2 row 4); set P.fim = False")
+        return compute_fim_loss(P, model, data, params, active_module, **kwargs)
     return compute_mse_loss(P, model, data, params, active_module)
 
 

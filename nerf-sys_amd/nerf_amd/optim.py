@@ -33,7 +33,8 @@ class FlatAdam:
     they stay opt-in until an 8-GPU run covers them."""
 
     def __init__(self, groups: List[Dict], betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 grad_clip=1.0, world_size: int = 1, shard: bool = False, bucket_tables: bool = True):
+                 grad_clip=1.0, world_size: int = 1, shard: bool = False, bucket_tables: bool = True,
+                 bucket_min_numel: int = 1 << 20):
         if len(groups) > 8:
             raise ValueError("at most 8 parameter groups (nerf_adam segments)")
         params = [p for g in groups for p in g["params"]]
@@ -81,10 +82,14 @@ class FlatAdam:
         self.betas, self.eps, self.wd, self.grad_clip = betas, eps, weight_decay, grad_clip
         self.step_count = 0
         # Bucketed exchange (replicated update, world_size > 1): a parameter whose gradient a HIP backward writes in
-        # place (the Instant-NGP hash tables, 0.54 GB for four experts) is its own bucket: the backward calls
-        # _bucket_ready when it has enqueued its write, and that slice's all-reduce starts at once on the
-        # collective's stream, overlapping the rest of the backward; step() waits for the buckets and all-reduces
-        # the remaining ranges.
+        # place (the Instant-NGP hash tables, 0.54 GB for four experts) is its own bucket.  The backward calls
+        # _bucket_ready when it has enqueued its write; the all-reduces are ISSUED in one fixed bucket order on every
+        # rank (RCCL / gloo match collectives by issue order), so a bucket starts as soon as it and every bucket
+        # before it in that order are ready, overlapping the rest of the backward.  Whether an expert's backward runs
+        # at all depends on the rank's data (an expert with no samples skips it), so step() issues every bucket not
+        # yet started, in the same order, then all-reduces the ranges outside the buckets — the same collective
+        # sequence on every rank whatever its data.  The order is the reverse of the flat layout: autograd runs the
+        # experts' backward in reverse of their forward, and the groups list the experts' tables in forward order.
         self.bucket_tables = bool(bucket_tables) and self.world_size > 1 and not self.shard
         self._slices = {}
         o = 0
@@ -93,24 +98,42 @@ class FlatAdam:
             o += p.numel()
         self._inflight = []     # (handle, offset, numel) of buckets started in this step
         self.exchange_events = None
-        self._fired = set()
+        self._ready = set()
+        self._next = 0          # buckets [0, _next) of _buckets have been issued this step
+        self._buckets = []
         if self.bucket_tables:
-            for p in params:
-                if p.numel() >= (1 << 20):  # big in-place-written parameters only (tables)
-                    p._nerf_grad_ready = self._bucket_ready
+            self._buckets = [p for p in params if p.numel() >= int(bucket_min_numel)][::-1]
+            for p in self._buckets:
+                p._nerf_grad_ready = self._bucket_ready
+        # the ranges no bucket covers, fixed at construction (identical on every rank)
+        cov = sorted(self._slices[id(p)] for p in self._buckets)
+        self._rest, lo = [], 0
+        for o, k in cov + [(self.grad.numel(), 0)]:
+            if o > lo:
+                self._rest.append((lo, o))
+            lo = max(lo, o + k)
 
     def _bucket_ready(self, p):
-        import torch.distributed as dist
-        if id(p) in self._fired:
+        if id(p) in self._ready:
             raise RuntimeError("bucketed exchange: a bucketed gradient was written twice in one step")
-        self._fired.add(id(p))
-        o, k = self._slices[id(p)]
-        self._inflight.append((dist.all_reduce(self.grad[o:o + k], async_op=True), o, k))
+        self._ready.add(id(p))
+        self._issue(all_buckets=False)
+
+    def _issue(self, all_buckets):
+        import torch.distributed as dist
+        while self._next < len(self._buckets):
+            q = self._buckets[self._next]
+            if not all_buckets and id(q) not in self._ready:
+                break
+            o, k = self._slices[id(q)]
+            self._inflight.append((dist.all_reduce(self.grad[o:o + k], async_op=True), o, k))
+            self._next += 1
 
     def zero_grad(self):
         if self._inflight:
             raise RuntimeError("zero_grad with bucketed all-reduces in flight (call step() first)")
-        self._fired.clear()
+        self._ready.clear()
+        self._next = 0
         self.grad.zero_()
         lo, hi = self.grad.data_ptr(), self.grad.data_ptr() + self.grad.numel() * 4
         for p in self.params:  # autograd must keep accumulating into the flat views
@@ -119,22 +142,22 @@ class FlatAdam:
 
     def allreduce_grads(self):
         """Data parallel (as for the vanilla step): ONE all-reduce of the flat gradient buffer, then
-        the mean over ranks (each rank's loss is its local-batch mean) — the gradient DDP would produce."""
+        the mean over ranks (each rank's loss is its local-batch mean) — the gradient DDP would produce.  With
+        buckets: the buckets not started during the backward, in the fixed order, then the uncovered ranges."""
         if self.world_size > 1:
             ev = self.exchange_events  # optional (start, end) torch.cuda.Events: the exchange's exposed tail
             if ev is not None:
                 ev[0].record()
-            if self._inflight:
+            if self._buckets:
                 import torch.distributed as dist
-                done = sorted((o, k) for _, o, k in self._inflight)
+                self._issue(all_buckets=True)
                 for h, _, _ in self._inflight:
                     h.wait()  # orders the current stream after the collective (no host sync on RCCL)
                 self._inflight = []
-                lo = 0
-                for o, k in done + [(self.grad.numel(), 0)]:  # the ranges no bucket covered
-                    if o > lo:
-                        dist.all_reduce(self.grad[lo:o])
-                    lo = max(lo, o + k)
+                self._ready.clear()
+                self._next = 0
+                for lo, hi in self._rest:
+                    dist.all_reduce(self.grad[lo:hi])
             else:
                 allreduce_flat(self.grad, self.world_size)
             if ev is not None:

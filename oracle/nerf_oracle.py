@@ -228,32 +228,60 @@ def init_vanilla_params(seed=0, dtype=torch.float32):
     return p
 
 
-def _lin(x, p, name):
-    """models/metamodule/metamodule.py:140-156 — out = x @ W^T + b."""
+def _f16(x):
+    return x.to(torch.float16).to(x.dtype)
+
+
+class _MatmulF16(torch.autograd.Function):
+    """``x.matmul(W.t())`` inside ``torch.autocast(float16)``: both operands cast to fp16 (matmul is on autocast's
+    lower-precision list), fp32 accumulation, fp16 output; the backward's two GEMMs take the fp16 gradient and return
+    fp16 results, which the autocast cast nodes hand back as fp32 (x, W are fp32 tensors)."""
+
+    @staticmethod
+    def forward(ctx, x, W):
+        x16, W16 = _f16(x), _f16(W)
+        ctx.save_for_backward(x16, W16)
+        return _f16(x16.matmul(W16.t()))
+
+    @staticmethod
+    def backward(ctx, g):
+        x16, W16 = ctx.saved_tensors
+        g16 = _f16(g)
+        return _f16(g16.matmul(W16)), _f16(g16.t().matmul(x16))
+
+
+def _lin(x, p, name, amp=None):
+    """models/metamodule/metamodule.py:140-156 — out = x @ W^T + b.  amp="fp16" restates the reference's
+    autocast(float16) numerics (configs/train.json "use_amp"): the matmul in fp16 (_MatmulF16), then the fp32 bias
+    added — an fp16 (M,N) tensor plus an fp32 (N,) tensor promotes to fp32, so every layer output, the ReLU and the
+    sigma head's trunc_exp input stay fp32 (trunc_exp clamps at 88.72, not fp16's 11.09; pinned by the imported
+    reference in tests/golden/amp.npz)."""
+    if amp == "fp16":
+        return _MatmulF16.apply(x, p[name + ".weight"]) + p[name + ".bias"]
     return x.matmul(p[name + ".weight"].t()) + p[name + ".bias"]
 
 
-def vanilla_density(p, x):
+def vanilla_density(p, x, amp=None):
     """models/inr/meta_vanilla.py:123-141 — skip at layer 4 is cat([h, enc]) (hidden first)."""
     enc = freq_encode(x, 10, True)
     h = enc
     for i in range(8):
         if i == 4:
             h = torch.cat([h, enc], -1)
-        h = torch.relu(_lin(h, p, f"trunk.{i}.linear"))
-    sigma = trunc_exp(_lin(h, p, "sigma_head"))
-    geo = _lin(h, p, "geo_head")
+        h = torch.relu(_lin(h, p, f"trunk.{i}.linear", amp))
+    sigma = trunc_exp(_lin(h, p, "sigma_head", amp))
+    geo = _lin(h, p, "geo_head", amp)
     return sigma, geo
 
 
-def vanilla_forward(p, x_d):
+def vanilla_forward(p, x_d, amp=None):
     """Expert contract (M,6)->(M,4) [rgb∈[0,1], σ≥0] (cf. models/inr/meta_ngp.py:226-241)
-    around MetaNeRF.forward (meta_vanilla.py:143-154, color :109-121)."""
+    around MetaNeRF.forward (meta_vanilla.py:143-154, color :109-121).  amp: see _lin."""
     x, d = x_d[:, :3], x_d[:, 3:6]
-    sigma, geo = vanilla_density(p, x)
+    sigma, geo = vanilla_density(p, x, amp)
     h = torch.cat([geo, freq_encode(d, 4, True)], -1)
-    h = torch.relu(_lin(h, p, "color_mlp.layer0.linear"))
-    rgb = torch.sigmoid(_lin(h, p, "color_mlp.color_out"))
+    h = torch.relu(_lin(h, p, "color_mlp.layer0.linear", amp))
+    rgb = torch.sigmoid(_lin(h, p, "color_mlp.color_out", amp))
     return torch.cat([rgb, sigma], -1)
 
 
@@ -293,7 +321,7 @@ def bg_default(N, policy, dtype=torch.float32):
 
 
 def render_rays(p_coarse, rays, S, training=False, u_strat=None, bg="white",
-                p_fine=None, n_importance=0, u_pdf=None):
+                p_fine=None, n_importance=0, u_pdf=None, amp=None):
     """nerfs/ray_rendering.py:290-345 (stratified) + canonical hierarchical extension.
 
     Returns (rgb, depth, weights, acc, extras) where extras holds the coarse outputs when
@@ -308,7 +336,7 @@ def render_rays(p_coarse, rays, S, training=False, u_strat=None, bg="white",
         pts = o.unsqueeze(1) + d.unsqueeze(1) * tv.unsqueeze(-1)
         dirs = d.unsqueeze(1).expand_as(pts)
         x_d = torch.cat([pts, dirs], -1).reshape(-1, 6)
-        rs = (p(x_d) if callable(p) else vanilla_forward(p, x_d)).view(N, tv.shape[1], 4)
+        rs = (p(x_d) if callable(p) else vanilla_forward(p, x_d, amp)).view(N, tv.shape[1], 4)
         return volume_render(rs, tv, bgc)
 
     out = one_pass(p_coarse, t)
@@ -364,10 +392,15 @@ class OracleTrainer:
     render → MSE (coarse + fine when hierarchical) → backward → clip_grad_norm_(1.0) → Adam.
 
     Param groups follow models/inr/meta_ngp.py:446-469 ('sigma' = trunk+heads, 'color' = colour MLP)
-    with per-group lr (common/utils.py:16-76)."""
+    with per-group lr (common/utils.py:16-76).
+
+    amp="fp16": the use_amp=True body (runtime_adapt.py:290-310) — the MLPs under the autocast(float16) restatement
+    of _lin, the loss scaled by ``loss_scale`` for the backward and the gradients unscaled (GradScaler.unscale_
+    multiplies by 1/scale) before the clip; a step whose gradients hold an inf / nan is skipped, as GradScaler.step
+    does (the returned loss is still the step's)."""
 
     def __init__(self, p_coarse, p_fine=None, lr_sigma=2e-3, lr_color=2e-3, betas=(0.9, 0.999),
-                 eps=1e-8, grad_clip=1.0, color_space="linear"):
+                 eps=1e-8, grad_clip=1.0, color_space="linear", amp=None, loss_scale=65536.0):
         self.nets = [OrderedDict((k, v.clone().requires_grad_(True)) for k, v in p_coarse.items())]
         if p_fine is not None:
             self.nets.append(OrderedDict((k, v.clone().requires_grad_(True)) for k, v in p_fine.items()))
@@ -380,17 +413,27 @@ class OracleTrainer:
                                     betas=betas, eps=eps)
         self.grad_clip = grad_clip
         self.color_space = color_space
+        self.amp = amp
+        self.loss_scale = float(loss_scale) if amp else 1.0
 
     def step(self, rays, gt, S, n_importance=0, training=True, u_strat=None, u_pdf=None, bg="white"):
         self.opt.zero_grad()
         pf = self.nets[1] if len(self.nets) > 1 else None
         rgb, depth, w, acc, ex = render_rays(self.nets[0], rays, S, training, u_strat, bg, pf,
-                                             n_importance, u_pdf)
+                                             n_importance, u_pdf, amp=self.amp)
         loss = mse_loss(rgb, gt, self.color_space)
         if n_importance > 0:
             loss = loss + mse_loss(ex["rgb_coarse"], gt, self.color_space)
-        loss.backward()
+        (loss * self.loss_scale).backward()
+        finite = True
+        if self.amp:
+            inv = 1.0 / self.loss_scale
+            for q in self.params:
+                if q.grad is not None:
+                    q.grad.mul_(inv)
+                    finite = finite and bool(torch.isfinite(q.grad).all())
         if self.grad_clip is not None:
             torch.nn.utils.clip_grad_norm_(self.params, self.grad_clip)
-        self.opt.step()
+        if finite:
+            self.opt.step()
         return float(loss.detach())

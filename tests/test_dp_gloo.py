@@ -119,3 +119,58 @@ def test_flat_adam_data_parallel_mean_gloo():
     for r in range(world):
         g0, g1 = out[r]
         assert torch.allclose(g0, torch.full((5, 3), 1.5)) and torch.allclose(g1, torch.full((7,), 3.0))
+
+
+def _bucket_worker(rank, world, port, q):
+    """Three bucketed 'tables' (bucket_min_numel 64) and one small tensor.  Rank 0's backward writes tables 2 and 0
+    (in that order), rank 1's only table 1 — as when an expert gets no samples on a rank (container.py skips its
+    backward).  The collective sequence must still match: every rank ends with the mean gradient."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "nerf-sys_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from nerf_amd.optim import FlatAdam
+    ps = [torch.nn.Parameter(torch.zeros(100)), torch.nn.Parameter(torch.zeros(5)),
+          torch.nn.Parameter(torch.zeros(80)), torch.nn.Parameter(torch.zeros(70))]
+    tables = [ps[0], ps[2], ps[3]]
+    opt = FlatAdam([{"params": ps, "lr": 1e-3}], world_size=world, bucket_min_numel=64)
+    for step in range(3):
+        opt.zero_grad()
+        fired = {0: [2, 0], 1: [1]}[rank] if step != 1 else {0: [], 1: [0, 1, 2]}[rank]
+        with torch.no_grad():
+            ps[1].grad.fill_(float(rank + 1))
+            for t in fired:
+                tables[t].grad.fill_(float(10 * (t + 1) * (rank + 1)))
+                tables[t]._nerf_grad_ready(tables[t])
+        opt.allreduce_grads()
+        q.put((rank, step, [p.grad.clone() for p in ps]))
+    dist.destroy_process_group()
+
+
+def test_flat_adam_buckets_data_dependent_firing_gloo():
+    """a bucket's all-reduce used to start from the expert's backward, so ranks whose experts got
+    different samples issued different collective sequences (hang or mismatched buffers under RCCL).  Buckets are
+    now issued in one fixed order and step() issues the ones that did not fire: any firing pattern gives every rank
+    the rank-mean gradient."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world * 3):
+        r, step, g = q.get(timeout=120)
+        got[(r, step)] = g
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for step in range(3):
+        fired = {0: [2, 0], 1: [1]} if step != 1 else {0: [], 1: [0, 1, 2]}
+        want_t = [sum(10.0 * (t + 1) * (r + 1) for r in range(world) if t in fired[r]) / world for t in range(3)]
+        for r in range(world):
+            g = got[(r, step)]
+            assert torch.allclose(g[1], torch.full((5,), 1.5)), (r, step, g[1])
+            for t, i in enumerate((0, 2, 3)):
+                assert torch.allclose(g[i], torch.full_like(g[i], want_t[t])), (r, step, t, g[i][:3], want_t[t])

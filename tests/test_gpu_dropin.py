@@ -18,7 +18,12 @@ an/pipelines/online_stage/runtime_adapt.py:286-310 —
   then two more steps' losses.
 * AMP (configs/train.json "use_amp": true): inside ``autocast(fp16)`` the expert runs the bf16 MLP kernels
   (bitwise ``nerf_mlp_fwd_bf16``), compositing stays fp32; the loop body as written with ``GradScaler`` trains,
-  its loss tracks the fp32 loop's from the same seed, and the scaler never finds an inf (its scale stays put)."""
+  its loss tracks the fp32 loop's from the same seed, and the scaler never finds an inf (its scale stays put).
+* AMP parity: the reference under autocast(float16) keeps trunc_exp's input fp32 (MetaLinear's fp32 bias promotes
+  the fp16 matmul output; tests/golden/amp.npz from the imported reference), so sigma is NOT clamped at fp16's 11.09
+  — known answers beyond +-11.09 through the drop-in expert under autocast; and the drop-in AMP hierarchical step's
+  first unscaled gradients against OracleTrainer(amp="fp16"), the CPU restatement of the reference's autocast
+  numerics pinned to that fixture (tests/test_oracle_golden.py::test_amp_*)."""
 import types
 
 import pytest
@@ -142,3 +147,71 @@ def test_reference_amp_loop_body_with_gradscaler(K):
     assert a[-10:].mean() < 0.8 * a[:5].mean(), a   # it learns
     assert (a[-10:].mean() - b[-10:].mean()).abs() <= 0.15 * b[-10:].mean(), (a[-10:].mean(), b[-10:].mean())
     assert not torch.equal(a, b)  # the AMP loop did run the bf16 kernels
+
+
+def test_amp_trunc_exp_beyond_fp16_clamp_golden(K):
+    """te16_x = [-30, -12, 0, 11, 12, 15, 30] as the sigma head's pre-activation (weights 0, bias x) under
+    autocast(float16): sigma and d sigma / d bias equal the imported reference's (tests/golden/amp.npz) — exp(x)
+    without fp16's 11.09 clamp (sigma(15) = 3.27e6), the gradient exp(x) too."""
+    from nerf_amd.vanilla import VanillaNeRF
+    from golden_io import mlp_params
+    z = load("amp")
+    x_d = load("mlp")["x_d"][:64].to(DEV)
+    for x, y, gref in zip(z["te16_x"].tolist(), z["te16_y"].tolist(), z["te16_g"].tolist()):
+        q = dict(mlp_params("w/"))
+        q["sigma_head.weight"] = torch.zeros(1, 256)
+        q["sigma_head.bias"] = torch.tensor([x])
+        net = VanillaNeRF().load_reference_state(q).to(DEV)
+        with torch.autocast("cuda", dtype=torch.float16):
+            out = net(x_d)
+        sig = out[:, 3].detach().cpu()
+        assert ((sig - y).abs() <= 1e-5 * y).all(), f"x={x}: sigma {sig[:3].tolist()} vs reference {y}"
+        net.zero_grad()
+        out[:, 3].sum().backward()
+        gb = net.sigma_head.bias.grad.item() / 64.0
+        assert abs(gb - gref) <= 1e-5 * gref, f"x={x}: d sigma / d bias {gb} vs reference {gref}"
+
+
+def test_amp_dropin_step_gradients_vs_oracle_amp(K):
+    """runtime_adapt.py:290-305 with use_amp=True on the drop-in surface (HierarchicalNeRF, compute_mse_loss,
+    GradScaler at its initial 2^16), 1024 golden rays x (64 + 128), injected jitter: the unscaled first-step
+    gradient of each net against OracleTrainer(amp="fp16") — the reference's autocast(float16) restatement — at
+    flat cosine >= 0.999 (the bar of the C3 engine test, test_gpu_convergence.py), the loss within 1e-3.  The
+    drop-in's MLP is bf16 (8-bit significands) where the reference's is fp16 (11-bit); both are printed against the
+    fp32 oracle too."""
+    from nerf_amd.losses import compute_mse_loss
+    pc, pf = O.init_vanilla_params(1), O.init_vanilla_params(2)
+    model = _model(pc, pf).train()
+    opt = _adam(model, 2e-3, 1e-3)
+    scaler = torch.amp.GradScaler("cuda")
+    P = types.SimpleNamespace(ray_samples=64, n_importance=128, chunk_points=1 << 22, color_space="linear")
+    rays = load("render")["rays"]
+    g = torch.Generator().manual_seed(23)
+    gt = torch.rand(rays.shape[0], 3, generator=g) * 0.5 + 0.25
+    us, up = torch.rand(rays.shape[0], 64, generator=g), torch.rand(rays.shape[0], 128, generator=g)
+    opt.zero_grad()
+    with torch.cuda.amp.autocast(dtype=torch.float16):
+        loss = compute_mse_loss(P, model, {"rays": rays.to(DEV), "rgbs": gt.to(DEV)}, u_strat=us.to(DEV),
+                                u_pdf=up.to(DEV))
+    scaler.scale(loss).backward()
+    scaler.unscale_(opt)
+    refs = {}
+    for amp in ("fp16", None):
+        ot = O.OracleTrainer(pc, pf, amp=amp, grad_clip=None)
+        ot.opt.step = lambda: None
+        refs[amp] = (ot.step(rays, gt, 64, n_importance=128, training=True, u_strat=us, u_pdf=up), ot)
+    lref = refs["fp16"][0]
+    assert abs(loss.item() - lref) <= 1e-3 * lref, (loss.item(), lref)
+    for k, net in enumerate((model.coarse, model.fine)):
+        names = [n for n, _ in net.named_parameters()]
+        a = torch.cat([q.grad.detach().double().cpu().flatten() for q in net.parameters()])
+        cos = {}
+        for amp, (_, ot) in refs.items():
+            b = torch.cat([ot.nets[k][n].grad.double().flatten() for n in names])
+            cos[amp] = float(a @ b / (a.norm() * b.norm()))
+        b16 = torch.cat([refs["fp16"][1].nets[k][n].grad.double().flatten() for n in names])
+        b32 = torch.cat([refs[None][1].nets[k][n].grad.double().flatten() for n in names])
+        ref_vs_fp32 = float(b16 @ b32 / (b16.norm() * b32.norm()))
+        print(f"net {k}: cos(drop-in AMP, reference AMP) {cos['fp16']:.6f}, cos(drop-in AMP, fp32) {cos[None]:.6f}, "
+              f"cos(reference AMP, fp32) {ref_vs_fp32:.6f}")
+        assert cos["fp16"] >= 0.999, f"net {k}: cosine vs the reference's AMP gradient {cos['fp16']:.5f}"

@@ -269,11 +269,20 @@ def test_task_adapt_amp_runs_bf16_kernels():
     assert any(not torch.equal(v.detach().cpu(), z[f"fast/{n}"]) for n, v in fast.items())
 
 
-def test_fim_loss_refused():
-    """compute_fim_loss (nerfs/losses.py:35-151) is dead code in the reference: P.fim raises."""
+def test_fim_loss_falls_back_to_mse():
+    """compute_loss with P.fim (nerfs/losses.py:154-166 -> compute_fim_loss :35-151): no module defines
+    ``fisher_store``, so the reference returns the per-ray MSE mean of one render (:67-78) — equal to the plain MSE
+    loss, the Fisher kwargs (grad_buffer, update_fisher) accepted and ignored.  A model WITH a Fisher store is refused
+    (the weighted branch is out of scope)."""
     from nerf_amd.meta import compute_loss
     z = load("meta")
     model, _ = _meta_model()
+    data = {"rays": z["rays"].to(DEV), "rgbs": z["gt"].to(DEV)}
     P = types.SimpleNamespace(algo="fomaml", fim=True, ray_samples=32, chunk_points=1 << 20, color_space="linear")
+    a = compute_loss(P, model, data, active_module=0, grad_buffer={}, update_fisher=False)
+    P0 = types.SimpleNamespace(**{**vars(P), "fim": False})
+    b = compute_loss(P0, model, data, active_module=0)
+    assert torch.isfinite(a) and abs(a.item() - b.item()) <= 1e-6 * b.item(), (a.item(), b.item())
+    model.fisher_store, model.fim_loss = object(), object()
     with pytest.raises(NotImplementedError):
-        compute_loss(P, model, {"rays": z["rays"].to(DEV), "rgbs": z["gt"].to(DEV)}, active_module=0)
+        compute_loss(P, model, data, active_module=0)

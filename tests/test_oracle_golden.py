@@ -1,5 +1,7 @@
 """Pin the CPU oracle (oracle/nerf_oracle.py) against golden vectors produced by importing the
 reference itself (tools/gen_golden.py).  CPU only."""
+from collections import OrderedDict
+
 import torch
 
 from oracle import nerf_oracle as O
@@ -123,3 +125,63 @@ def test_sample_pdf_known_answers():
     uu, _ = torch.sort(torch.rand(N, 64), -1)
     s = O.sample_pdf(bins, torch.rand(N, B), 64, u=uu)
     assert (s[:, 1:] >= s[:, :-1] - 1e-6).all()
+
+
+# ------------------------------------------------------------------ the reference's AMP numerics (tests/golden/amp.npz)
+
+
+def _cos(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float(a @ b / (a.norm() * b.norm() + 1e-300))
+
+
+def test_amp_trunc_exp_input_is_fp32_golden():
+    """Under autocast(float16) the imported reference's MetaNeRF hands trunc_exp an fp32 tensor (MetaLinear adds
+    its fp32 bias to the fp16 matmul output, metamodule.py:153-156), so the clamp is fp32's 88.72
+    (trunc_exp.py:30-35), not fp16's 11.09: sigma(15) = exp(15) = 3.27e6 > 65504.  The oracle's AMP restatement
+    gives the same sigma and d sigma / d bias at every pre-activation of the known-answer set."""
+    z = load("amp")
+    assert int(z["sigma_in_bits"]) == 32 and int(z["out_bits"]) == 32
+    x = z["te16_x"]
+    y, g = z["te16_y"], z["te16_g"]
+    assert float(y[x == 15.0]) > 65504.0 * 40 and float(y[x == 30.0]) > 1e12
+    xr = x.clone().requires_grad_(True)
+    h = O.trunc_exp(xr.view(-1, 1))
+    gx, = torch.autograd.grad(h.sum(), xr)
+    torch.testing.assert_close(h.detach().view(-1), y, rtol=1e-6, atol=0)
+    torch.testing.assert_close(gx, g, rtol=1e-6, atol=0)
+
+
+def test_amp_mlp_forward_backward_golden():
+    """oracle.vanilla_forward(amp="fp16") (fp16 matmul operands / outputs, fp32 bias, ReLU and trunc_exp) against
+    the reference's MetaNeRF run under autocast(float16): forward bitwise, every parameter gradient within 1e-3 of
+    its norm (the fp16 rounding of the backward GEMM outputs happens inside the host's matmul differently)."""
+    z = load("amp")
+    m = load("mlp")
+    p = OrderedDict((k, v.clone().requires_grad_(True)) for k, v in mlp_params("w/").items())
+    x, gup = m["x_d"][:256], m["gup"][:256]
+    out = O.vanilla_forward(p, x, amp="fp16")
+    torch.testing.assert_close(out.detach(), z["out"], rtol=0, atol=1e-6)
+    grads = torch.autograd.grad((out * gup).sum(), list(p.values()))
+    for (n, _), gr in zip(p.items(), grads):
+        ref = z[f"g/{n}"].double()
+        rel = float((gr.double() - ref).norm() / (ref.norm() + 1e-30))
+        assert rel <= 1e-3, f"{n}: AMP gradient rel err {rel:.2e}"
+    # the fp32 oracle is NOT the reference's AMP result (fp16 rounding moves the early-layer gradients by ~8 %)
+    out32 = O.vanilla_forward(mlp_params("w/"), x)
+    assert (out32 - z["out"]).abs().max() > 1e-5
+
+
+def test_amp_train_loss_and_scaled_gradients_golden():
+    """The reference's use_amp loop body (runtime_adapt.py:291-305) on 64 rays x 32 coarse samples, jitter as
+    recorded: autocast(float16) loss, backward of loss x 2^16, gradients unscaled.  OracleTrainer(amp="fp16")'s
+    render + loss + scaled backward gives the same loss (to fp32 rounding) and gradients within 1e-3 of their norm."""
+    z = load("amp")
+    ot = O.OracleTrainer(mlp_params("w/"), amp="fp16", grad_clip=None)
+    ot.opt.step = lambda: None  # compare the unscaled gradients, before any update
+    loss = ot.step(z["step_rays"], z["step_gt"], 32, training=True, u_strat=z["step_u"])
+    assert abs(loss - float(z["step_loss"])) <= 1e-6 * float(z["step_loss"]) + 1e-9, (loss, float(z["step_loss"]))
+    for n, q in ot.nets[0].items():
+        ref = z[f"sg/{n}"].double()
+        rel = float((q.grad.double() - ref).norm() / (ref.norm() + 1e-30))
+        assert rel <= 1e-3 and _cos(q.grad, ref) >= 0.99999, f"{n}: rel {rel:.2e}"

@@ -12,7 +12,8 @@ renderer), ``jaxtyping`` (scene_box.py:3, a type annotation), ``viser.transforms
 MetaNeRF's (x,d,params)->dict forward is wrapped in a 6-line adapter to the container
 contract expert(x_d (M,6), params) -> (M,4) (SURVEY.md §0 defect 2).
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--only-ngp | --only-moe | --only-data | --only-meta]
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--only-ngp | --only-moe | --only-data | --only-meta |
+        --only-amp]
 """
 import math
 import os
@@ -442,8 +443,94 @@ def gen_meta():
     np.savez_compressed(os.path.join(OUT, "meta.npz"), **arr)
 
 
+def gen_amp():
+    """The reference's AMP numerics (configs/train.json "use_amp": true; pipelines/online_stage/runtime_adapt.py:290-310:
+    autocast(float16) around compute_mse_loss, scaler.scale(loss).backward() outside it).  Run on the CPU autocast,
+    whose fp16 cast policy for matmul is CUDA's (lower-precision list); the arithmetic inside one fp16 matmul is the
+    host's, so the fixture pins dtypes / clamps exactly and values to fp16 rounding.
+      * dtype of trunc_exp's input: MetaLinear (metamodule.py:140-156) adds its fp32 bias to the fp16 matmul output,
+        so type promotion makes the sigma pre-activation fp32 and trunc_exp clamps at 88.72, not 11.09;
+      * te16: sigma_head weight 0, bias = x for x beyond +-11.09 -> sigma and d sigma / d bias under autocast;
+      * a MetaNeRF forward + parameter gradients under autocast (mlp.npz weights, 256 samples);
+      * one coarse-only train-loss + loss-scaled gradient (scale 2^16, unscaled) through render_rays on 64 rays."""
+    from models.inr.meta_vanilla import MetaNeRF                      # noqa: E402
+    from nerfs.losses import compute_mse_loss                         # noqa: E402
+    z = np.load(os.path.join(OUT, "mlp.npz"))
+    zr = np.load(os.path.join(OUT, "rays.npz"))
+    net = MetaNeRF(encoding_dir="frequency")
+    with torch.no_grad():
+        for n, p in net.meta_named_parameters():
+            p.copy_(torch.from_numpy(z[f"w/{n}"]))
+    seen = []
+    act = net.sigma_act
+
+    def spy(x):
+        seen.append(x.dtype)
+        return act(x)
+
+    net.sigma_act = spy
+
+    class Expert(torch.nn.Module):
+        def __init__(self, n):
+            super().__init__(); self.net = n; self.use_occ = False; self.submodules = [self]
+
+        def forward(self, x_d, params=None):
+            o = self.net(x_d[:, :3], x_d[:, 3:6], params=params)
+            return torch.cat([o["rgb"], o["sigma"]], -1)
+
+    model = Expert(net).train()
+    arr = {}
+    x_d = torch.from_numpy(z["x_d"][:256])
+    gup = torch.from_numpy(z["gup"][:256])
+    with torch.autocast("cpu", dtype=torch.float16):
+        out = model(x_d)
+    grads = torch.autograd.grad((out * gup).sum(), list(net.parameters()))
+    arr["out"] = out.detach().float().numpy()
+    arr["out_bits"] = np.int32(torch.finfo(out.dtype).bits)            # 32: the expert's output is fp32
+    arr["sigma_in_bits"] = np.int32(torch.finfo(seen[-1]).bits)       # 32: trunc_exp sees an fp32 tensor
+    arr.update({f"g/{n}": gr.float().numpy() for (n, _), gr in zip(net.named_parameters(), grads)})
+    # trunc_exp beyond the fp16 clamp, through the module under autocast
+    te_x = [-30.0, -12.0, 0.0, 11.0, 12.0, 15.0, 30.0]
+    ys, gs = [], []
+    w0, b0 = net.sigma_head.weight.detach().clone(), net.sigma_head.bias.detach().clone()
+    for x in te_x:
+        with torch.no_grad():
+            net.sigma_head.weight.zero_()
+            net.sigma_head.bias.fill_(x)
+        with torch.autocast("cpu", dtype=torch.float16):
+            o = model(x_d[:8])
+        gb, = torch.autograd.grad(o[:, 3].sum(), [net.sigma_head.bias])
+        ys.append(float(o[0, 3])); gs.append(float(gb[0]) / 8.0)
+    with torch.no_grad():
+        net.sigma_head.weight.copy_(w0); net.sigma_head.bias.copy_(b0)
+    arr["te16_x"], arr["te16_y"], arr["te16_g"] = (np.array(v, np.float32) for v in (te_x, ys, gs))
+    # one coarse-only loss + scaled backward, as runtime_adapt.py:291-305 runs it
+    g = torch.Generator().manual_seed(99)
+    rays = torch.from_numpy(zr["rays_const"])[torch.randperm(10000, generator=g)[:64]].contiguous()
+    gt = torch.rand(64, 3, generator=g)
+    P = SimpleNamespace(ray_samples=32, chunk_points=1 << 20, color_space="linear")
+    torch.manual_seed(5)  # stratified_t_vals' jitter draw (ray_rendering.py:286) is recorded below
+    u = torch.rand(64, 32)
+    torch.manual_seed(5)
+    with torch.autocast("cpu", dtype=torch.float16):
+        loss = compute_mse_loss(P, model, {"rays": rays, "rgbs": gt})
+    scale = 65536.0
+    sg = torch.autograd.grad(loss * scale, list(net.parameters()))
+    arr["step_rays"], arr["step_gt"], arr["step_u"] = rays.numpy(), gt.numpy(), u.numpy()
+    arr["step_loss"] = np.float32(loss.item())
+    arr.update({f"sg/{n}": (gr.float() / scale).numpy() for (n, _), gr in zip(net.named_parameters(), sg)})
+    np.savez_compressed(os.path.join(OUT, "amp.npz"), **arr)
+    print("amp: sigma_in_dtype", seen[-1], "out", out.dtype, "te16_y", ys)
+
+
 if __name__ == "__main__":
-    if "--only-meta" in sys.argv:
+    if "--only-amp" in sys.argv:
+        sys.dont_write_bytecode = True
+        _install_stubs()
+        sys.path.insert(0, REF)
+        torch.set_num_threads(8)
+        gen_amp()
+    elif "--only-meta" in sys.argv:
         sys.dont_write_bytecode = True
         _install_stubs()
         sys.path.insert(0, REF)
