@@ -26,7 +26,11 @@ Prints ONE JSON line on rank 0 (contract in the task statement), with
   psnr          — (N = 1) the metric's PSNR half: both precisions' engines, from the same seed-0 weights and
                   batches, continue to --psnr-steps total steps (outside the timed region), then render every
                   held-out 800x800 view; mean full-image PSNR per precision and the bf16 - fp32 gap.
-  dp            — (N > 1) per-rank step time (max / min) and HIP-event time of each all-reduce bucket.
+  dp            — (N > 1) per-rank step time (max / min), HIP-event time of each all-reduce bucket, and
+                  params_equal_across_ranks: an all-gathered fp64 sum + bit hash of every rank's parameters.
+  llff          — BASELINE configs[3] (C4): the Fern-style 1008x756 NDC scene, same fp32 engine, --llff-steps steps.
+  sweep         — BASELINE configs[4] (C5): 8 seeded scenes x --sweep-steps bf16 4096-ray steps, rank r training
+                  scenes r, r+N, ...; aggregate rays/s vs the bf16 MFMA roofline and mean held-out PSNR.
   cpu_baseline  — the CPU oracle (a restatement of the reference's PyTorch path, pinned to its golden
                   vectors) running the same train step (4096 rays, 64+128, 2 nets), median of >= 5 steps
                   on this host's CPU share (rank 0, N=1); `all_cores` beside it at os.cpu_count() threads.
@@ -106,7 +110,13 @@ def parse():
                     help="skip the sub-record of the other MLP precision (bf16 beside fp32, or fp32 beside bf16)")
     ap.add_argument("--psnr-steps", type=int, default=3000,
                     help="total train steps of each precision's engine before the held-out PSNR renders")
-    ap.add_argument("--psnr-views", type=int, default=2, help="held-out 800x800 views rendered for the PSNR")
+    ap.add_argument("--psnr-views", type=int, default=8, help="held-out 800x800 views rendered for the PSNR")
+    ap.add_argument("--no-llff", action="store_true", help="skip the C4 (Fern-style NDC) sub-record")
+    ap.add_argument("--llff-steps", type=int, default=20, help="timed steps of the C4 sub-record")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the C5 (8-scene sweep) sub-record")
+    ap.add_argument("--sweep-scenes", type=int, default=8)
+    ap.add_argument("--sweep-steps", type=int, default=500, help="bf16 train steps per scene of the C5 sub-record")
+    ap.add_argument("--sweep-views", type=int, default=20, help="training views per C5 scene")
     ap.add_argument("--fp32-gemm", default="split", choices=["split", "native_dgrad", "native"],
                     help="fp32 trunk GEMMs: all as bf16 split products (gemm_x6.hpp, default), input gradients on the "
                          "fp32 MFMA (native_dgrad), or all on the fp32 MFMA kernels (native)")
@@ -457,6 +467,7 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_
                                 "fine gradient + loss, after the fine backward), mean over the event steps; includes "
                                 "the wait for the slowest rank",
               "bytes_per_step": int(tr.gbuf.numel() * 4)}
+        dp.update(params_checksum(tr.params, world))
     rec = {"value": round(n_local * world * a.steps / el, 1), "ms_per_step": round(el / a.steps * 1e3, 3),
            "final_loss": round(float(loss.item()), 6),
            "roofline": dict(roofline(tm, precision == "bf16", False, tr.bf16_flags,
@@ -475,6 +486,70 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_
     if dp:
         rec["dp"] = dp
     return rec, tr, (coarse, fine)
+
+
+def params_checksum(params, world):
+    """After the timed region: every rank's flat parameter buffer reduced to (fp64 sum, position-weighted int64 hash of
+    the fp32 bit patterns) and all-gathered — data parallel with one gradient all-reduce keeps the replicas bitwise
+    equal, so an N-GPU run validates itself from its own line (params_equal_across_ranks)."""
+    bits = params.detach().contiguous().view(torch.int32).to(torch.int64)
+    wpos = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 1048573 + 1
+    h = (bits * wpos).sum().view(1)                      # int64, wraps on overflow identically on every rank
+    f = params.detach().double().sum().view(1)
+    hs, fs = [torch.zeros_like(h) for _ in range(world)], [torch.zeros_like(f) for _ in range(world)]
+    dist.all_gather(hs, h)
+    dist.all_gather(fs, f)
+    rows = [(float(x.item()), int(y.item())) for x, y in zip(fs, hs)]
+    return {"params_equal_across_ranks": all(r == rows[0] for r in rows), "world_size_checked": dist.get_world_size(),
+            "params_sum_per_rank": [r[0] for r in rows], "params_bit_hash_per_rank": [r[1] for r in rows]}
+
+
+def llff_run(a, dev, world, rank, barrier, nccl):
+    """BASELINE configs[3] (C4): the Fern-style 1008x756 forward-facing scene with NDC rays (synthetic, 20 views), the
+    same fp32 engine step (64 + 128, two nets) over a.llff_steps timed steps; data parallel at N > 1 as the headline."""
+    from types import SimpleNamespace
+    from nerf_amd.scene import make_llff_scene
+    from nerf_amd.trainer import RayBatcher
+    torch.manual_seed(0)
+    scene = make_llff_scene(n_train=20, n_test=1, seed=0, device=dev)
+    rb = RayBatcher(scene, dev)
+    b = SimpleNamespace(**{**vars(a), "steps": a.llff_steps, "timing_steps": 1})
+    n_local = a.batch // world if a.strong else a.batch
+    rec, _, _ = engine_run(b, dev, rb, world, rank, n_local, "fp32", barrier, nccl)
+    out = {"config": "configs[3]: Fern-style 1008x756 forward-facing, NDC rays (near plane 1, t in [0,1]), 64+128, "
+                     "2 x (8x256 MLP), fp32 engine (synthetic analytic scene, 20 views; LLFF data is not in the image)",
+           "value": rec["value"], "unit": "rays/s", "ms_per_step": rec["ms_per_step"], "steps": b.steps,
+           "n_gpus": world, "step_mfma_frac": rec["step_mfma_frac"], "final_loss": rec["final_loss"],
+           "roofline_class_ms": rec["roofline"].get("classes_ms")}
+    if rec.get("dp"):
+        out["dp"] = {k: rec["dp"][k] for k in ("world_size", "step_ms_max", "step_ms_min", "params_equal_across_ranks")}
+    return out
+
+
+def sweep_run(a, dev, world, rank):
+    """BASELINE configs[4] (C5): a.sweep_scenes seeded Lego-style scenes (800x800, a.sweep_views training views, 2 held-out),
+    each trained independently by the bf16 engine for a.sweep_steps 4096-ray steps (64 + 128, lr 2e-3); rank r trains
+    scenes r, r+N, ... (no collective on the data path), results all-gathered once.  Aggregate rays/s = sum over GPUs
+    of each GPU's rays / its training time, against the bf16 MFMA roofline; mean held-out PSNR after a.sweep_steps."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import sweep_scenes
+    res = []
+    for sid in range(rank, a.sweep_scenes, world):
+        r = sweep_scenes.train_scene(sid, steps=a.sweep_steps, batch=a.batch, train_views=a.sweep_views, test_views=2,
+                                     precision="bf16", lr=2e-3, dev=dev)
+        r.pop("losses", None)
+        r["rank"] = rank
+        res.append(r)
+        progress(f"sweep: scene {sid} psnr {r['psnr']} at {r['rays_per_s']} rays/s")
+        torch.cuda.empty_cache()
+    if world > 1:
+        allr = [None] * world
+        dist.all_gather_object(allr, res)
+        res = [r for rr in allr for r in rr]
+    summ = sweep_scenes.summarize(res, a.batch, "bf16", world)
+    summ.update({"steps_per_scene": a.sweep_steps, "train_views": a.sweep_views, "test_views": 2,
+                 "per_scene": [{k: r[k] for k in ("scene_seed", "psnr", "rays_per_s", "loss", "rank")} for r in res]})
+    return summ
 
 
 def psnr_run(a, rb, scene, runs, rank, world, n_local):
@@ -615,9 +690,17 @@ def main():
     if native:
         out["fp32_native_gemm"] = {k: native[k] for k in ("value", "ms_per_step", "final_loss", "step_mfma_frac")}
         out["fp32_native_gemm"]["roofline_classes_ms"] = native["roofline"].get("classes_ms")
+    if not a.no_llff and a.scene == "blender" and a.path == "engine":
+        progress("C4 (llff) leg")
+        out["llff"] = llff_run(a, dev, world, rank, barrier, nccl)
     progress("timed legs done")
     if not a.no_psnr and rank == 0 and runs and world == 1:
         out["psnr"] = psnr_run(a, rb, scene, runs, rank, world, n_local)
+    if not a.no_sweep and a.scene == "blender" and a.path == "engine":
+        progress("C5 (8-scene sweep) leg")
+        sw = sweep_run(a, dev, world, rank)
+        if rank == 0:
+            out["sweep"] = sw
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.samples, a.importance, a.cpu_batch, a.cpu_steps)
     elif rank == 0:

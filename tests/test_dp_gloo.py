@@ -174,3 +174,39 @@ def test_flat_adam_buckets_data_dependent_firing_gloo():
             assert torch.allclose(g[1], torch.full((5,), 1.5)), (r, step, g[1])
             for t, i in enumerate((0, 2, 3)):
                 assert torch.allclose(g[i], torch.full_like(g[i], want_t[t])), (r, step, t, g[i][:3], want_t[t])
+
+
+def _checksum_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    p = torch.randn(100003, generator=torch.Generator().manual_seed(5))
+    same = bench.params_checksum(p, world)
+    if rank == 1:  # one flipped low mantissa bit on one rank: the fp64 sum may not see it, the bit hash does
+        p.view(torch.int32)[77777] ^= 1
+    diff = bench.params_checksum(p, world)
+    q.put((rank, same, diff))
+    dist.destroy_process_group()
+
+
+def test_bench_params_checksum_gloo():
+    """bench.py's dp record: after the timed region the ranks all-gather a checksum of their
+    parameters, so an N-GPU run reports whether the replicas stayed bitwise equal."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_checksum_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict((r, (a, b)) for r, a, b in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        same, diff = out[r]
+        assert same["params_equal_across_ranks"] and same["world_size_checked"] == 2
+        assert not diff["params_equal_across_ranks"]
+        assert diff["params_bit_hash_per_rank"][0] != diff["params_bit_hash_per_rank"][1]
