@@ -52,8 +52,13 @@ __device__ constexpr int X6_PB[6] = {0, 1, 2, 0, 1, 0};
 // the forward kernels' order: the same as X6_PA / X6_PB (lo.hi first).  A hi.lo-first order let a k-step's first
 // MFMAs overlap the rest of the activation split (0.635 -> 0.629 ms per fine layer) but moved the C2 trajectory's
 // 3000-step PSNR from 28.20 to 27.74 dB; the probe-characterised order is kept (profiles/r03/x6_fwd_term_order_ab.txt)
+#ifdef NERF_X6_FWD_HIFIRST  // A/B builds: the hi.lo-first forward order (PSNR noise-band study, round 4)
+__device__ constexpr int X6F_PA[6] = {0, 2, 1, 1, 0, 0};
+__device__ constexpr int X6F_PB[6] = {2, 0, 1, 0, 1, 0};
+#else
 __device__ constexpr int X6F_PA[6] = {2, 1, 0, 1, 0, 0};
 __device__ constexpr int X6F_PB[6] = {0, 1, 2, 0, 1, 0};
+#endif
 // acc_[TM_][TN_] += over the six terms; MFMA(first_, second_) operands: NT passes (B fragment, A fragment) so the
 // accumulator is C^T (gemm_bf16.hpp); the weight gradient passes (G^T fragment, X fragment)
 #ifndef NERF_X6_TERMS  // ablation builds only (tools/build_exp.sh): fewer terms -> wrong results, MFMA cost probe
@@ -230,6 +235,67 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_x6_kernel(const float* __re
 #endif
 }
 
+// ------------------------------------------------------------------------------------------ LDS-staged epilogue
+// The C^T accumulator leaves lane (li, lh) with row li, columns 8q + 4lh .. + 3 of each 32 x 32 block: the direct
+// store (ntb_epilogue) writes 32 rows x 32 B per instruction, and with one workgroup per CU the 256 KiB of a tile's
+// outputs leave at the store-issue rate while the matrix cores idle (cdna_hip_programming.md T21).  Here each block
+// goes registers -> a private [32][36] fp32 LDS tile (144-B pitch) -> registers as 8 lanes per row, so every store
+// instruction writes 8 whole 128-B lines.  Bias / ReLU / mask words are applied in registers first, exactly as
+// ntb_epilogue does (same fp32 operations, bitwise the same outputs).
+constexpr int X6E_PITCH = 36;
+constexpr int X6E_WAVE_FLOATS = 32 * X6E_PITCH;
+template <int TM, int TN, int EPI>
+__device__ __forceinline__ void x6_epilogue_lds(nerf_f32x16 (&acc)[TM][TN], int64_t mw, int n0, int lane,
+                                                const float* __restrict__ bias, float* __restrict__ C, int ldc,
+                                                const uint32_t* __restrict__ mbits, int ldmb,
+                                                uint32_t* __restrict__ mbits_out, float* E) {
+  const int li = lane & 31, lh = lane >> 5;
+  const int rr = lane >> 3, cc = 4 * (lane & 7);  // read-back: row rr + 8 i, columns cc .. cc + 3
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int nb = n0 + b * 32;
+    const int g = nb >> 5;
+    float4 bv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) bv[q] = *reinterpret_cast<const float4*>(bias + nb + 8 * q + 4 * lh);
+    }
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const int64_t m = mw + a * 32 + li;
+      uint32_t word = 0;
+      if (EPI == EPI_MASK) word = mbits[m * ldmb + g];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[a][b][4 * q + e];
+          const float bb = e == 0 ? bv[q].x : (e == 1 ? bv[q].y : (e == 2 ? bv[q].z : bv[q].w));
+          if (EPI == EPI_BIAS) v[e] += bb;
+          if (EPI == EPI_BIAS_RELU) {
+            v[e] = fmaxf(v[e] + bb, 0.f);
+            word |= (v[e] > 0.f ? 1u : 0u) << (8 * q + 4 * lh + e);
+          }
+          if (EPI == EPI_MASK) v[e] = ((word >> (8 * q + 4 * lh + e)) & 1u) ? v[e] : 0.f;
+        }
+        *reinterpret_cast<float4*>(E + li * X6E_PITCH + 8 * q + 4 * lh) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+      if (EPI == EPI_BIAS_RELU && mbits_out) {
+        word |= __shfl_xor(word, 32, 64);
+        if (lh == 0) mbits_out[m * ldmb + g] = word;
+      }
+      float4 o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = *reinterpret_cast<const float4*>(E + (rr + 8 * i) * X6E_PITCH + cc);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<float4*>(C + (mw + a * 32 + rr + 8 * i) * ldc + nb + cc) = o[i];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------ gemm_nt_x6w
 // Wide-wave form of gemm_nt_x6: a (64 NW) x 128 workgroup tile whose NW waves each own 64 rows x ALL 128 columns
 // (2 x 4 MFMA tiles), so every activation row is loaded and split by exactly one wave (gemm_nt_x6's 64 x 64 waves
@@ -255,6 +321,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   constexpr int LS = BK + 8;
   constexpr int PL = BN * LS;
   __shared__ __attribute__((aligned(16))) nerf_bf16 smem[2 * 3 * PL];
+  static_assert(NW * X6E_WAVE_FLOATS * 4 <= 2 * 3 * PL * 2, "epilogue tiles fit in the weight images");
 
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
@@ -409,7 +476,19 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
 #pragma unroll
       for (int b = 0; b < TN; ++b) acc[a][b] += accs[a][b];
   }
+#if defined(NERF_X6W_NOSTORE)  // ablation builds only: the epilogue's cost (outputs left stale)
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) asm volatile("" ::"v"(acc[a][b]));
+#elif defined(NERF_X6W_REGEPI)  // A/B builds: the direct row-per-lane stores (32 rows x 32 B per store instruction)
   ntb_epilogue<TM, TN, WTM, WTN, EPI, 0>(acc, m0 + wave * WTM, n0, li, lh, bias, C, ldc, mbits, ldmb, mbits_out);
+#else
+  // the loop's last barrier freed the weight images: every wave stages its 32 x 32 blocks through a private LDS
+  // tile and stores whole 128-B row lines (8 lanes per row)
+  x6_epilogue_lds<TM, TN, EPI>(acc, m0 + wave * WTM, n0, lane, bias, C, ldc, mbits, ldmb, mbits_out,
+                               reinterpret_cast<float*>(smem) + wave * X6E_WAVE_FLOATS);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------ gemm_wgrad_x6

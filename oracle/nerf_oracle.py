@@ -112,7 +112,7 @@ def ndc_rays(H, W, focal, near_plane, rays):
 
 def stratified_t_vals(near, far, S, randomized, u=None):
     """nerfs/ray_rendering.py:262-287.  ``u`` replaces ``torch.rand_like(low)`` (:286)."""
-    t_lin = torch.linspace(0.0, 1.0, S, dtype=near.dtype).unsqueeze(0)
+    t_lin = torch.linspace(0.0, 1.0, S, dtype=near.dtype, device=near.device).unsqueeze(0)
     t = near.unsqueeze(1) * (1.0 - t_lin) + far.unsqueeze(1) * t_lin
     if randomized:
         mids = 0.5 * (t[:, :-1] + t[:, 1:])
@@ -309,14 +309,14 @@ def volume_render(rgb_sigma, t, bg=None, sigma_scale=1.0):
     return rgb_map, depth, w, acc
 
 
-def bg_default(N, policy, dtype=torch.float32):
+def bg_default(N, policy, dtype=torch.float32, device=None):
     """nerfs/ray_rendering.py:48-79 (deterministic policies only)."""
     if policy == "none":
         return None
     if policy == "white":
-        return torch.ones(N, 3, dtype=dtype)
+        return torch.ones(N, 3, dtype=dtype, device=device)
     if policy == "black":
-        return torch.zeros(N, 3, dtype=dtype)
+        return torch.zeros(N, 3, dtype=dtype, device=device)
     raise ValueError(policy)
 
 
@@ -330,7 +330,7 @@ def render_rays(p_coarse, rays, S, training=False, u_strat=None, bg="white",
     o, d = rays[:, :3], rays[:, 3:6]
     N = rays.shape[0]
     t = stratified_t_vals(rays[:, 6], rays[:, 7], S, training, u_strat)
-    bgc = bg if isinstance(bg, torch.Tensor) or bg is None else bg_default(N, bg, rays.dtype)
+    bgc = bg if isinstance(bg, torch.Tensor) or bg is None else bg_default(N, bg, rays.dtype, rays.device)
 
     def one_pass(p, tv):
         pts = o.unsqueeze(1) + d.unsqueeze(1) * tv.unsqueeze(-1)

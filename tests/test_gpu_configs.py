@@ -2,7 +2,7 @@
 
 * C4 — Fern-style forward-facing scene, 1008x756, NDC rays, 64 + 128: the engine's ray batch (``RayBatcher`` over a
   ``scene.ndc`` scene: pixel pick -> rays -> NDC on the device) against ``oracle.get_rays`` + ``oracle.ndc_rays``, and
-  two engine train steps against ``OracleTrainer`` on identical jitter (loss to 1e-5, clipped gradients to 1e-4 of
+  two engine train steps of 1024 rays against ``OracleTrainer`` on identical jitter (loss to 1e-5, clipped gradients to 1e-4 of
   their scale);
 * C5 — the 8-scene sweep driver (``tools/sweep_scenes.py``) at its 4096-ray batch on 8 scenes (200x200 views):
   finite, decreasing loss and a per-scene PSNR above the untrained one, aggregate rays/s;
@@ -47,7 +47,7 @@ def test_c4_llff_ndc_engine_step_vs_oracle(K):
     imgs = torch.randint(0, 256, (2, H, W, 3), dtype=torch.uint8, generator=g)
     scene = Scene(H, W, f, 0.0, 1.0, poses[:2].to(DEV), imgs.to(DEV), poses[2:].to(DEV), imgs[:1], ndc=True)
     rb = RayBatcher(scene, DEV)
-    n = 128
+    n = 1024
     rays, gt = rb.batch(n, seed=3)
     pix = K.pick_pixels(n, 2, H, W, 3, DEV).long().cpu()
     # oracle rays: directions of those pixels -> cam-to-world (near 0 / far 1) -> NDC (near plane 1)

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--test-views", type=int, default=2)
     ap.add_argument("--out", default=None)
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--jitter-seed", type=int, default=0,
+                    help="offset of the per-step jitter seeds (same batches, same initial weights): noise-band runs")
     a = ap.parse_args()
 
     from nerf_amd.scene import make_blender_scene, make_llff_scene
@@ -76,11 +78,12 @@ def main():
         t0 = time.perf_counter()
         for _ in range(n):
             rays, gt = rb.batch(a.batch, seed=step)
-            loss = tr.step(rays, gt, seed=step)
+            loss = tr.step(rays, gt, seed=step + a.jitter_seed * 1000003)
             step += 1
         torch.cuda.synchronize()
         train_s += time.perf_counter() - t0
-        rec = {"scene": a.scene, "precision": a.precision, "step": step, "train_s": round(train_s, 2), "loss": round(float(loss.item()), 6),
+        rec = {"scene": a.scene, "precision": a.precision, "jitter_seed": a.jitter_seed,
+               "lib": os.path.basename(os.environ.get("NERF_AMD_LIB", "libnerf_amd.so")), "step": step, "train_s": round(train_s, 2), "loss": round(float(loss.item()), 6),
                "psnr": round(evaluate(), 3), "rays_per_s": round(step * a.batch / train_s, 1)}
         print(json.dumps(rec), flush=True)
         if outf:
