@@ -408,6 +408,26 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   }
   X6W_BSTORE(0);
   __syncthreads();
+  // PIPE (ASMB kernels): the activation split of k-step i + 1 runs under the MFMAs of k-step i (its VALU spread one
+  // group per MFMA by sched_group_barrier); k-step i consumes the pieces split during k-step i - 1
+#ifdef NERF_X6W_PIPE
+  constexpr bool PIPE = ASMB;
+#else
+  constexpr bool PIPE = false;
+#endif
+  auto split_into = [&](nerf_bf16x8 (&dst)[TM][3], const float4 (&src)[TM][KS][2], int ks) {
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      uint2 h0, m0_, l0, h1, m1, l1;
+      x6_split4(src[a][ks][0], h0, m0_, l0);
+      x6_split4(src[a][ks][1], h1, m1, l1);
+      dst[a][0] = __builtin_bit_cast(nerf_bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+      dst[a][1] = __builtin_bit_cast(nerf_bf16x8, make_uint4(m0_.x, m0_.y, m1.x, m1.y));
+      dst[a][2] = __builtin_bit_cast(nerf_bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+    }
+  };
+  nerf_bf16x8 afc[TM][3];
+  if constexpr (PIPE) split_into(afc, ra[0], 0);
   for (int kt0 = 0; kt0 < nk; kt0 += 2) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {  // slab kt = kt0 + j: LDS buffer j, activation register set j
@@ -419,18 +439,21 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
         const nerf_bf16* S = smem + j * 3 * PL;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          nerf_bf16x8 af[TM][3];
+          nerf_bf16x8 af[TM][3], afn[TM][3];
+          if constexpr (PIPE) {
 #pragma unroll
-          for (int a = 0; a < TM; ++a) {
-            uint2 h0, m0_, l0, h1, m1, l1;
-            x6_split4(ra[j][a][ks][0], h0, m0_, l0);
-            x6_split4(ra[j][a][ks][1], h1, m1, l1);
-            af[a][0] = __builtin_bit_cast(nerf_bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
-            af[a][1] = __builtin_bit_cast(nerf_bf16x8, make_uint4(m0_.x, m0_.y, m1.x, m1.y));
-            af[a][2] = __builtin_bit_cast(nerf_bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+              for (int p = 0; p < 3; ++p) af[a][p] = afc[a][p];
+          } else {
+            split_into(af, ra[j], ks);
           }
 #pragma unroll
           for (int bp = 0; bp < TN / 2; ++bp) {  // column-block pairs: 2 x 3 B fragments live
+            if (PIPE && bp == TN / 2 - 1) {  // the next k-step's pieces: this slab's next k-step or the next slab's first
+              if (ks + 1 < KS) split_into(afn, ra[j], ks + 1 < KS ? ks + 1 : 0);
+              else split_into(afn, ra[j ^ 1], 0);
+            }
             nerf_bf16x8 bf[2][3];
 #pragma unroll
             for (int p = 0; p < 3; ++p)
@@ -456,6 +479,20 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
                                                                                acc[a][2 * bp + b], 0, 0, 0);
                   }
                 }
+            if (PIPE && bp == TN / 2 - 1) {  // the pair's fragment reads, then one MFMA per ~4 VALU of the split
+              __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+              for (int q = 0; q < 6 * TM * 2; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+              }
+            }
+          }
+          if constexpr (PIPE) {
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+              for (int p = 0; p < 3; ++p) afc[a][p] = afn[a][p];
           }
         }
         X6W_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);  // set j consumed: slab kt + 2 streams into it
@@ -476,16 +513,12 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
 #pragma unroll
       for (int b = 0; b < TN; ++b) acc[a][b] += accs[a][b];
   }
-#if defined(NERF_X6W_NOSTORE)  // ablation builds only: the epilogue's cost (outputs left stale)
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b) asm volatile("" ::"v"(acc[a][b]));
-#elif defined(NERF_X6W_REGEPI)  // A/B builds: the direct row-per-lane stores (32 rows x 32 B per store instruction)
+#if defined(NERF_X6W_REGEPI)  // A/B builds: the direct row-per-lane stores (32 rows x 32 B per store instruction)
   ntb_epilogue<TM, TN, WTM, WTN, EPI, 0>(acc, m0 + wave * WTM, n0, li, lh, bias, C, ldc, mbits, ldmb, mbits_out);
 #else
   // the loop's last barrier freed the weight images: every wave stages its 32 x 32 blocks through a private LDS
-  // tile and stores whole 128-B row lines (8 lanes per row)
+  // tile and stores whole 128-B row lines (8 lanes per row).  C2 bench on MI355X (profiles/r04/x6_epilogue_ab.txt):
+  // fwd 0.625 -> 0.591 ms, dgrad 0.669 -> 0.610 ms per fine layer, 208.0k -> 217.0k rays/s, bitwise the same loss
   x6_epilogue_lds<TM, TN, EPI>(acc, m0 + wave * WTM, n0, lane, bias, C, ldc, mbits, ldmb, mbits_out,
                                reinterpret_cast<float*>(smem) + wave * X6E_WAVE_FLOATS);
 #endif
