@@ -82,68 +82,85 @@ __device__ __forceinline__ float srgb_to_linear(float x) {
   return x <= 0.04045f ? x / 12.92f : powf((x + 0.055f) / 1.055f, 2.4f);
 }
 
+// The loss head's sum: one float atomic per workgroup of FWD_RAYS rays (the per-ray partials meet in LDS first).  With
+// one atomic per ray the 4096 same-address atomics of a C2 batch serialised at the L2: 56-61 us per fine / coarse
+// launch on MI355X (profiles/r03/prof_fp32_summary.txt) for ~15 MB of data.
+constexpr int FWD_RAYS = 16;
 template <int SPL>
-__global__ __launch_bounds__(256) void composite_fwd_kernel(const float* __restrict__ rgb_sigma,
+__global__ __launch_bounds__(64 * FWD_RAYS) void composite_fwd_kernel(const float* __restrict__ rgb_sigma,
                                                             const float* __restrict__ t, const float* __restrict__ bg,
                                                             int64_t n, int S, float sigma_scale,
                                                             float* __restrict__ rgb, float* __restrict__ depth,
                                                             float* __restrict__ weights, float* __restrict__ acc,
                                                             const float* __restrict__ gt, int cs, float inv_count,
                                                             float* __restrict__ loss_sum, float* __restrict__ d_rgb) {
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= n) return;
+  __shared__ float s_loss[FWD_RAYS];
+  const int wv = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * FWD_RAYS + wv;
   const int lane = nerf_lane();
-  SampleState st[SPL];
-  load_ray<SPL>(rgb_sigma, t, r, S, sigma_scale, st);
-  float T[SPL];
-  transmittance<SPL>(st, T);
-  float cr = 0.f, cg = 0.f, cb = 0.f, dd = 0.f, aa = 0.f;
+  if (gt && lane == 0) s_loss[wv] = 0.f;
+  if (r < n) {
+    SampleState st[SPL];
+    load_ray<SPL>(rgb_sigma, t, r, S, sigma_scale, st);
+    float T[SPL];
+    transmittance<SPL>(st, T);
+    float cr = 0.f, cg = 0.f, cb = 0.f, dd = 0.f, aa = 0.f;
 #pragma unroll
-  for (int j = 0; j < SPL; ++j) {
-    const int i = lane * SPL + j;
-    const float w = st[j].alpha * T[j];
-    if (i < S) weights[r * S + i] = w;
-    cr += w * fminf(fmaxf(st[j].rs.x, 0.f), 1.f);
-    cg += w * fminf(fmaxf(st[j].rs.y, 0.f), 1.f);
-    cb += w * fminf(fmaxf(st[j].rs.z, 0.f), 1.f);
-    dd += w * st[j].t;
-    aa += w;
-  }
-  cr = wave_sum(cr); cg = wave_sum(cg); cb = wave_sum(cb); dd = wave_sum(dd); aa = wave_sum(aa);
-  if (bg) {
-    const float k = 1.0f - aa;
-    cr = cr + k * bg[3 * r];
-    cg = cg + k * bg[3 * r + 1];
-    cb = cb + k * bg[3 * r + 2];
-  }
-  if (lane == 0) {
-    rgb[3 * r] = cr; rgb[3 * r + 1] = cg; rgb[3 * r + 2] = cb;
-    if (depth) depth[r] = dd;
-    if (acc) acc[r] = aa;
-  }
-  if (gt && lane < 3) {
-    const float p = lane == 0 ? cr : (lane == 1 ? cg : cb);
-    float g = fminf(fmaxf(gt[3 * r + lane], 0.f), 1.f);
-    float pp, dp;
-    if (cs == 0) {  // linear: compare clamp(pred) with clamp(srgb_to_linear(gt))
-      pp = fminf(fmaxf(p, 0.f), 1.f);
-      dp = (p >= 0.f && p <= 1.f) ? 1.f : 0.f;
-      g = fminf(fmaxf(srgb_to_linear(g), 0.f), 1.f);
-    } else if (cs == 1) {  // srgb: compare clamp(linear_to_srgb(pred)) with gt
-      const float xc = fminf(fmaxf(p, 0.f), 1.f);
-      const float y = xc <= 0.0031308f ? 12.92f * xc : 1.055f * powf(xc, 1.0f / 2.4f) - 0.055f;
-      const float dy = xc <= 0.0031308f ? 12.92f : (1.055f / 2.4f) * powf(xc, 1.0f / 2.4f - 1.0f);
-      pp = fminf(fmaxf(y, 0.f), 1.f);
-      dp = ((y >= 0.f && y <= 1.f) ? 1.f : 0.f) * ((p >= 0.f && p <= 1.f) ? dy : 0.f);
-    } else {  // identity
-      pp = p;
-      dp = 1.f;
+    for (int j = 0; j < SPL; ++j) {
+      const int i = lane * SPL + j;
+      const float w = st[j].alpha * T[j];
+      if (i < S) weights[r * S + i] = w;
+      cr += w * fminf(fmaxf(st[j].rs.x, 0.f), 1.f);
+      cg += w * fminf(fmaxf(st[j].rs.y, 0.f), 1.f);
+      cb += w * fminf(fmaxf(st[j].rs.z, 0.f), 1.f);
+      dd += w * st[j].t;
+      aa += w;
     }
-    const float diff = pp - g;
-    d_rgb[3 * r + lane] = 2.0f * diff * inv_count * dp;
-    float l = diff * diff * inv_count;
-    l += __shfl_down(l, 1, 64) + __shfl_down(l, 2, 64);
-    if (lane == 0) atomicAdd(loss_sum, l);
+    cr = wave_sum(cr); cg = wave_sum(cg); cb = wave_sum(cb); dd = wave_sum(dd); aa = wave_sum(aa);
+    if (bg) {
+      const float k = 1.0f - aa;
+      cr = cr + k * bg[3 * r];
+      cg = cg + k * bg[3 * r + 1];
+      cb = cb + k * bg[3 * r + 2];
+    }
+    if (lane == 0) {
+      rgb[3 * r] = cr; rgb[3 * r + 1] = cg; rgb[3 * r + 2] = cb;
+      if (depth) depth[r] = dd;
+      if (acc) acc[r] = aa;
+    }
+    if (gt && lane < 3) {
+      const float p = lane == 0 ? cr : (lane == 1 ? cg : cb);
+      float g = fminf(fmaxf(gt[3 * r + lane], 0.f), 1.f);
+      float pp, dp;
+      if (cs == 0) {  // linear: compare clamp(pred) with clamp(srgb_to_linear(gt))
+        pp = fminf(fmaxf(p, 0.f), 1.f);
+        dp = (p >= 0.f && p <= 1.f) ? 1.f : 0.f;
+        g = fminf(fmaxf(srgb_to_linear(g), 0.f), 1.f);
+      } else if (cs == 1) {  // srgb: compare clamp(linear_to_srgb(pred)) with gt
+        const float xc = fminf(fmaxf(p, 0.f), 1.f);
+        const float y = xc <= 0.0031308f ? 12.92f * xc : 1.055f * powf(xc, 1.0f / 2.4f) - 0.055f;
+        const float dy = xc <= 0.0031308f ? 12.92f : (1.055f / 2.4f) * powf(xc, 1.0f / 2.4f - 1.0f);
+        pp = fminf(fmaxf(y, 0.f), 1.f);
+        dp = ((y >= 0.f && y <= 1.f) ? 1.f : 0.f) * ((p >= 0.f && p <= 1.f) ? dy : 0.f);
+      } else {  // identity
+        pp = p;
+        dp = 1.f;
+      }
+      const float diff = pp - g;
+      d_rgb[3 * r + lane] = 2.0f * diff * inv_count * dp;
+      float l = diff * diff * inv_count;
+      l += __shfl_down(l, 1, 64) + __shfl_down(l, 2, 64);
+      if (lane == 0) s_loss[wv] = l;
+    }
+  }
+  if (gt) {  // uniform: every wave reaches the barrier
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float l = 0.f;
+#pragma unroll
+      for (int k = 0; k < FWD_RAYS; ++k) l += s_loss[k];
+      atomicAdd(loss_sum, l);
+    }
   }
 }
 
@@ -222,8 +239,8 @@ __global__ __launch_bounds__(256) void composite_bwd_kernel(const float* __restr
 template <int SPL>
 void launch_fwd(const float* rs, const float* t, const float* bg, int64_t n, int S, float sc, float* rgb, float* depth,
                 float* w, float* acc, const float* gt, int cs, float ic, float* ls, float* drgb, hipStream_t st) {
-  composite_fwd_kernel<SPL><<<(unsigned)nerf_cdiv(n, 4), 256, 0, st>>>(rs, t, bg, n, S, sc, rgb, depth, w, acc, gt,
-                                                                        cs, ic, ls, drgb);
+  composite_fwd_kernel<SPL><<<(unsigned)nerf_cdiv(n, FWD_RAYS), 64 * FWD_RAYS, 0, st>>>(rs, t, bg, n, S, sc, rgb, depth,
+                                                                                      w, acc, gt, cs, ic, ls, drgb);
 }
 template <int SPL>
 void launch_bwd(const float* rs, const float* t, const float* bg, int64_t n, int S, float sc, const float* gr,
