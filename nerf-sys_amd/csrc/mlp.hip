@@ -298,10 +298,14 @@ int nt_x6(const float* A, int lda, const nerf_bf16* Bp, int ldb, int64_t bplane,
   if constexpr (EPI == EPI_MASK) {
     // input gradients: split accumulators (gemm_x6.hpp BIGSMALL) on 32-row waves, two per SIMD (256 x 128 tiles of 8
     // waves): 0.73-0.75 -> 0.665 ms per fine layer against 64-row waves at one per SIMD, bitwise the same results
-    if (M % 256 == 0 && K % 64 == 0) {  // gemm_nt_x6w walks the slabs in pairs
-      gemm_nt_x6w_kernel<EPI, 32, 8, true, 1><<<(unsigned)((M / 256) * ntn), 512, 0, st>>>(A, lda, Bp, ldb, bplane, bias,
-                                                                                        C, ldc, mbits, N / 32,
-                                                                                        mbits_out, K, ntn);
+#ifndef NERF_X6_DG_NW  // A/B builds: waves per input-gradient workgroup (4: two workgroups per CU)
+#define NERF_X6_DG_NW 8
+#endif
+    constexpr int DGM = 32 * NERF_X6_DG_NW;
+    if (M % DGM == 0 && K % 64 == 0) {  // gemm_nt_x6w walks the slabs in pairs
+      gemm_nt_x6w_kernel<EPI, 32, NERF_X6_DG_NW, true, 1, 8 / NERF_X6_DG_NW><<<(unsigned)((M / DGM) * ntn),
+                                                                             64 * NERF_X6_DG_NW, 0, st>>>(
+          A, lda, Bp, ldb, bplane, bias, C, ldc, mbits, N / 32, mbits_out, K, ntn);
       return NERF_OK;
     }
   }
