@@ -49,9 +49,10 @@ __device__ __forceinline__ void x6_split4(const float4 v, uint2& h, uint2& m, ui
 // chain on one accumulator (a dependent 32x32x16 MFMA waits for its predecessor's result).
 __device__ constexpr int X6_PA[6] = {2, 1, 0, 1, 0, 0};
 __device__ constexpr int X6_PB[6] = {0, 1, 2, 0, 1, 0};
-// the forward kernels' order: the same as X6_PA / X6_PB (lo.hi first).  A hi.lo-first order let a k-step's first
-// MFMAs overlap the rest of the activation split (0.635 -> 0.629 ms per fine layer) but moved the C2 trajectory's
-// 3000-step PSNR from 28.20 to 27.74 dB; the probe-characterised order is kept (profiles/r03/x6_fwd_term_order_ab.txt)
+// the forward kernels' order: the same as X6_PA / X6_PB (lo.hi first).  A hi.lo-first order measured 0.635 -> 0.629 ms
+// per fine layer in round 3; with the LDS epilogue (round 4) its training run is slower (227.9k vs 229.3k rays/s) and
+// its 3000-step PSNR (25.93 dB, sd 0.30 over 3 jitter seeds, 8 views) sits inside the default's band (26.12 dB, sd
+// 0.16): decided by speed, lo.hi first is kept (profiles/r04/psnr_band.txt)
 #ifdef NERF_X6_FWD_HIFIRST  // A/B builds: the hi.lo-first forward order (PSNR noise-band study, round 4)
 __device__ constexpr int X6F_PA[6] = {0, 2, 1, 1, 0, 0};
 __device__ constexpr int X6F_PB[6] = {2, 0, 1, 0, 1, 0};
@@ -348,7 +349,24 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   // (the touch below), so the compiler's counted waits on its own activation loads never wait on these as well.  At two
   // waves per SIMD the extra live registers spill (fwd 0.62 -> 0.65 ms): plain loads there.  32-row waves (TM = 1) have
   // the registers: a forward of that shape went 0.76 -> 0.655 ms with them, still behind 0.63 ms for 64-row waves.
+#ifdef NERF_X6W_ASMB2  // A/B builds: inline-asm weight loads for the 64-row-wave forward too (with NERF_X6W_BF1)
+  constexpr bool ASMB = true;
+#else
   constexpr bool ASMB = BIGSMALL || TM == 1;
+#endif
+  // B fragments are read per group of BPG column blocks (BPG x 3 fragments live); NERF_X6W_BF1 (A/B builds): one
+  // block at a time, 12 VGPRs fewer, for the inline-asm weight loads' registers
+#ifdef NERF_X6W_BF1
+  constexpr int BPG = 1;
+#else
+  constexpr int BPG = 2;
+#endif
+#ifdef NERF_X6W_BPREF  // A/B builds (with NERF_X6W_BF1): block b + 1's fragments read under block b's MFMAs
+  constexpr bool BPREF = true;
+  static_assert(BPG == 1, "BPREF prefetches one block");
+#else
+  constexpr bool BPREF = false;
+#endif
 #define X6W_BLOAD(k0_)                                                                                    \
   if constexpr (ASMB) {                                                                                   \
     _Pragma("unroll") for (int a = 0; a < TM; ++a)                                                       \
@@ -408,26 +426,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   }
   X6W_BSTORE(0);
   __syncthreads();
-  // PIPE (ASMB kernels): the activation split of k-step i + 1 runs under the MFMAs of k-step i (its VALU spread one
-  // group per MFMA by sched_group_barrier); k-step i consumes the pieces split during k-step i - 1
-#ifdef NERF_X6W_PIPE
-  constexpr bool PIPE = ASMB;
-#else
-  constexpr bool PIPE = false;
-#endif
-  auto split_into = [&](nerf_bf16x8 (&dst)[TM][3], const float4 (&src)[TM][KS][2], int ks) {
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
-      uint2 h0, m0_, l0, h1, m1, l1;
-      x6_split4(src[a][ks][0], h0, m0_, l0);
-      x6_split4(src[a][ks][1], h1, m1, l1);
-      dst[a][0] = __builtin_bit_cast(nerf_bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
-      dst[a][1] = __builtin_bit_cast(nerf_bf16x8, make_uint4(m0_.x, m0_.y, m1.x, m1.y));
-      dst[a][2] = __builtin_bit_cast(nerf_bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
-    }
-  };
-  nerf_bf16x8 afc[TM][3];
-  if constexpr (PIPE) split_into(afc, ra[0], 0);
   for (int kt0 = 0; kt0 < nk; kt0 += 2) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {  // slab kt = kt0 + j: LDS buffer j, activation register set j
@@ -437,62 +435,63 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
       if (ASMB || kt < nk) {
         X6W_BLOAD((kt + 1 < nk ? kt + 1 : kt) * BK);
         const nerf_bf16* S = smem + j * 3 * PL;
+        auto rd_b = [&](nerf_bf16x8 (&d)[3], int b, int ks_) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            d[p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + (b * 32 + li) * LS + 16 * ks_ + 8 * lh);
+        };
+        nerf_bf16x8 bfc[3];  // BPREF: the current column block's fragments, the next block's read under its MFMAs
+        if constexpr (BPREF) rd_b(bfc, 0, 0);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          nerf_bf16x8 af[TM][3], afn[TM][3];
-          if constexpr (PIPE) {
+          nerf_bf16x8 af[TM][3];
 #pragma unroll
-            for (int a = 0; a < TM; ++a)
-#pragma unroll
-              for (int p = 0; p < 3; ++p) af[a][p] = afc[a][p];
-          } else {
-            split_into(af, ra[j], ks);
+          for (int a = 0; a < TM; ++a) {
+            uint2 h0, m0_, l0, h1, m1, l1;
+            x6_split4(ra[j][a][ks][0], h0, m0_, l0);
+            x6_split4(ra[j][a][ks][1], h1, m1, l1);
+            af[a][0] = __builtin_bit_cast(nerf_bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+            af[a][1] = __builtin_bit_cast(nerf_bf16x8, make_uint4(m0_.x, m0_.y, m1.x, m1.y));
+            af[a][2] = __builtin_bit_cast(nerf_bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
           }
 #pragma unroll
-          for (int bp = 0; bp < TN / 2; ++bp) {  // column-block pairs: 2 x 3 B fragments live
-            if (PIPE && bp == TN / 2 - 1) {  // the next k-step's pieces: this slab's next k-step or the next slab's first
-              if (ks + 1 < KS) split_into(afn, ra[j], ks + 1 < KS ? ks + 1 : 0);
-              else split_into(afn, ra[j ^ 1], 0);
+          for (int bp = 0; bp < TN / BPG; ++bp) {  // groups of BPG column blocks: BPG x 3 B fragments live
+            nerf_bf16x8 bf[BPG][3], bfn[3];
+            if constexpr (BPREF) {
+#pragma unroll
+              for (int p = 0; p < 3; ++p) bf[0][p] = bfc[p];
+              if (bp + 1 < TN) rd_b(bfn, bp + 1, ks);
+              else if (ks + 1 < KS) rd_b(bfn, 0, ks + 1 < KS ? ks + 1 : ks);
+            } else {
+#pragma unroll
+              for (int p = 0; p < 3; ++p)
+#pragma unroll
+                for (int b = 0; b < BPG; ++b)
+                  bf[b][p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + ((BPG * bp + b) * 32 + li) * LS +
+                                                                   16 * ks + 8 * lh);
             }
-            nerf_bf16x8 bf[2][3];
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-#pragma unroll
-              for (int b = 0; b < 2; ++b)
-                bf[b][p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + ((2 * bp + b) * 32 + li) * LS + 16 * ks +
-                                                                 8 * lh);
 #pragma unroll
             for (int t = 0; t < 6; ++t)
 #pragma unroll
               for (int a = 0; a < TM; ++a)
 #pragma unroll
-                for (int b = 0; b < 2; ++b) {
+                for (int b = 0; b < BPG; ++b) {
                   if constexpr (BIGSMALL) {
                     if (t < 5)
-                      accs[a][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                          bf[b][X6_PB[t]], af[a][X6_PA[t]], accs[a][2 * bp + b], 0, 0, 0);
+                      accs[a][BPG * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                          bf[b][X6_PB[t]], af[a][X6_PA[t]], accs[a][BPG * bp + b], 0, 0, 0);
                     else
-                      acc[a][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                          bf[b][X6_PB[t]], af[a][X6_PA[t]], acc[a][2 * bp + b], 0, 0, 0);
+                      acc[a][BPG * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                          bf[b][X6_PB[t]], af[a][X6_PA[t]], acc[a][BPG * bp + b], 0, 0, 0);
                   } else {
-                    acc[a][2 * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[b][X6F_PB[t]], af[a][X6F_PA[t]],
-                                                                               acc[a][2 * bp + b], 0, 0, 0);
+                    acc[a][BPG * bp + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                        bf[b][X6F_PB[t]], af[a][X6F_PA[t]], acc[a][BPG * bp + b], 0, 0, 0);
                   }
                 }
-            if (PIPE && bp == TN / 2 - 1) {  // the pair's fragment reads, then one MFMA per ~4 VALU of the split
-              __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+            if constexpr (BPREF) {
 #pragma unroll
-              for (int q = 0; q < 6 * TM * 2; ++q) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-              }
+              for (int p = 0; p < 3; ++p) bfc[p] = bfn[p];
             }
-          }
-          if constexpr (PIPE) {
-#pragma unroll
-            for (int a = 0; a < TM; ++a)
-#pragma unroll
-              for (int p = 0; p < 3; ++p) afc[a][p] = afn[a][p];
           }
         }
         X6W_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);  // set j consumed: slab kt + 2 streams into it

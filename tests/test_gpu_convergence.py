@@ -70,7 +70,7 @@ def test_matched_psnr_fp32_bf16(env):
     make_scene, _, RayBatcher, _ = env
     from nerf_amd.losses import image_psnr
     from nerf_amd.ray_rendering import render_image
-    scene = make_scene(n_train=20, n_test=1, H=400, W=400, seed=3, device=DEV)
+    scene = make_scene(n_train=20, n_test=8, H=400, W=400, seed=3, device=DEV)
     rb = RayBatcher(scene, DEV)
     tr = _pair(env, lr=5e-4)
     psnr = {}
@@ -81,9 +81,14 @@ def test_matched_psnr_fp32_bf16(env):
         t.sync_to_modules()
         c, f = (n.eval() for n in t.nets)
         fx, fy, cx, cy = scene.intrinsics
-        img, _, _ = render_image(c, H=scene.H, W=scene.W, fx=fx, fy=fy, cx=cx, cy=cy, c2w=scene.test_poses[0],
-                                 near=scene.near, far=scene.far, ray_samples=64, n_importance=128, fine_model=f)
-        psnr[prec] = image_psnr(img, scene.test_images[0], "linear")
+        ps = []
+        for v in range(scene.test_poses.shape[0]):
+            img, _, _ = render_image(c, H=scene.H, W=scene.W, fx=fx, fy=fy, cx=cx, cy=cy, c2w=scene.test_poses[v],
+                                     near=scene.near, far=scene.far, ray_samples=64, n_importance=128, fine_model=f)
+            ps.append(image_psnr(img, scene.test_images[v], "linear"))
+        psnr[prec] = sum(ps) / len(ps)
     assert all(math.isfinite(v) and v > 20.0 for v in psnr.values()), psnr
-    assert abs(psnr["fp32"] - psnr["bf16"]) <= 0.5, psnr
+    # the bound is the measured trajectory noise (profiles/r04/psnr_band.txt: fp32 over 3 jitter seeds, mean of 8
+    # held-out views, sd 0.156 dB per trajectory -> the difference of two trajectories has sd 0.22 dB): 3 sd = 0.65 dB
+    assert abs(psnr["fp32"] - psnr["bf16"]) <= 0.65, psnr
     print(f"matched PSNR after 1000 steps: {psnr}")
