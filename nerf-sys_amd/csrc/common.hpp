@@ -6,6 +6,17 @@
 
 #define NERF_WAVE 64
 
+// Compute units of the current device (256 on MI355X), read once per process (one process per GPU).
+static inline int nerf_cu_count() {
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    n_cu = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+  }
+  return n_cu;
+}
+
 // Return the launch status of the last kernel as the C-ABI int convention.
 static inline int nerf_launch_status() {
   hipError_t e = hipGetLastError();

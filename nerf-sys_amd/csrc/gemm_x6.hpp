@@ -349,24 +349,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   // (the touch below), so the compiler's counted waits on its own activation loads never wait on these as well.  At two
   // waves per SIMD the extra live registers spill (fwd 0.62 -> 0.65 ms): plain loads there.  32-row waves (TM = 1) have
   // the registers: a forward of that shape went 0.76 -> 0.655 ms with them, still behind 0.63 ms for 64-row waves.
-#ifdef NERF_X6W_ASMB2  // A/B builds: inline-asm weight loads for the 64-row-wave forward too (with NERF_X6W_BF1)
-  constexpr bool ASMB = true;
-#else
   constexpr bool ASMB = BIGSMALL || TM == 1;
-#endif
-  // B fragments are read per group of BPG column blocks (BPG x 3 fragments live); NERF_X6W_BF1 (A/B builds): one
-  // block at a time, 12 VGPRs fewer, for the inline-asm weight loads' registers
-#ifdef NERF_X6W_BF1
-  constexpr int BPG = 1;
-#else
+  // B fragments are read per pair of column blocks (2 x 3 fragments live).  Measured and not kept (round 4,
+  // profiles/r04/x6_bfrag_ab.txt): one block at a time (fwd 0.603 -> 0.612 ms), with the next block read under the
+  // current block's MFMAs (0.613-0.619), and one block at a time with inline-asm weight loads (0.599-0.601)
   constexpr int BPG = 2;
-#endif
-#ifdef NERF_X6W_BPREF  // A/B builds (with NERF_X6W_BF1): block b + 1's fragments read under block b's MFMAs
-  constexpr bool BPREF = true;
-  static_assert(BPG == 1, "BPREF prefetches one block");
-#else
-  constexpr bool BPREF = false;
-#endif
 #define X6W_BLOAD(k0_)                                                                                    \
   if constexpr (ASMB) {                                                                                   \
     _Pragma("unroll") for (int a = 0; a < TM; ++a)                                                       \
@@ -435,13 +422,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
       if (ASMB || kt < nk) {
         X6W_BLOAD((kt + 1 < nk ? kt + 1 : kt) * BK);
         const nerf_bf16* S = smem + j * 3 * PL;
-        auto rd_b = [&](nerf_bf16x8 (&d)[3], int b, int ks_) {
-#pragma unroll
-          for (int p = 0; p < 3; ++p)
-            d[p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + (b * 32 + li) * LS + 16 * ks_ + 8 * lh);
-        };
-        nerf_bf16x8 bfc[3];  // BPREF: the current column block's fragments, the next block's read under its MFMAs
-        if constexpr (BPREF) rd_b(bfc, 0, 0);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           nerf_bf16x8 af[TM][3];
@@ -456,20 +436,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
           }
 #pragma unroll
           for (int bp = 0; bp < TN / BPG; ++bp) {  // groups of BPG column blocks: BPG x 3 B fragments live
-            nerf_bf16x8 bf[BPG][3], bfn[3];
-            if constexpr (BPREF) {
+            nerf_bf16x8 bf[BPG][3];
 #pragma unroll
-              for (int p = 0; p < 3; ++p) bf[0][p] = bfc[p];
-              if (bp + 1 < TN) rd_b(bfn, bp + 1, ks);
-              else if (ks + 1 < KS) rd_b(bfn, 0, ks + 1 < KS ? ks + 1 : ks);
-            } else {
+            for (int p = 0; p < 3; ++p)
 #pragma unroll
-              for (int p = 0; p < 3; ++p)
-#pragma unroll
-                for (int b = 0; b < BPG; ++b)
-                  bf[b][p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + ((BPG * bp + b) * 32 + li) * LS +
-                                                                   16 * ks + 8 * lh);
-            }
+              for (int b = 0; b < BPG; ++b)
+                bf[b][p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + ((BPG * bp + b) * 32 + li) * LS + 16 * ks +
+                                                                 8 * lh);
 #pragma unroll
             for (int t = 0; t < 6; ++t)
 #pragma unroll
@@ -488,10 +461,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
                         bf[b][X6F_PB[t]], af[a][X6F_PA[t]], acc[a][BPG * bp + b], 0, 0, 0);
                   }
                 }
-            if constexpr (BPREF) {
-#pragma unroll
-              for (int p = 0; p < 3; ++p) bfc[p] = bfn[p];
-            }
           }
         }
         X6W_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);  // set j consumed: slab kt + 2 streams into it

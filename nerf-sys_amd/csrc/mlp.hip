@@ -11,9 +11,9 @@
 // Activation layout in the caller's workspace (Mp = M rounded up to 256, row-major, fp32):
 //   X3E [Mp][320] : cols 0..255 = trunk.3 output, cols 256..318 = xyz encoding, col 319 = 0
 //                   (so trunk.4 reads cat([h, enc]) with K = 320 and no copy; trunk.0 reads cols 256..319)
-//   Y0..Y2, Y4..Y7 [Mp][256], O16 [Mp][32] (sigma_raw, geo0..14, 0...), CIN [Mp][64] (geo | dir-enc | 0),
-//   C0 [Mp][128], O3 [Mp][32].  Backward adds dA/dB [Mp][256], dO16 [Mp][32] (from the fused colour-branch
-//   backward), transposed trunk / head weights, and S split-M partial slabs of the packed gradient.
+//   Y0..Y2, Y4..Y7 [Mp][256], HO [Mp][4] (colour pre-activations 0..2, sigma_raw), CIN [Mp][64] (geo | dir-enc |
+//   0), C0 [Mp][128].  Backward adds dA/dB [Mp][256], dO16 [Mp][16] (from the fused colour-branch backward),
+//   transposed trunk weights, and S split-M partial slabs of the packed gradient.
 #include "gemm.hpp"
 #include "gemm_x6.hpp"
 #include "mlp_common.hpp"
@@ -25,7 +25,7 @@ using namespace nerf_mlp;
 
 struct WS {
   int64_t Mp;
-  float *X3E, *Y[8], *O16, *CIN, *C0, *O3;
+  float *X3E, *Y[8], *HO, *CIN, *C0;
   uint32_t* MB[8];  // ReLU bitmasks of the trunk outputs [Mp][8] (colour layer 0 re-derives its mask from C0 > 0)
   // backward
   float *dA, *dB, *dO16, *WT, *partial, *partial2;
@@ -37,7 +37,7 @@ struct WS {
   int64_t bytes;
 };
 
-constexpr int64_t WT_FLOATS = 7 * 65536 + 256 * 32;
+constexpr int64_t WT_FLOATS = 7 * 65536;
 // bf16 piece planes (gemm_x6.hpp): forward 3 x 256 x sum(KPAD) bf16, input gradient 7 x 3 x 256 x 256 bf16
 inline int64_t x6_fwd_off(int i) {
   int64_t o = 0;
@@ -45,13 +45,9 @@ inline int64_t x6_fwd_off(int i) {
   return o;
 }
 constexpr int64_t X6_BWD_BF16 = 7 * 3 * 65536;
-// the head backward (dZ7, head weight / bias sums) is one pass (head_bwd_kernel) unless NERF_BWD_TAIL_CHAIN keeps the
-// separate head dgrad / wgrad GEMMs for A/B runs; the second-half sums of the split walks start at P2BASE
-#ifndef NERF_BWD_TAIL_CHAIN
+// the head backward (dZ7, head weight / bias sums) is one pass (head_bwd_kernel); the second-half sums of the split
+// walks (head + colour tensors) start at P2BASE
 #define P2BASE (layout().off[16])
-#else
-#define P2BASE (layout().off[18])
-#endif
 
 WS carve(void* base, int64_t M, int training) {
   WS w{};
@@ -71,10 +67,9 @@ WS carve(void* base, int64_t M, int training) {
     float* q = take(Mp * 256);
     for (int i = 0; i < 8; ++i) w.Y[i] = (i % 2 == 0) ? q : w.X3E;  // ping-pong
   }
-  w.O16 = take(Mp * 32);
+  w.HO = take(Mp * 4);
   w.CIN = take(Mp * 64);
   w.C0 = take(Mp * 128);
-  w.O3 = take(Mp * 32);
   if (training) {
     for (int i = 0; i < 8; ++i) w.MB[i] = reinterpret_cast<uint32_t*>(take(Mp * 8));
     if (training == 2) {  // the weight-gradient stream reads dZ_i while the input-gradient chain runs ahead
@@ -85,7 +80,7 @@ WS carve(void* base, int64_t M, int training) {
       w.dA = take(Mp * 256);
       w.dB = take(Mp * 256);
     }
-    w.dO16 = take(Mp * 32);  // [Mp][16] for the fused head backward, [Mp][32] for the chain
+    w.dO16 = take(Mp * 16);  // [Mp][16]: the head-output gradient, written by color_bwd, read by head_bwd
     w.WT = take(WT_FLOATS);
     w.WPb = reinterpret_cast<nerf_bf16*>(take(X6_BWD_BF16 / 2));
     w.S = n_splits(Mp);
@@ -130,50 +125,6 @@ __global__ void pe_xyz_kernel(const float* __restrict__ xd, int64_t M, int64_t M
   v[63] = 0.f;
 #pragma unroll
   for (int c = 0; c < 16; ++c) q4[c] = make_float4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
-}
-
-// CIN[m] = [O16[m][1..15], direction encoding (27), zeros]
-__global__ void build_cin_kernel(const float* __restrict__ xd, const float* __restrict__ O16, int64_t M, int64_t Mp,
-                                 float* __restrict__ CIN) {
-  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= Mp) return;
-  float4* q4 = reinterpret_cast<float4*>(CIN + m * 64);
-  if (m >= M) {
-    for (int c = 0; c < 16; ++c) q4[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-    return;
-  }
-  float v[64];
-  const float* o = O16 + m * 32;
-#pragma unroll
-  for (int c = 0; c < 15; ++c) v[c] = o[1 + c];
-  const float d[3] = {xd[m * 6 + 3], xd[m * 6 + 4], xd[m * 6 + 5]};
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    v[15 + k] = d[k];
-    float band = 1.0f;
-#pragma unroll
-    for (int l = 0; l < 4; ++l) {
-      float s, c;
-      sincosf(d[k] * band, &s, &c);
-      v[18 + k * 8 + l] = c;
-      v[18 + k * 8 + 4 + l] = s;
-      band *= 2.0f;
-    }
-  }
-#pragma unroll
-  for (int c = 42; c < 64; ++c) v[c] = 0.f;
-#pragma unroll
-  for (int c = 0; c < 16; ++c) q4[c] = make_float4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
-}
-
-__global__ void head_out_kernel(const float* __restrict__ O3, const float* __restrict__ O16, int64_t M,
-                                float* __restrict__ out) {
-  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
-  const float* c = O3 + m * 32;
-  const float sr = O16[m * 32];
-  const float sg = expf(fminf(fmaxf(sr, -EXP_MAX), EXP_MAX));
-  reinterpret_cast<float4*>(out)[m] = make_float4(sigmoidf_(c[0]), sigmoidf_(c[1]), sigmoidf_(c[2]), sg);
 }
 
 // batched transpose: dst_i[c][r] = src_i[r][c] for r < rows_i, c < cols_i  (src pitch lds_i)
@@ -415,37 +366,21 @@ extern "C" int nerf_mlp_fwd_ex(const float* w, const float* x_d, int64_t M, floa
     in = out;
     ld_in = ld_out;
   }
-  // heads + colour MLP + output activations in ONE launch (mlp_fwd_tail.hpp); NERF_FWD_TAIL_CHAIN keeps the
-  // five-launch chain (head GEMM, colour-input build, colour GEMMs, head_out) for A/B runs
-#ifndef NERF_FWD_TAIL_CHAIN
+  // heads + colour MLP + output activations in ONE launch (mlp_fwd_tail.hpp)
   {
-    static int n_cu = 0;
-    if (!n_cu) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
-    }
     FwdTailArgs T{};
     T.Y7 = in; T.ldy = ld_in; T.xd = x_d; T.w = w;
     T.off_wh = L.off[16]; T.off_bh = L.off[17]; T.off_wc0 = L.off[18]; T.off_bc0 = L.off[19];
     T.off_wc1 = L.off[20]; T.off_bc1 = L.off[21];
-    T.O16 = W.O16; T.CIN = W.CIN; T.C0 = W.C0; T.O3 = W.O3; T.out = rgb_sigma;
+    T.HO = W.HO; T.CIN = W.CIN; T.C0 = W.C0; T.out = rgb_sigma;
     T.M = M; T.Mp = Mp; T.ntiles = (int)(Mp / FT_ROWS);
+    const int n_cu = nerf_cu_count();
     const int grid = T.ntiles < 2 * n_cu ? T.ntiles : 2 * n_cu;
     if (training)
       fwd_tail_kernel<true><<<grid, 256, 0, st>>>(T);
     else
       fwd_tail_kernel<false><<<grid, 256, 0, st>>>(T);
   }
-#else
-  TRY(nt<EPI_BIAS>(in, ld_in, Wt(16), 256, Wt(17), W.O16, 32, nullptr, nullptr, Mp, 32, 256, st));
-  build_cin_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(x_d, W.O16, M, Mp, W.CIN);
-  // K = 48: the colour input has 42 real columns (15 geo + 27 direction PE), columns 48..63 are zero in CIN
-  TRY(nt<EPI_BIAS_RELU>(W.CIN, 64, Wt(18), 64, Wt(19), W.C0, 128, nullptr, nullptr, Mp, 128, 48,
-                        st));
-  TRY(nt<EPI_BIAS>(W.C0, 128, Wt(20), 128, Wt(21), W.O3, 32, nullptr, nullptr, Mp, 32, 128, st));
-  head_out_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(W.O3, W.O16, M, rgb_sigma);
-#endif
   return nerf_launch_status();
 }
 
@@ -511,9 +446,6 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
       xj.j[i - 1] = X6Job{Wt(2 * i), W.WPb + 3 * 65536 * (int64_t)(i - 1), 256, 256, KPAD[i], 1, 65536};
     x6_planes_kernel<<<dim3(8, 8, 7), 256, 0, st>>>(xj);
   }
-#ifdef NERF_BWD_TAIL_CHAIN
-  float* Wht = W.WT + 7 * 65536;  jobs.j[nj++] = TJob{Wt(16), Wht, 32, 256, 256};  // [256][32]
-#endif
   if (nj) transpose_kernel<<<dim3(8, 8, nj), 256, 0, st>>>(jobs);
 
   // colour branch + head activations in one kernel: dO16 and the colour weight / bias slabs (two workgroups per
@@ -522,26 +454,14 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
   float* dnext = W.dB;
   // events 2/3 (layer 0 has no input gradient) bracket the backward tail (colour branch + heads -> dZ7)
   if (ev) (void)hipEventRecord(ev[2], st);
-#ifndef NERF_BWD_TAIL_CHAIN
   // colour branch -> dO16 [Mp][16]; then ONE pass over Y7 for dZ7 and the head weight / bias sums (mlp_tail.hpp)
-  color_bwd_kernel<float, float><<<2 * W.S, 256, 0, st>>>(d_rgb_sigma, W.O3, W.O16, W.C0, W.CIN, Wt(18), Wt(20), W.dO16,
+  color_bwd_kernel<float, float><<<2 * W.S, 256, 0, st>>>(d_rgb_sigma, W.HO, W.C0, W.CIN, Wt(18), Wt(20), W.dO16,
                                                           W.partial, L.total, L.off[18], L.off[19], L.off[20], L.off[21],
                                                           W.rps, M, Mp, W.partial2, L.total - P2BASE, P2BASE, 16);
   head_bwd_kernel<<<2 * W.S, 256, 0, st>>>(W.dO16, W.Y[7], Wt(16), dcur, W.partial, L.total, W.partial2,
                                            L.total - P2BASE, P2BASE, L.off[16], L.off[17], W.rps, Mp);
   if (ev) (void)hipEventRecord(ev[3], st);
   TRY(handoff(1));  // dZ7 and the head / colour slabs are complete
-#else
-  color_bwd_kernel<float, float><<<2 * W.S, 256, 0, st>>>(d_rgb_sigma, W.O3, W.O16, W.C0, W.CIN, Wt(18), Wt(20), W.dO16, W.partial,
-                                        L.total, L.off[18], L.off[19], L.off[20], L.off[21], W.rps, M, Mp, W.partial2,
-                                        L.total - P2BASE, P2BASE, 32);
-  // heads -> dZ7.  K = 16: head rows 16..31 are padding (zero weights, zero dO16 columns), so their products are
-  // exact zeros and dropping them changes no bit of dZ7
-  TRY(nt<EPI_MASK>(W.dO16, 32, Wht, 32, nullptr, dcur, 256, W.MB[7], nullptr, Mp, 256, 16, st));
-  if (ev) (void)hipEventRecord(ev[3], st);
-  TRY(handoff(1));  // dZ7 and dO16 are complete (the colour branch ran before the head dgrad on st)
-  TRY(wgrad(W.dO16, 32, W.Y[7], 256, 16, W, 32, 256, sw));
-#endif
   // trunk
   for (int i = 7; i >= 0; --i) {
     const float* X = (i == 0) ? W.X3E + 256 : (i == 4 ? W.X3E : W.Y[i - 1]);

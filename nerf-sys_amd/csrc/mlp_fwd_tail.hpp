@@ -7,7 +7,7 @@
 //   rgb_sigma = [sigmoid(O3), trunc_exp(sigma_raw)]                              (models/trunc_exp.py:30-61)
 // The unfused chain ran five launches per net (two N = 32 GEMMs, the colour-input build, the colour layer-0 GEMM and
 // the head activation) and moved ~2.9 KB per sample row through HBM; this kernel reads the trunk.7 row (1 KB) and
-// the direction, and writes what the backward reads (O16 128 B, CIN 256 B, C0 512 B, O3 128 B) and rgb_sigma.
+// the direction, and writes what the backward reads (HO 16 B, CIN 256 B, C0 512 B) and rgb_sigma.
 //
 // Geometry: a 256-thread workgroup (4 waves) walks 64-row tiles (persistent, two workgroups per CU); wave w owns rows
 // 16 w .. 16 w + 15 of the tile through all three layers.  Every product is v_mfma_f32_16x16x4_f32 (exact fp32 fmaf
@@ -36,7 +36,7 @@ struct FwdTailArgs {
   const float* xd;   // [M][6] (directions in cols 3..5)
   const float* w;    // packed fp32 parameters
   int64_t off_wh, off_bh, off_wc0, off_bc0, off_wc1, off_bc1;
-  float *O16, *CIN, *C0, *O3;  // [Mp][32], [Mp][64], [Mp][128], [Mp][32] (training: what the backward reads)
+  float *HO, *CIN, *C0;        // [Mp][4] (o3_0..2, sigma_raw), [Mp][64], [Mp][128] (training: what the backward reads)
   float* out;                  // [M][4] rgb_sigma
   int64_t M, Mp;
   int ntiles, ldy;
@@ -99,10 +99,6 @@ __global__ __launch_bounds__(256, 2) void fwd_tail_kernel(FwdTailArgs A) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) o16[r] = ah[r] + sB[4 * g + r];
     const float sigma_raw = o16[0];  // meaningful in lanes g == 0
-    if (TRAIN) {
-      *reinterpret_cast<float4*>(A.O16 + m * 32 + 4 * g) = make_float4(o16[0], o16[1], o16[2], o16[3]);
-      *reinterpret_cast<float4*>(A.O16 + m * 32 + 16 + 4 * g) = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
     // ---- colour input in the head's alignment: chunk 0 = O16 columns 0..15, chunks 1, 2 = canonical CIN
     // columns 15 + 4g + s and 31 + 4g + s (direction and its encoding); rows >= M are all zero (build_cin_kernel)
     const bool real = m < A.M;
@@ -183,10 +179,9 @@ __global__ __launch_bounds__(256, 2) void fwd_tail_kernel(FwdTailArgs A) {
     float o3[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) o3[r] = ao[r] + sB[144 + 4 * g + r];
-    if (TRAIN) {
-      *reinterpret_cast<float4*>(A.O3 + m * 32 + 4 * g) = make_float4(o3[0], o3[1], o3[2], o3[3]);
-      *reinterpret_cast<float4*>(A.O3 + m * 32 + 16 + 4 * g) = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    // the backward's head-output inputs, one 16-B row (round 4; the [Mp][32] O16 / O3 rows, 256 B written and read
+    // back at line granularity for 16 used bytes, are gone): the colour pre-activations and sigma_raw
+    if (TRAIN && g == 0) reinterpret_cast<float4*>(A.HO)[m] = make_float4(o3[0], o3[1], o3[2], sigma_raw);
     if (g == 0 && real) {
       const float sg = expf(fminf(fmaxf(sigma_raw, -EXP_MAX), EXP_MAX));
       reinterpret_cast<float4*>(A.out)[m] = make_float4(sigmoidf_(o3[0]), sigmoidf_(o3[1]), sigmoidf_(o3[2]), sg);

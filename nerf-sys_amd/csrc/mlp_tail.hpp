@@ -41,8 +41,7 @@ __device__ __forceinline__ void tail_st4(__bf16* p, float4 v) {
 }
 
 template <typename TA, typename TD>
-__global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restrict__ g, const float* __restrict__ O3,
-                                                        const float* __restrict__ O16,
+__global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restrict__ g, const float* __restrict__ HO,
                                                         const TA* __restrict__ C0,
                                                         const TA* __restrict__ CIN,
                                                         const float* __restrict__ Wc0,  // [128][64]
@@ -80,9 +79,8 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
 
   // register prefetch of one tile: C0 = 2048 float4 (8 / thread), CIN = 1024 float4 (4 / thread); wave 0 also
   // prefetches the tile's head outputs: d_rgb_sigma (M rows: the row index is clamped, the value zeroed below for
-  // m >= M), the three colour pre-activations of O3 and sigma_raw of O16.
+  // m >= M) and the HO row (the three colour pre-activations, sigma_raw).
   float4 pc[8], pi[4], pg = make_float4(0.f, 0.f, 0.f, 0.f), po = pg;
-  float ps = 0.f;
   // r0, r1, rps and the half length are multiples of CB_ROWS (the host rounds rps to 64; Mp is a multiple of 256),
   // so every row of a tile is < r1 and the loads carry no row guard (a guarded load became a branch with a
   // vmcnt(0) drain after it); a uniform tile base + 32-bit lane offsets keeps no 64-bit address per load live
@@ -96,8 +94,7 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
     if (tid < CB_ROWS) {  // wave 0 (uniform branch)
       const int64_t m = t0 + tid, mc = m < M ? m : M - 1;
       pg = reinterpret_cast<const float4*>(g)[mc];
-      po = *reinterpret_cast<const float4*>(O3 + m * 32);
-      ps = O16[m * 32];
+      po = reinterpret_cast<const float4*>(HO)[m];
     }
   };
 
@@ -129,7 +126,7 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
         a = pg.x * (s0 * (1.0f - s0));
         b = pg.y * (s1 * (1.0f - s1));
         c = pg.z * (s2 * (1.0f - s2));
-        ds = pg.w * expf(fminf(fmaxf(ps, -EXP_MAX), EXP_MAX));
+        ds = pg.w * expf(fminf(fmaxf(po.w, -EXP_MAX), EXP_MAX));
       }
       s_do3[tid * 4 + 0] = a;
       s_do3[tid * 4 + 1] = b;
