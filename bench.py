@@ -394,7 +394,10 @@ def roofline(tm, bf16, overlap, bf16_flags=0, split=False):
                     "frac": round(X6_PRODUCTS * ach / BF16_MFMA_PEAK_TFLOPS, 4),
                     "flop_per_launch": X6_PRODUCTS * flop256, "fp32_flop_per_launch": flop256,
                     "fp32_equiv_tflops": round(ach, 2),
-                    "fp32_equiv_frac_of_fp32_peak": round(ach / FP32_MFMA_PEAK_TFLOPS, 4)}
+                    "fp32_equiv_frac_of_fp32_peak": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                    # the split method's own ceiling: the dense bf16 peak over 6 products per fp32 product (= `frac`)
+                    "split_ceiling_fp32_equiv_tflops": round(BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS, 1),
+                    "fp32_equiv_frac_of_split_ceiling": round(ach / (BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS), 4)}
         else:
             roof = {"bound": "mfma", "kernel": kern, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "flop_per_launch": flop256}
