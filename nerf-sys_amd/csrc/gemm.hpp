@@ -473,18 +473,41 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt16_kernel(const float* __res
   }
 }
 
-// dst[i] = (acc ? dst[i] : 0) + sum_{s<S} src[s*slab + i]   (float4 lanes, deterministic order)
-static __global__ void reduce_splits_kernel(const float* __restrict__ src, int64_t slab, int S, float* __restrict__ dst,
-                                     int64_t n4, int accumulate) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n4) return;
-  float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-  const float4* p = reinterpret_cast<const float4*>(src) + i;
-  const int64_t st = slab / 4;
+// Split-M reduce (round 4): a float4 element's S slab terms in RG consecutive groups of slabs, one wave per group (64
+// elements per 256-thread block), each group summed in slab order from 0, then the group sums added in group order onto
+// the initial value by wave 0.  A fixed order — bitwise reproducible, and the same in every reduce kernel (the layered
+// and the fused bf16 backward stay bitwise equal) — with RG times the loads in flight of one thread walking all S
+// slabs: that walk is latency-bound (the 131-MB bf16 reduce ran at ~1 TB/s, 130 us per call).
+constexpr int RG = 4;
+__device__ __forceinline__ float4 rg_group_sum(const float* __restrict__ base, int64_t stride, int S, int g) {
+  const int s0 = (int)((int64_t)S * g / RG), s1 = (int)((int64_t)S * (g + 1) / RG);
+  const float4* p = reinterpret_cast<const float4*>(base);
+  const int64_t st = stride / 4;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 16
-  for (int s = 0; s < S; ++s) {  // loads batched by the unroll, adds kept in split order
+  for (int s = s0; s < s1; ++s) {  // loads batched by the unroll, adds kept in split order
     const float4 v = p[s * st];
     a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
   }
-  reinterpret_cast<float4*>(dst)[i] = a;
+  return a;
+}
+__device__ __forceinline__ void rg_add(float4& a, const float4& v) {
+  a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+}
+
+// dst[i] = (acc ? dst[i] : 0) + sum_{s<S} src[s*slab + i]   (float4 lanes, the RG-group order above); grid cdiv(n4, 64)
+static __global__ __launch_bounds__(256) void reduce_splits_kernel(const float* __restrict__ src, int64_t slab, int S,
+                                                                   float* __restrict__ dst, int64_t n4,
+                                                                   int accumulate) {
+  __shared__ float4 part[RG][64];
+  const int e = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + e;
+  part[g][e] = i < n4 ? rg_group_sum(src + 4 * i, slab, S, g) : make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  if (g == 0 && i < n4) {
+    float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < RG; ++k) rg_add(a, part[k][e]);
+    reinterpret_cast<float4*>(dst)[i] = a;
+  }
 }

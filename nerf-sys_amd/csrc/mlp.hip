@@ -490,7 +490,7 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
     TRY(nerf_hip_status(hipStreamWaitEvent(st, sync[9], 0)));
   }
   const int64_t n4 = L.total / 4;
-  reduce_splits2_kernel<<<(unsigned)nerf_cdiv(n4, 256), 256, 0, st>>>(W.partial, L.total, W.S, d_w, n4, accumulate,
+  reduce_splits2_kernel<<<(unsigned)nerf_cdiv(n4, 64), 256, 0, st>>>(W.partial, L.total, W.S, d_w, n4, accumulate,
                                                                       W.partial2, L.total - P2BASE, P2BASE / 4);
   return nerf_launch_status();
 }

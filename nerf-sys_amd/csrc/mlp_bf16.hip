@@ -393,14 +393,18 @@ int fused_forward(const float* w, const float* x_d, int64_t M, float* rgb_sigma,
 //   trunk.0 W / b and trunk.4 W[:, 256:320]  sum over the S2 narrow sub-slabs (np);
 //   everything else                          sum over the S split slabs, plus (e >= off16: head / colour) the S
 //                                            second-half tail slabs after them.
-__global__ void reduce_fused_bf16_kernel(const float* __restrict__ partial, int64_t slab, int S,
-                                         const float* __restrict__ partial2, int64_t slab2, int64_t off16,
-                                         const float* __restrict__ np, int S2, float* __restrict__ dst, int64_t n4,
-                                         int accumulate, int64_t off0, int64_t off1, int64_t off8) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n4) return;
+__global__ __launch_bounds__(256) void reduce_fused_bf16_kernel(const float* __restrict__ partial, int64_t slab, int S,
+                                                                const float* __restrict__ partial2, int64_t slab2,
+                                                                int64_t off16, const float* __restrict__ np, int S2,
+                                                                float* __restrict__ dst, int64_t n4, int accumulate,
+                                                                int64_t off0, int64_t off1, int64_t off8) {
+  // gemm.hpp's RG-group order (one wave per group of slabs, 64 elements per block; grid cdiv(n4, 64)): the 256-wide
+  // trunk weights sum exactly as the layered path's reduce_splits_kernel does
+  __shared__ float4 part[2][RG][64];
+  const int el = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + el;
   const int64_t e = 4 * i;
-  float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
   int64_t nofs = -1;  // offset in the narrow slab, or -1
   if (e >= off0 && e < off0 + 256 * 64) nofs = e - off0;
   else if (e >= off1 && e < off1 + 256) nofs = 32768 + (e - off1);
@@ -408,21 +412,20 @@ __global__ void reduce_fused_bf16_kernel(const float* __restrict__ partial, int6
     const int64_t n = (e - off8) / 320, k = (e - off8) % 320 - 256;
     nofs = 16384 + n * 64 + k;
   }
-  auto add = [&](const float* base, int64_t stride, int count) {
-    const float4* p = reinterpret_cast<const float4*>(base);
-#pragma unroll 16
-    for (int s = 0; s < count; ++s) {
-      const float4 v = p[s * (stride / 4)];
-      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  const bool live = i < n4, two = live && nofs < 0 && e >= off16;
+  part[0][g][el] = !live ? z : (nofs >= 0 ? rg_group_sum(np + nofs, NPS, S2, g) : rg_group_sum(partial + e, slab, S, g));
+  part[1][g][el] = two ? rg_group_sum(partial2 + (e - off16), slab2, S, g) : z;
+  __syncthreads();
+  if (g == 0 && live) {
+    float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : z;
+#pragma unroll
+    for (int k = 0; k < RG; ++k) rg_add(a, part[0][k][el]);
+    if (two) {
+#pragma unroll
+      for (int k = 0; k < RG; ++k) rg_add(a, part[1][k][el]);
     }
-  };
-  if (nofs >= 0) {
-    add(np + nofs, NPS, S2);
-  } else {
-    add(partial + e, slab, S);
-    if (e >= off16) add(partial2 + (e - off16), slab2, S);
+    reinterpret_cast<float4*>(dst)[i] = a;
   }
-  reinterpret_cast<float4*>(dst)[i] = a;
 }
 
 // The fused bf16 backward: ONE tail launch (mlp_bf16_tail.hpp: head-output derivatives, colour branch, head dgrad +
@@ -482,7 +485,7 @@ int fused_backward(const float* w, int64_t M, const float* d_rgb_sigma, float* d
                                                                   NPS, W.rps2, Mp, 1, 2);
   if (ev) (void)hipEventRecord(ev[1], st);
   const int64_t n4 = L.total / 4;
-  reduce_fused_bf16_kernel<<<(unsigned)nerf_cdiv(n4, 256), 256, 0, st>>>(
+  reduce_fused_bf16_kernel<<<(unsigned)nerf_cdiv(n4, 64), 256, 0, st>>>(
       W.partial, L.total, W.S, W.partial2, L.total - L.off[16], L.off[16], W.np, W.S2, d_w, n4, accumulate, L.off[0],
       L.off[1], L.off[8]);
   return nerf_launch_status();
@@ -595,6 +598,6 @@ extern "C" int nerf_mlp_bwd_bf16(const float* w, int64_t M, const float* d_rgb_s
     }
   }
   const int64_t n4 = L.total / 4;
-  reduce_splits_kernel<<<(unsigned)nerf_cdiv(n4, 256), 256, 0, st>>>(W.partial, L.total, W.S, d_w, n4, accumulate);
+  reduce_splits_kernel<<<(unsigned)nerf_cdiv(n4, 64), 256, 0, st>>>(W.partial, L.total, W.S, d_w, n4, accumulate);
   return nerf_launch_status();
 }

@@ -350,29 +350,29 @@ static __global__ __launch_bounds__(256, 2) void head_bwd_kernel(const float* __
   if (tid >= 16 && tid < 32) P[off_bh + tid] = 0.f;
 }
 
-// reduce_splits plus the second-half colour sums: float4 i >= c0 of the packed gradient also adds
-// sum_s src2[s][i - c0] after the S slab terms (fixed order: bitwise reproducible)
-static __global__ void reduce_splits2_kernel(const float* __restrict__ src, int64_t slab, int S, float* __restrict__ dst,
-                                      int64_t n4, int accumulate, const float* __restrict__ src2, int64_t slab2,
-                                      int64_t c0) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n4) return;
-  float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-  const float4* p = reinterpret_cast<const float4*>(src) + i;
-#pragma unroll 16
-  for (int s = 0; s < S; ++s) {  // loads batched by the unroll, adds kept in split order
-    const float4 v = p[s * (slab / 4)];
-    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-  }
-  if (i >= c0) {
-    const float4* q = reinterpret_cast<const float4*>(src2) + (i - c0);
-#pragma unroll 16
-    for (int s = 0; s < S; ++s) {
-      const float4 v = q[s * (slab2 / 4)];
-      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+// reduce_splits plus the second-half colour sums: float4 i >= c0 of the packed gradient also adds the S terms of src2
+// (src2[s][i - c0]) after the slab terms, both in gemm.hpp's RG-group order (bitwise reproducible); grid cdiv(n4, 64)
+static __global__ __launch_bounds__(256) void reduce_splits2_kernel(const float* __restrict__ src, int64_t slab, int S,
+                                                                    float* __restrict__ dst, int64_t n4, int accumulate,
+                                                                    const float* __restrict__ src2, int64_t slab2,
+                                                                    int64_t c0) {
+  __shared__ float4 part[2][RG][64];
+  const int e = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + e;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  part[0][g][e] = i < n4 ? rg_group_sum(src + 4 * i, slab, S, g) : z;
+  part[1][g][e] = (i < n4 && i >= c0) ? rg_group_sum(src2 + 4 * (i - c0), slab2, S, g) : z;
+  __syncthreads();
+  if (g == 0 && i < n4) {
+    float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : z;
+#pragma unroll
+    for (int k = 0; k < RG; ++k) rg_add(a, part[0][k][e]);
+    if (i >= c0) {
+#pragma unroll
+      for (int k = 0; k < RG; ++k) rg_add(a, part[1][k][e]);
     }
+    reinterpret_cast<float4*>(dst)[i] = a;
   }
-  reinterpret_cast<float4*>(dst)[i] = a;
 }
 
 }  // namespace nerf_mlp
