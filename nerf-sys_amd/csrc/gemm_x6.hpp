@@ -297,6 +297,19 @@ __device__ __forceinline__ void x6_epilogue_lds(nerf_f32x16 (&acc)[TM][TN], int6
   }
 }
 
+#ifdef NERF_X6W_STAMPS  // diagnostic builds only (tools/x6_stamps.py): s_memtime per pipeline point, one workgroup
+__device__ unsigned long long nerf_x6_stamps[2][8][128];
+#define X6W_STAMP()                                                                                       \
+  if (stamp_on) {                                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                                                    \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                           \
+    if (lane == 0 && si_ < 128) nerf_x6_stamps[BIGSMALL ? 1 : 0][wave][si_] = t_;                          \
+    ++si_;                                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                                    \
+  }
+#else
+#define X6W_STAMP()
+#endif
 // ------------------------------------------------------------------------------------------ gemm_nt_x6w
 // Wide-wave form of gemm_nt_x6: a (64 NW) x 128 workgroup tile whose NW waves each own 64 rows x ALL 128 columns
 // (2 x 4 MFMA tiles), so every activation row is loaded and split by exactly one wave (gemm_nt_x6's 64 x 64 waves
@@ -319,11 +332,25 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   constexpr int KS = BK / 16, CPR = BK / 8;       // MFMA k-steps / 16-B weight chunks per row, per slab
   constexpr int BCH = 3 * BN * CPR / NT;          // weight chunks per thread per slab
   static_assert((3 * BN * CPR) % NT == 0 && (BN * CPR) % NT == 0, "weight staging");
+#ifdef NERF_X6W_SWIZZLE  // (validation pending: default after its GPU tests)
+  // weight images [BN][BK] bf16 unpadded, 16-B chunk q of row r in slot q ^ ((r >> 2) & 3) (BK = 32: four chunks per
+  // 64-B row): the staging writes (4 rows x 4 chunks per 16-lane group) and the fragment reads (16 consecutive rows,
+  // one chunk) both hit 16 distinct 16-B bank slots.  The 80-B padded pitch it replaces was 2-way conflicted on the
+  // staging writes (PMC SQ_LDS_BANK_CONFLICT 8.5e6 cycles per fine forward launch, profiles/r04/pmc_split.txt).
+  constexpr int LS = BK;
+  static_assert(BK == 32, "the swizzle assumes four 16-B chunks per row");
+  auto sw = [](int r, int q) { return q ^ ((r >> 2) & 3); };
+#else  // A/B builds: the 80-B padded pitch
   constexpr int LS = BK + 8;
+  auto sw = [](int r, int q) { return q; };
+#endif
   constexpr int PL = BN * LS;
   __shared__ __attribute__((aligned(16))) nerf_bf16 smem[2 * 3 * PL];
   static_assert(NW * X6E_WAVE_FLOATS * 4 <= 2 * 3 * PL * 2, "epilogue tiles fit in the weight images");
 
+#ifdef NERF_X6W_STAGGER  // probe builds: every other workgroup starts ~NERF_X6W_STAGGER x 64 clocks late
+  if ((blockIdx.x >> 3) & 1) __builtin_amdgcn_s_sleep(NERF_X6W_STAGGER);
+#endif
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
   const int64_t m0 = (int64_t)mt * BM;
@@ -387,7 +414,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
 #define X6W_BSTORE(buf_)                                                                                  \
   _Pragma("unroll") for (int i = 0; i < BCH; ++i) {                                                      \
     const int c = tid + NT * i, p = c / (BN * CPR), r = (c / CPR) % BN, q = c % CPR;                     \
-    *reinterpret_cast<uint4*>(smem + ((buf_) * 3 + p) * PL + r * LS + 8 * q) = rb[i];                    \
+    *reinterpret_cast<uint4*>(smem + ((buf_) * 3 + p) * PL + r * LS + 8 * sw(r, q)) = rb[i];             \
   }
 
   // BIGSMALL: the five small piece products accumulate in their own registers (2^-8 of the hi.hi sum, so the bf16
@@ -413,6 +440,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   }
   X6W_BSTORE(0);
   __syncthreads();
+#ifdef NERF_X6W_STAMPS
+  const bool stamp_on = blockIdx.x == 777 && (BIGSMALL || EPI == EPI_BIAS_RELU);
+  int si_ = 0;
+#endif
+  X6W_STAMP();
   for (int kt0 = 0; kt0 < nk; kt0 += 2) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {  // slab kt = kt0 + j: LDS buffer j, activation register set j
@@ -434,6 +466,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
             af[a][1] = __builtin_bit_cast(nerf_bf16x8, make_uint4(m0_.x, m0_.y, m1.x, m1.y));
             af[a][2] = __builtin_bit_cast(nerf_bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
           }
+          X6W_STAMP();
 #pragma unroll
           for (int bp = 0; bp < TN / BPG; ++bp) {  // groups of BPG column blocks: BPG x 3 B fragments live
             nerf_bf16x8 bf[BPG][3];
@@ -441,8 +474,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
             for (int p = 0; p < 3; ++p)
 #pragma unroll
               for (int b = 0; b < BPG; ++b)
-                bf[b][p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + ((BPG * bp + b) * 32 + li) * LS + 16 * ks +
-                                                                 8 * lh);
+                bf[b][p] = *reinterpret_cast<const nerf_bf16x8*>(S + p * PL + ((BPG * bp + b) * 32 + li) * LS +
+                                                                 8 * sw((BPG * bp + b) * 32 + li, 2 * ks + lh));
 #pragma unroll
             for (int t = 0; t < 6; ++t)
 #pragma unroll
@@ -462,11 +495,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
                   }
                 }
           }
+          X6W_STAMP();
         }
         X6W_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);  // set j consumed: slab kt + 2 streams into it
         X6W_BWAIT();
+        X6W_STAMP();
         X6W_BSTORE(j ^ 1);
         __syncthreads();
+        X6W_STAMP();
       }
     }
   }
@@ -490,6 +526,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   x6_epilogue_lds<TM, TN, EPI>(acc, m0 + wave * WTM, n0, lane, bias, C, ldc, mbits, ldmb, mbits_out,
                                reinterpret_cast<float*>(smem) + wave * X6E_WAVE_FLOATS);
 #endif
+  X6W_STAMP();
 }
 
 // ------------------------------------------------------------------------------------------ gemm_wgrad_x6

@@ -384,6 +384,12 @@ extern "C" int nerf_mlp_fwd_ex(const float* w, const float* x_d, int64_t M, floa
   return nerf_launch_status();
 }
 
+#ifdef NERF_X6W_STAMPS  // diagnostic builds only: the split NT kernels' pipeline stamps (tools/x6_stamps.py)
+extern "C" int nerf_debug_x6_stamps(unsigned long long* out) {
+  return nerf_hip_status(hipMemcpyFromSymbol(out, HIP_SYMBOL(nerf_x6_stamps), sizeof(nerf_x6_stamps)));
+}
+#endif
+
 extern "C" int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws, int64_t ws_bytes,
                             int training, hipEvent_t* ev, hipStream_t st) {
   return nerf_mlp_fwd_ex(w, x_d, M, rgb_sigma, ws, ws_bytes, training, 0, ev, st);
