@@ -332,7 +332,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   constexpr int KS = BK / 16, CPR = BK / 8;       // MFMA k-steps / 16-B weight chunks per row, per slab
   constexpr int BCH = 3 * BN * CPR / NT;          // weight chunks per thread per slab
   static_assert((3 * BN * CPR) % NT == 0 && (BN * CPR) % NT == 0, "weight staging");
-#ifdef NERF_X6W_SWIZZLE  // (validation pending: default after its GPU tests)
+#if !defined(NERF_X6W_REGB) || defined(NERF_X6W_SWIZZLE)
   // weight images [BN][BK] bf16 unpadded, 16-B chunk q of row r in slot q ^ ((r >> 2) & 3) (BK = 32: four chunks per
   // 64-B row): the staging writes (4 rows x 4 chunks per 16-lane group) and the fragment reads (16 consecutive rows,
   // one chunk) both hit 16 distinct 16-B bank slots.  The 80-B padded pitch it replaces was 2-way conflicted on the
@@ -363,8 +363,26 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
 #pragma unroll
   for (int a = 0; a < TM; ++a) aoff[a] = (a * 32 + li) * lda + 8 * lh;
 
+#ifndef NERF_X6W_REGB  // NERF_X6W_REGB (A/B builds): register-staged weight slabs
+  constexpr bool GLDS = true;
+#else
+  constexpr bool GLDS = false;
+#endif
   float4 ra[2][TM][KS][2];
-  uint4 rb[BCH];  // chunk c = tid + NT i: plane c / (BN CPR), row (c / CPR) % BN, chunk c % CPR
+  const uint32_t bofs = (uint32_t)(((tid / CPR) * ldb + 8 * (tid % CPR)) * (int)sizeof(nerf_bf16));  // bytes
+  uint4 rb[GLDS ? 1 : BCH];
+  // GLDS: the weight slab DMA'd straight into the LDS image (global_load_lds_dwordx4, no VGPRs): one wave-instruction
+  // fills 16 rows x 64 B of a piece image, lane l -> row l / 4, slot l % 4, so the swizzle goes on the source: lane l
+  // reads chunk (l % 4) ^ ((row >> 2) & 3) = (l & 3) ^ ((l >> 4) & 3) of its row.  Issued as inline asm after the touch
+  // of the slab's activation registers (hipcc neither counts these loads nor drains them at its own waits).  Against
+  // register staging (profiles/r04/x6_glds_ab.txt, C2 on MI355X): fwd 0.595 -> 0.572-0.583 ms, dgrad 0.614 ->
+  // 0.588-0.594 ms per fine launch, 218.5k -> 221k rays/s, the same loss bits; s_memtime stamps of the forward: slab
+  // 11.4k -> 9.6k cycles, its "weight store + barrier" tail 3.5k -> 1.9k
+  constexpr int GPP = BN * BK * 2 / 1024, GPW = 3 * GPP / NW;  // 1-KiB groups per piece image / per wave
+  static_assert(!GLDS || (BK == 32 && (3 * GPP) % NW == 0), "GLDS staging");
+  const int wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t gofs = (uint32_t)((((lane >> 2) * ldb) + 8 * ((lane & 3) ^ ((lane >> 4) & 3))) * 2);
+  const uint32_t smem_u32 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;  // chunk c = tid + NT i: plane c / (BN CPR), row (c / CPR) % BN, chunk c % CPR
 #define X6W_ALOAD(set_, k0_)                                                                              \
   _Pragma("unroll") for (int a = 0; a < TM; ++a)                                                         \
     _Pragma("unroll") for (int ks = 0; ks < KS; ++ks)                                                    \
@@ -376,22 +394,41 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   // (the touch below), so the compiler's counted waits on its own activation loads never wait on these as well.  At two
   // waves per SIMD the extra live registers spill (fwd 0.62 -> 0.65 ms): plain loads there.  32-row waves (TM = 1) have
   // the registers: a forward of that shape went 0.76 -> 0.655 ms with them, still behind 0.63 ms for 64-row waves.
-  constexpr bool ASMB = BIGSMALL || TM == 1;
+  constexpr bool ASMB = !GLDS && (BIGSMALL || TM == 1);
+  constexpr bool ASML = ASMB || GLDS;  // weight loads hipcc does not count
   // B fragments are read per pair of column blocks (2 x 3 fragments live).  Measured and not kept (round 4,
   // profiles/r04/x6_bfrag_ab.txt): one block at a time (fwd 0.603 -> 0.612 ms), with the next block read under the
-  // current block's MFMAs (0.613-0.619), and one block at a time with inline-asm weight loads (0.599-0.601)
+  // current block's MFMAs (0.613-0.619), and one block at a time with inline-asm weight loads (0.599-0.601).  Also not
+  // kept: the two 4-wave halves staggered by one barrier (ping-pong: one half's 24-MFMA cluster under the other's split
+  // and fragment reads, three DMA'd weight buffers, two barriers per cluster): fwd 0.58 -> 0.64, dgrad 0.59 -> 0.67 ms
+  // (profiles/r04/x6_pingpong_ab.txt)
   constexpr int BPG = 2;
-#define X6W_BLOAD(k0_)                                                                                    \
-  if constexpr (ASMB) {                                                                                   \
+#define X6W_BLOAD(k0_, dbuf_)                                                                             \
+  if constexpr (GLDS) {                                                                                   \
+    _Pragma("unroll") for (int a = 0; a < TM; ++a)                                                       \
+      _Pragma("unroll") for (int ks = 0; ks < KS; ++ks)                                                  \
+        asm volatile("" ::"v"(__builtin_bit_cast(x6_f32x4, ra[j][a][ks][0])),                            \
+                     "v"(__builtin_bit_cast(x6_f32x4, ra[j][a][ks][1])) : "memory");                     \
+    _Pragma("unroll") for (int i = 0; i < GPW; ++i) {                                                    \
+      const int g_ = wave_u + NW * i, p_ = g_ / GPP, rb_ = (g_ % GPP) * 16;                              \
+      const nerf_bf16* sb_ = Bb + p_ * bplane + (int64_t)rb_ * ldb + (k0_);                              \
+      const uint32_t dst_ = smem_u32 + (uint32_t)((((dbuf_) * 3 + p_) * PL + rb_ * LS) * 2);             \
+      unsigned keep_;                                                                                     \
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t" \
+                   "s_mov_b32 m0, %0" : "=&s"(keep_) : "v"(gofs), "s"(sb_), "s"(dst_) : "memory");       \
+    }                                                                                                     \
+  } else if constexpr (ASMB) {                                                                            \
     _Pragma("unroll") for (int a = 0; a < TM; ++a)                                                       \
       _Pragma("unroll") for (int ks = 0; ks < KS; ++ks)                                                  \
         asm volatile("" ::"v"(__builtin_bit_cast(x6_f32x4, ra[j][a][ks][0])),                            \
                      "v"(__builtin_bit_cast(x6_f32x4, ra[j][a][ks][1])) : "memory");                     \
     _Pragma("unroll") for (int i = 0; i < BCH; ++i) {                                                    \
-      const int c = tid + NT * i, p = c / (BN * CPR), r = (c / CPR) % BN, q = c % CPR;                   \
-      const nerf_bf16* src_ = Bb + p * bplane + (int64_t)r * ldb + (k0_) + 8 * q;                        \
+      /* NT divides BN CPR: chunk c's plane and the row base of its NT-chunk group are uniform, so the     \
+         address is a uniform SGPR base plus one 32-bit lane offset (bofs) instead of a VGPR pair a chunk */ \
+      const int pu = (NT * i) / (BN * CPR), ru = ((NT * i) % (BN * CPR)) / CPR;                          \
+      const nerf_bf16* sb_ = Bb + pu * bplane + (int64_t)ru * ldb + (k0_);                              \
       x6_f32x4 v_;                                                                                        \
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v_) : "v"(src_) : "memory");                 \
+      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(v_) : "v"(bofs), "s"(sb_) : "memory");       \
       rb[i] = __builtin_bit_cast(uint4, v_);                                                              \
     }                                                                                                     \
   } else {                                                                                                \
@@ -401,7 +438,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
     }                                                                                                     \
   }
 #define X6W_BWAIT()                                                                                       \
-  if constexpr (ASMB) {                                                                                   \
+  if constexpr (GLDS) {                                                                                   \
+    if constexpr (TM * KS * 2 == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                    \
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                                                \
+  } else if constexpr (ASMB) {                                                                            \
     static_assert(TM * KS * 2 == 8 || TM * KS * 2 == 4, "vmcnt: the activation loads after the weight loads"); \
     if constexpr (TM * KS * 2 == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                    \
     else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                                                \
@@ -412,7 +452,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
     }                                                                                                     \
   }
 #define X6W_BSTORE(buf_)                                                                                  \
-  _Pragma("unroll") for (int i = 0; i < BCH; ++i) {                                                      \
+  if constexpr (!GLDS) _Pragma("unroll") for (int i = 0; i < BCH; ++i) {                                 \
     const int c = tid + NT * i, p = c / (BN * CPR), r = (c / CPR) % BN, q = c % CPR;                     \
     *reinterpret_cast<uint4*>(smem + ((buf_) * 3 + p) * PL + r * LS + 8 * sw(r, q)) = rb[i];             \
   }
@@ -435,8 +475,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   X6W_ALOAD(1, (nk > 1 ? 1 : 0) * BK);
   {
     const int j = 0;
-    X6W_BLOAD(0);
-    if constexpr (ASMB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    X6W_BLOAD(0, 0);
+    if constexpr (ASML) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   X6W_BSTORE(0);
   __syncthreads();
@@ -451,8 +491,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
       const int kt = kt0 + j;
       // ASMB: nk is even (host: K % (2 BK) == 0), so no guard — every path into the loop header then has the same
       // loads in flight and the compiler's counted wait there stays vmcnt(8) instead of draining to vmcnt(0)
-      if (ASMB || kt < nk) {
-        X6W_BLOAD((kt + 1 < nk ? kt + 1 : kt) * BK);
+      if (ASML || kt < nk) {
+        X6W_BLOAD((kt + 1 < nk ? kt + 1 : kt) * BK, j ^ 1);
         const nerf_bf16* S = smem + j * 3 * PL;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {

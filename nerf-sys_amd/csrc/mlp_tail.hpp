@@ -18,15 +18,17 @@
 // writes them into its slab once.  Per row it reads C0 / CIN / O3 / O16[0] / d_rgb_sigma (~1 KB) and writes
 // one 128-B dO16 row; the unfused chain moved ~2.7 KB per row through six launches.
 //   dO3   = g.rgb * s(1-s)                   (3 columns; VALU)
-//   dWc1 += dO3^T C0, dbc1 += sum dO3        (3 x 128: VALU, thread = output column)
-//   dC0   = (dO3 Wc1[:3]) * (C0 > 0)         (VALU, the forward ReLU mask is C0 > 0)
-//   dWc0 += dC0^T CIN, dbc0 += sum dC0       (128 x 64: MFMA, wave w -> rows 32w.., both 32-col blocks)
-//   dgeo  = dC0 Wc0[:, :15]                  (MFMA, C^T form (lane = row); wave w -> row block w&1,
-//                                             contraction half w>>1, the halves summed through LDS)
-//   dO16  = [g.sigma * exp(clamp(sigma_raw)), dgeo, 0...]
+//   dWc1 += dO3^T C0, dbc1 += sum dO3        (3 x 128: VALU, thread = output column x row half, in the same pass
+//   dC0   = (dO3 Wc1[:3]) * (C0 > 0)          as dC0; the forward ReLU mask is C0 > 0)
+//   dWc0 += dC0^T CIN, dbc0 += sum dC0       (128 x 64: MFMA 32x32x2, wave w -> rows 32w.., both 32-col blocks)
+//   dgeo  = dC0 Wc0[:, :15]                  (MFMA 16x16x4, wave w -> rows 16w.., Wc0 in registers)
+//   dO16  = [g.sigma * exp(clamp(sigma_raw)), dgeo, 0...]   (stored from the dgeo accumulators)
+// Round 4: the dC0 pass was 4-way LDS bank-conflicted (row-per-lane-group mapping), the dWc0 k-steps 2-way, and dgeo
+// ran on 32x32x2 tiles with 17 of 32 columns unused plus an LDS sum of two contraction halves (5 barriers per tile,
+// now 3).
 namespace nerf_mlp {
 constexpr int CB_ROWS = 64;
-constexpr int CB_C0 = 132, CB_CIN = 68, CB_WT = 132, CB_GEO = 33;
+constexpr int CB_C0 = 132, CB_CIN = 68;
 
 // 4 consecutive activations as fp32 (fp32 or bf16 storage) and 4 fp32 values stored as T
 __device__ __forceinline__ float4 tail_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -51,18 +53,14 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
                                                         int64_t off_w1, int64_t off_b1, int64_t rps, int64_t M,
                                                         int64_t Mp, float* __restrict__ partial2, int64_t cslab,
                                                         int64_t p2base, int ldd) {
-  // dC0 overwrites C0 in place and the dgeo halves reuse the CIN tile (one extra barrier each): 70.6 KB of
-  // LDS, two workgroups per CU.  Workgroup 2s + h walks half h of split s; half 0 writes the colour sums into
-  // slab s, half 1 into row s of partial2 (cslab floats: packed offsets p2base .. total of one slab; p2base <=
-  // off_w0).  dO16 rows have pitch ldd: 32 (columns 16..31 written as zeros) or 16.
+  // dC0 overwrites C0 in place (each element by the thread that read it, so without a barrier between): 52 KB of LDS,
+  // two workgroups per CU, three barriers per tile.  Workgroup 2s + h walks half h of split s; half 0 writes the
+  // colour sums into slab s, half 1 into row s of partial2 (cslab floats: packed offsets p2base .. total of one slab;
+  // p2base <= off_w0).  dO16 rows have pitch ldd: 32 (columns 16..31 written as zeros) or 16.
   __shared__ __attribute__((aligned(16))) float s_c0[CB_ROWS * CB_C0];
   float* const s_dc0 = s_c0;
   __shared__ __attribute__((aligned(16))) float s_cin[CB_ROWS * CB_CIN];
-  __shared__ __attribute__((aligned(16))) float s_wt[32 * CB_WT];  // Wc0^T rows c < 32: [c][j]
-  __shared__ __attribute__((aligned(16))) float s_w1[3 * 128];
-  __shared__ float s_do3[CB_ROWS * 4];
-  float* const s_geo = s_cin;
-  static_assert(2 * CB_ROWS * CB_GEO <= CB_ROWS * CB_CIN, "dgeo halves fit the CIN tile");
+  __shared__ __attribute__((aligned(16))) float s_do3[CB_ROWS * 4];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 31, lh = lane >> 5;
   const int64_t sp = blockIdx.x >> 1, half = blockIdx.x & 1;
@@ -70,12 +68,6 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
   const int64_t r0 = sp * rps + half * rph;
   int64_t r1 = half ? sp * rps + rps : r0 + rph;
   if (r1 > Mp) r1 = Mp;
-
-  for (int i = tid; i < 32 * 128; i += 256) {
-    const int c = i >> 7, j = i & 127;
-    s_wt[c * CB_WT + j] = Wc0[j * 64 + c];
-  }
-  for (int i = tid; i < 3 * 128; i += 256) s_w1[i] = Wc1[i];
 
   // register prefetch of one tile: C0 = 2048 float4 (8 / thread), CIN = 1024 float4 (4 / thread); wave 0 also
   // prefetches the tile's head outputs: d_rgb_sigma (M rows: the row index is clamped, the value zeroed below for
@@ -98,10 +90,17 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
     }
   };
 
-  // VALU accumulators: thread t -> dWc1 column j = t & 127, rows n = 0,1 (t < 128) or 2 (t >= 128)
-  const int jw = tid & 127, nw = tid < 128 ? 0 : 2;
-  float w1a = 0.f, w1b = 0.f, b1 = 0.f, b1b = 0.f;  // b1 / b1b: dbc1 sums kept by threads 0 and 128
-  nerf_f32x16 acc0[2], accg;
+  // colour_out / dC0 phase: thread (column jw, row half rh); its colour_out weight column lives in registers
+  const int jw = tid & 127, rh = tid >> 7;
+  const float w10 = Wc1[jw], w11 = Wc1[128 + jw], w12 = Wc1[256 + jw];
+  float w1a = 0.f, w1b = 0.f, w1c = 0.f, b1a = 0.f, b1b = 0.f, b1c = 0.f;  // b1*: kept by jw == 0
+  // dgeo phase (16x16x4 MFMA, wave w -> rows 16w..16w+15, all 128 contraction columns): lane group kg = lane >> 4
+  // owns contraction columns 32 kg + kk; its B operand Wc0[32 kg + kk][c = lane & 15] lives in registers
+  const int gc = lane & 15, kg = lane >> 4;
+  float wg[32];
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk) wg[kk] = Wc0[(32 * kg + kk) * 64 + gc];
+  nerf_f32x16 acc0[2];
   for (int r = 0; r < 16; ++r) { acc0[0][r] = 0.f; acc0[1][r] = 0.f; }
   float bsum0 = 0.f;
 
@@ -128,98 +127,64 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
         c = pg.z * (s2 * (1.0f - s2));
         ds = pg.w * expf(fminf(fmaxf(po.w, -EXP_MAX), EXP_MAX));
       }
-      s_do3[tid * 4 + 0] = a;
-      s_do3[tid * 4 + 1] = b;
-      s_do3[tid * 4 + 2] = c;
-      s_do3[tid * 4 + 3] = ds;
+      *reinterpret_cast<float4*>(s_do3 + tid * 4) = make_float4(a, b, c, ds);
     }
     __syncthreads();
     if (t0 + CB_ROWS < r1) fetch(t0 + CB_ROWS);  // in flight during this tile's compute
-    // ---- VALU: dWc1 / dbc1 columns, then dC0 (row r = tid / 4, 32 columns)
-#pragma unroll 16
-    for (int r = 0; r < CB_ROWS; ++r) {
-      const float c0 = s_c0[r * CB_C0 + jw];
-      const float d0 = s_do3[r * 4 + nw];
-      w1a += d0 * c0;
-      if (nw == 0) {
-        const float d1 = s_do3[r * 4 + 1];
-        w1b += d1 * c0;
-        if (jw == 0) b1b += d1;
-      }
-      if (jw == 0) b1 += d0;
-    }
-    __syncthreads();  // every row of C0 read by the dWc1 sums before dC0 overwrites it
-    {
-      const int r = tid >> 2, jb = (tid & 3) * 32;
-      const float d0 = s_do3[r * 4 + 0], d1 = s_do3[r * 4 + 1], d2 = s_do3[r * 4 + 2];
-      const float* crow = s_c0 + r * CB_C0 + jb;
-      float* drow = s_dc0 + r * CB_C0 + jb;
+    // ---- VALU: dWc1 / dbc1 sums over the thread's 32 rows, then its dC0 element written over the C0 element it read
 #pragma unroll 8
-      for (int j = 0; j < 32; ++j) {
-        const float v = d0 * s_w1[jb + j] + d1 * s_w1[128 + jb + j] + d2 * s_w1[256 + jb + j];
-        drow[j] = crow[j] > 0.f ? v : 0.f;
-      }
+    for (int rr = 0; rr < CB_ROWS / 2; ++rr) {
+      const int r = 32 * rh + rr;
+      const float c0 = s_c0[r * CB_C0 + jw];
+      const float4 d = *reinterpret_cast<const float4*>(s_do3 + r * 4);
+      w1a += d.x * c0;
+      w1b += d.y * c0;
+      w1c += d.z * c0;
+      if (jw == 0) { b1a += d.x; b1b += d.y; b1c += d.z; }
+      const float v = d.x * w10 + d.y * w11 + d.z * w12;
+      s_dc0[r * CB_C0 + jw] = c0 > 0.f ? v : 0.f;
     }
     __syncthreads();
-    // ---- MFMA: dWc0 (wave w -> rows 32w..), bias sums; dgeo partial over contraction half w >> 1
+    // ---- MFMA: dWc0 (wave w -> rows 32w..), bias sums.  k-step st pairs rows r and r + 8 (lane halves): 8 rows apart
+    // the two halves' LDS reads sit 32 banks apart (pitches 132 / 68), conflict-free
 #pragma unroll 16
     for (int st = 0; st < CB_ROWS / 2; ++st) {
-      const int row = 2 * st + lh;
+      const int row = (st & 7) + 16 * (st >> 3) + 8 * lh;
       const float av = s_dc0[row * CB_C0 + 32 * wave + li];
       bsum0 += av;
       acc0[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, s_cin[row * CB_CIN + li], acc0[0], 0, 0, 0);
       acc0[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, s_cin[row * CB_CIN + 32 + li], acc0[1], 0, 0, 0);
     }
+    // ---- dgeo = dC0 Wc0[:, :15] (16x16x4: A lane (row gc, k 32 kg + kk), B lane (k, column gc)), then the dO16 rows
+    //      [ds, dgeo, 0...] straight from the accumulator (lane (kg, gc) holds rows 4 kg + v, column gc)
     {
-      const int rb = wave & 1, kh = wave >> 1;
-      for (int r = 0; r < 16; ++r) accg[r] = 0.f;
-      const float* arow = s_dc0 + (rb * 32 + li) * CB_C0 + 64 * kh;
-      const float* brow = s_wt + li * CB_WT + 64 * kh;
+      nerf_f32x4 accg = {0.f, 0.f, 0.f, 0.f};
+      const float* arow = s_dc0 + (16 * wave + gc) * CB_C0 + 32 * kg;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {  // 16 k per slab: lane half lh owns k = 16q + 8lh + t
-        const float4 a0 = *reinterpret_cast<const float4*>(arow + 16 * q + 8 * lh);
-        const float4 a1 = *reinterpret_cast<const float4*>(arow + 16 * q + 8 * lh + 4);
-        const float4 b0 = *reinterpret_cast<const float4*>(brow + 16 * q + 8 * lh);
-        const float4 bb = *reinterpret_cast<const float4*>(brow + 16 * q + 8 * lh + 4);
-        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.x, a0.x, accg, 0, 0, 0);
-        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.y, a0.y, accg, 0, 0, 0);
-        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.z, a0.z, accg, 0, 0, 0);
-        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.w, a0.w, accg, 0, 0, 0);
-        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.x, a1.x, accg, 0, 0, 0);
-        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.y, a1.y, accg, 0, 0, 0);
-        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.z, a1.z, accg, 0, 0, 0);
-        accg = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.w, a1.w, accg, 0, 0, 0);
+      for (int k4 = 0; k4 < 8; ++k4) {
+        const float4 a4 = *reinterpret_cast<const float4*>(arow + 4 * k4);
+        accg = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, wg[4 * k4 + 0], accg, 0, 0, 0);
+        accg = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, wg[4 * k4 + 1], accg, 0, 0, 0);
+        accg = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, wg[4 * k4 + 2], accg, 0, 0, 0);
+        accg = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, wg[4 * k4 + 3], accg, 0, 0, 0);
       }
-      __syncthreads();  // all waves done reading CIN (dWc0) before the dgeo halves overwrite it
-      // lane li holds row rb*32 + li; register 4q + e holds column 8q + 4lh + e
-      float* grow = s_geo + (kh * CB_ROWS + rb * 32 + li) * CB_GEO;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int c = 8 * q + 4 * lh + e;
-          if (c < 15) grow[c] = accg[4 * q + e];
-        }
-    }
-    __syncthreads();
-    // ---- dO16 rows: [ds, dgeo (sum of the two halves), 0 x 16]
-    const int nc4 = ldd / 4;
-    for (int f = tid; f < CB_ROWS * nc4; f += 256) {
-      const int r = f / nc4, c4 = f - r * nc4;
-      const int64_t m = t0 + r;
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (c4 < 4) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int c = 4 * c4 + e;  // dO16 column
-          if (c == 0) v[e] = s_do3[r * 4 + 3];
-          else if (c <= 15) v[e] = s_geo[r * CB_GEO + c - 1] + s_geo[(CB_ROWS + r) * CB_GEO + c - 1];
-        }
+      for (int v = 0; v < 4; ++v) {
+        const int r = 16 * wave + 4 * kg + v;
+        TD* drow = dO16 + (t0 + r) * ldd;
+        if (gc < 15) drow[gc + 1] = (TD)accg[v];
+        else drow[0] = (TD)s_do3[r * 4 + 3];
+        if (ldd == 32) drow[16 + gc] = (TD)0.f;
       }
-      tail_st4(dO16 + m * ldd + 4 * c4, make_float4(v[0], v[1], v[2], v[3]));
     }
   }
-  // ---- this split's slab: weight sums, bias sums (lane halves combined)
+  // ---- this split's slab: weight sums, bias sums (lane halves combined); the dWc1 row halves combined through LDS
+  __syncthreads();
+  if (rh == 1) {
+    s_c0[jw * 4 + 0] = w1a; s_c0[jw * 4 + 1] = w1b; s_c0[jw * 4 + 2] = w1c;
+    if (jw == 0) { s_c0[512] = b1a; s_c0[513] = b1b; s_c0[514] = b1c; }
+  }
+  __syncthreads();
   float* P = half ? partial2 + sp * cslab - p2base : partial + sp * slab;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -234,14 +199,17 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
     const int n = i >> 7;
     if (n >= 3) P[off_w1 + i] = 0.f;
   }
-  P[off_w1 + (int64_t)nw * 128 + jw] = w1a;
-  if (nw == 0) P[off_w1 + 128 + jw] = w1b;
-  if (tid >= 3 && tid < 32) P[off_b1 + tid] = 0.f;
-  if (tid == 0) {
-    P[off_b1 + 0] = b1;
-    P[off_b1 + 1] = b1b;
+  if (rh == 0) {
+    P[off_w1 + jw] = w1a + s_c0[jw * 4 + 0];
+    P[off_w1 + 128 + jw] = w1b + s_c0[jw * 4 + 1];
+    P[off_w1 + 256 + jw] = w1c + s_c0[jw * 4 + 2];
+    if (jw == 0) {
+      P[off_b1 + 0] = b1a + s_c0[512];
+      P[off_b1 + 1] = b1b + s_c0[513];
+      P[off_b1 + 2] = b1c + s_c0[514];
+    }
   }
-  if (tid == 128) P[off_b1 + 2] = b1;
+  if (tid >= 3 && tid < 32) P[off_b1 + tid] = 0.f;
 }
 // ------------------------------------------------------------------ fused head backward (fp32 path)
 // dZ7 = (dO16 Wh) * [Y7 > 0] and the head sums dWh += dO16^T Y7, dbh += colsum(dO16) in ONE pass over Y7: the one

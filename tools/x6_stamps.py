@@ -31,14 +31,18 @@ def main():
                    torch.nn.functional.normalize(torch.randn(M, 3, generator=g), dim=-1)], -1).to(dev)
     gup = (torch.randn(M, 4, generator=g) * 1e-3).to(dev)
     ws = K.mlp_workspace(M, True, dev)
-    for _ in range(3):
+    buf = (ctypes.c_ulonglong * (2 * 8 * 128))()
+    L = lib()
+    L.nerf_debug_x6_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    for _ in range(2):
         K.mlp_fwd(w, x, ws, True)
         K.mlp_bwd(w, M, gup, ws)
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * (2 * 8 * 128))()
-    L = lib()
-    L.nerf_debug_x6_stamps.argtypes = [ctypes.c_void_p]
-    rc = L.nerf_debug_x6_stamps(ctypes.addressof(buf))
+    assert L.nerf_debug_x6_stamps(None, 1) == 0  # clear: only the last forward / backward below leave stamps
+    K.mlp_fwd(w, x, ws, True)
+    K.mlp_bwd(w, M, gup, ws)
+    torch.cuda.synchronize()
+    rc = L.nerf_debug_x6_stamps(ctypes.addressof(buf), 0)
     assert rc == 0, rc
     names = ["split ks0", "mfma ks0", "split ks1", "mfma ks1", "A issue+B wait", "B store+barrier"]
     out = {}
@@ -46,8 +50,9 @@ def main():
         waves = []
         for wv in range(8):
             st = [buf[(kind * 8 + wv) * 128 + i] for i in range(128)]
-            n = next((i for i, v in enumerate(st) if v == 0), 128)
-            waves.append(st[:n])
+            # the last launch of each kind (trunk.7 forward, trunk.1 input gradient) has K = 256: 8 slabs, 1 + 8 x 6
+            # stamps + the epilogue's; entries past them are stale from the K = 320 trunk.4 launch
+            waves.append(st[:2 + 8 * 6])
         # layout: s0 = loop start; per slab 6 stamps (V0 M0 V1 M1 W T), then the epilogue end
         per_wave = []
         for st in waves:
