@@ -319,7 +319,8 @@ __device__ unsigned long long nerf_x6_stamps[2][8][128];
 // workgroup per CU): C2 step 204.0k -> 207.5-209.0k rays/s over BK = 16, NW = 4 (fwd / dgrad 0.65 -> 0.63 ms).
 // TM = 1 (32-row waves; the BIGSMALL input gradients, whose 256 accumulator registers per 64-row wave allowed only one
 // wave per SIMD): 256 x 128 tiles at two waves per SIMD.
-template <int EPI, int BK = 32, int NW = 8, bool BIGSMALL = false, int TM = 2, int MINW = (BIGSMALL ? 1 : 8 / NW)>
+template <int EPI, int BK = 32, int NW = 8, bool BIGSMALL = false, int TM = 2, int MINW = (BIGSMALL ? 1 : 8 / NW),
+          int NKC = 0>
 __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float* __restrict__ A, int lda,
                                                                      const nerf_bf16* __restrict__ Bp, int ldb,
                                                                      int64_t bplane, const float* __restrict__ bias,
@@ -368,7 +369,12 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
 #else
   constexpr bool GLDS = false;
 #endif
-  float4 ra[2][TM][KS][2];
+  // NKC > 0 (K = NKC BK at compile time, TM = 1): three activation register sets, the slab loop fully unrolled — slab
+  // kt + 2's loads are issued at the start of slab kt, after its weight DMA, so the end-of-slab weight wait leaves them
+  // in flight (two slabs of latency instead of one)
+  constexpr bool A3 = NKC > 0;
+  static_assert(!A3 || TM == 1, "three activation sets: 32-row waves");
+  float4 ra[A3 ? 3 : 2][TM][KS][2];
   const uint32_t bofs = (uint32_t)(((tid / CPR) * ldb + 8 * (tid % CPR)) * (int)sizeof(nerf_bf16));  // bytes
   uint4 rb[GLDS ? 1 : BCH];
   // GLDS: the weight slab DMA'd straight into the LDS image (global_load_lds_dwordx4, no VGPRs): one wave-instruction
@@ -470,7 +476,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
         if constexpr (BIGSMALL) accs[a][b][r] = 0.f;
       }
 
-  const int nk = K / BK;
+  const int nk = A3 ? NKC : K / BK;
   X6W_ALOAD(0, 0);
   X6W_ALOAD(1, (nk > 1 ? 1 : 0) * BK);
   {
@@ -484,24 +490,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   const bool stamp_on = blockIdx.x == 777 && (BIGSMALL || EPI == EPI_BIAS_RELU);
   int si_ = 0;
 #endif
-  X6W_STAMP();
-  for (int kt0 = 0; kt0 < nk; kt0 += 2) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {  // slab kt = kt0 + j: LDS buffer j, activation register set j
-      const int kt = kt0 + j;
-      // ASMB: nk is even (host: K % (2 BK) == 0), so no guard — every path into the loop header then has the same
-      // loads in flight and the compiler's counted wait there stays vmcnt(8) instead of draining to vmcnt(0)
-      if (ASML || kt < nk) {
-        X6W_BLOAD((kt + 1 < nk ? kt + 1 : kt) * BK, j ^ 1);
-        const nerf_bf16* S = smem + j * 3 * PL;
+  // one slab's k-steps on activation register set rj and weight buffer S
+  auto slab_mfma = [&](const float4 (&rj)[TM][KS][2], const nerf_bf16* S) __attribute__((always_inline)) {
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           nerf_bf16x8 af[TM][3];
 #pragma unroll
           for (int a = 0; a < TM; ++a) {
             uint2 h0, m0_, l0, h1, m1, l1;
-            x6_split4(ra[j][a][ks][0], h0, m0_, l0);
-            x6_split4(ra[j][a][ks][1], h1, m1, l1);
+            x6_split4(rj[a][ks][0], h0, m0_, l0);
+            x6_split4(rj[a][ks][1], h1, m1, l1);
             af[a][0] = __builtin_bit_cast(nerf_bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
             af[a][1] = __builtin_bit_cast(nerf_bf16x8, make_uint4(m0_.x, m0_.y, m1.x, m1.y));
             af[a][2] = __builtin_bit_cast(nerf_bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
@@ -537,6 +535,38 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
           }
           X6W_STAMP();
         }
+  };
+  X6W_STAMP();
+  if constexpr (A3) {
+#pragma unroll
+    for (int kt = 0; kt < NKC; ++kt) {
+      const int j = kt % 3;
+      X6W_BLOAD((kt + 1 < NKC ? kt + 1 : kt) * BK, (kt + 1) & 1);
+      // set (kt + 2) % 3 was consumed by slab kt - 1; the last two slabs load nothing (a dead load would be deleted by the
+      // compiler and leave the counted weight wait short), so their weight wait drains the queue
+      if (kt + 2 < NKC) X6W_ALOAD((kt + 2) % 3, (kt + 2) * BK);
+      asm volatile("" ::: "memory");  // pinned here: hipcc otherwise sinks the loads to the end of the slab
+      slab_mfma(ra[j], smem + (kt & 1) * 3 * PL);
+      if (kt + 2 < NKC) {
+        X6W_BWAIT();
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      X6W_STAMP();
+      __syncthreads();
+      X6W_STAMP();
+    }
+  } else
+  for (int kt0 = 0; kt0 < nk; kt0 += 2) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // slab kt = kt0 + j: LDS buffer j, activation register set j
+      const int kt = kt0 + j;
+      // ASMB: nk is even (host: K % (2 BK) == 0), so no guard — every path into the loop header then has the same
+      // loads in flight and the compiler's counted wait there stays vmcnt(8) instead of draining to vmcnt(0)
+      if (ASML || kt < nk) {
+        X6W_BLOAD((kt + 1 < nk ? kt + 1 : kt) * BK, j ^ 1);
+        const nerf_bf16* S = smem + j * 3 * PL;
+        slab_mfma(ra[j], S);
         X6W_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);  // set j consumed: slab kt + 2 streams into it
         X6W_BWAIT();
         X6W_STAMP();

@@ -96,46 +96,35 @@ inline int ld_of(const WS& w, int i) { return (i == 3) ? 320 : 256; }
 
 // ------------------------------------------------------------------ elementwise kernels
 
-// xyz positional encoding of x_d[:, :3] into X3E cols 256..319 (pad col 319 = 0; rows >= M zero).  Thread = sample
-// row for the 30 sincos; the 64 values go through a wave-private LDS tile [64 rows][pitch 65] and leave as whole
-// 256-B row segments (16 lanes per row, one float4 each) instead of 16 row-strided float4 stores per thread
-// (rocprof: 79 us per fine launch before).  Block = 256 rows (Mp is a multiple of 256).
-__global__ __launch_bounds__(256) void pe_xyz_kernel(const float* __restrict__ xd, int64_t M, int64_t Mp,
-                                                     float* __restrict__ X3E) {
-  constexpr int PP = 65;
-  __shared__ float s_v[256 * PP];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t b0 = (int64_t)blockIdx.x * 256;
-  const int64_t m = b0 + tid;
-  float* sv = s_v + tid * PP;
-  if (m < M) {
-    const float x[3] = {xd[m * 6], xd[m * 6 + 1], xd[m * 6 + 2]};
+// xyz positional encoding of x_d[:, :3] into X3E cols 256..319 (pad col 319 = 0; rows >= M zero).
+// One thread per sample row: the 64 encoded values leave as 16 float4 stores (256 contiguous bytes).
+__global__ void pe_xyz_kernel(const float* __restrict__ xd, int64_t M, int64_t Mp, float* __restrict__ X3E) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= Mp) return;
+  float4* q4 = reinterpret_cast<float4*>(X3E + m * 320 + 256);
+  if (m >= M) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      sv[k] = x[k];
-      float band = 1.0f;
+    for (int c = 0; c < 16; ++c) q4[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  float v[64];
+  const float x[3] = {xd[m * 6], xd[m * 6 + 1], xd[m * 6 + 2]};
 #pragma unroll
-      for (int l = 0; l < 10; ++l) {
-        float sn, cs;
-        sincosf(x[k] * band, &sn, &cs);
-        sv[3 + k * 20 + l] = cs;
-        sv[3 + k * 20 + 10 + l] = sn;
-        band *= 2.0f;
-      }
+  for (int k = 0; k < 3; ++k) {
+    v[k] = x[k];
+    float band = 1.0f;
+#pragma unroll
+    for (int l = 0; l < 10; ++l) {
+      float s, c;
+      sincosf(x[k] * band, &s, &c);
+      v[3 + k * 20 + l] = c;
+      v[3 + k * 20 + 10 + l] = s;
+      band *= 2.0f;
     }
-    sv[63] = 0.f;
-  } else {
+  }
+  v[63] = 0.f;
 #pragma unroll
-    for (int c = 0; c < 64; ++c) sv[c] = 0.f;
-  }
-  __syncthreads();
-  const float* tw = s_v + wave * 64 * PP;
-#pragma unroll 4
-  for (int it = 0; it < 16; ++it) {
-    const int r = 4 * it + (lane >> 4), c4 = lane & 15;
-    const float* q = tw + r * PP + 4 * c4;
-    *reinterpret_cast<float4*>(X3E + (b0 + wave * 64 + r) * 320 + 256 + 4 * c4) = make_float4(q[0], q[1], q[2], q[3]);
-  }
+  for (int c = 0; c < 16; ++c) q4[c] = make_float4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
 }
 
 // batched transpose: dst_i[c][r] = src_i[r][c] for r < rows_i, c < cols_i  (src pitch lds_i)
@@ -264,6 +253,15 @@ int nt_x6(const float* A, int lda, const nerf_bf16* Bp, int ldb, int64_t bplane,
 #define NERF_X6_DG_NW 8
 #endif
     constexpr int DGM = 32 * NERF_X6_DG_NW;
+#ifndef NERF_X6W_NOA3  // three activation register sets, K = 256 unrolled (NERF_X6W_NOA3: the two-set loop, A/B builds)
+    // (profiles/r04/x6_a3_ab.txt: 0.597 -> 0.584 ms per fine launch, C2 +0.5 %, bitwise the same)
+    if (M % DGM == 0 && K == 256) {
+      gemm_nt_x6w_kernel<EPI, 32, NERF_X6_DG_NW, true, 1, 8 / NERF_X6_DG_NW, 8><<<(unsigned)((M / DGM) * ntn),
+                                                                                64 * NERF_X6_DG_NW, 0, st>>>(
+          A, lda, Bp, ldb, bplane, bias, C, ldc, mbits, N / 32, mbits_out, K, ntn);
+      return NERF_OK;
+    }
+#endif
     if (M % DGM == 0 && K % 64 == 0) {  // gemm_nt_x6w walks the slabs in pairs
       gemm_nt_x6w_kernel<EPI, 32, NERF_X6_DG_NW, true, 1, 8 / NERF_X6_DG_NW><<<(unsigned)((M / DGM) * ntn),
                                                                              64 * NERF_X6_DG_NW, 0, st>>>(
@@ -352,7 +350,7 @@ extern "C" int nerf_mlp_fwd_ex(const float* w, const float* x_d, int64_t M, floa
   const int64_t Mp = W.Mp;
   auto Wt = [&](int t) { return w + L.off[t]; };
 
-  pe_xyz_kernel<<<(unsigned)(Mp / 256), 256, 0, st>>>(x_d, M, Mp, W.X3E);
+  pe_xyz_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(x_d, M, Mp, W.X3E);
   if (!native) {  // this call's weights as bf16 piece planes
     X6Jobs jobs{};
     for (int i = 0; i < 8; ++i)
