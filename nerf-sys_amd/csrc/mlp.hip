@@ -302,6 +302,8 @@ int wgrad_x6(const float* G, int ldg, const float* X, int ldx, int tensor_w, con
 #endif
   };
   auto t64 = [&](const float* Xk, float* Pk, float* Pbk) {
+    // (a one-workgroup-per-split form reading G and X once, as gemm_wgrad_x6w, measured 185 -> 191 us per launch:
+    // profiles/r04/x6_narrow_wgrad_ab.txt)
     gemm_wgrad_x6_kernel<128, 64, 4><<<2 * w.S, 256, 0, st>>>(G, ldg, Xk, ldx, Pk, ldp, Pbk, slab, w.rps, w.Mp, 1, 2);
   };
   if (K == 64) {

@@ -13,7 +13,7 @@ path = sys.argv[1]
 steps = float(sys.argv[2]) if len(sys.argv) > 2 else 13
 OURS = ("gemm_", "reduce_splits", "composite", "sample_pdf", "stratified", "build_xd", "pe_xyz", "build_cin",
         "head_out", "geo_bwd", "transpose", "adam", "sqnorm", "rays_gen", "pick_pixels", "head_", "fused",
-        "bwd_layer", "bwd_tail", "reduce_fused", "pe_prefill", "frag_pack", "color_bwd")
+        "bwd_layer", "bwd_tail", "reduce_fused", "pe_prefill", "frag_pack", "color_bwd", "fwd_tail", "x6_planes")
 rows = list(csv.DictReader(open(path)))
 tot = 0.0
 out = []
