@@ -95,11 +95,6 @@ __global__ __launch_bounds__(256, 2) void fwd_tail_kernel(FwdTailArgs A) {
       ah = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.z, yf[hh].z, ah, 0, 0, 0);
       ah = __builtin_amdgcn_mfma_f32_16x16x4f32(wf.w, yf[hh].w, ah, 0, 0, 0);
     }
-#ifdef NERF_FT_EARLY_Y
-    // the trunk.7 fragments are consumed: the next tile's rows load under this tile's colour layers (A/B builds)
-    if (t + (int)gridDim.x < A.ntiles) load_y(t + gridDim.x);
-    asm volatile("" ::: "memory");  // keep the loads here (hipcc sinks plain loads toward their use)
-#endif
     float o16[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) o16[r] = ah[r] + sB[4 * g + r];
@@ -170,9 +165,9 @@ __global__ __launch_bounds__(256, 2) void fwd_tail_kernel(FwdTailArgs A) {
                            fmaxf(ac[cb][3] + b[3], 0.f));
       if (TRAIN) *reinterpret_cast<float4*>(A.C0 + m * 128 + 16 * cb + 4 * g) = c0[cb];
     }
-#ifndef NERF_FT_EARLY_Y
-    if (t + (int)gridDim.x < A.ntiles) load_y(t + gridDim.x);  // the next tile's trunk.7 rows, under colour out
-#endif
+    // the next tile's trunk.7 rows, under colour out (issued right after the head MFMAs instead, pinned there: 214 -> 218
+    // us per launch, round 4 — not kept)
+    if (t + (int)gridDim.x < A.ntiles) load_y(t + gridDim.x);
     // ---- colour out: O3 = C0 Wc1^T + b (16 columns, 3 real), K = 128: C0 block cb is k chunk cb
     nerf_f32x4 ao = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
