@@ -58,7 +58,7 @@ def _worker(rank, world, port, q):
     allreduce_flat(buf, world)
     seeds = [shard_seed(s, rank, world) for s in range(5)]
     if rank == 0:
-        q.put((buf, seeds))
+        q.put((buf.numpy(), seeds))  # numpy: pickled by value (a tensor's shared-memory handle dies with the worker)
     else:
         q.put((None, seeds))
     dist.barrier()
@@ -77,7 +77,7 @@ def test_two_rank_allreduce_equals_full_batch():
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    dp = next(b for b, _ in res if b is not None)
+    dp = torch.from_numpy(next(b for b, _ in res if b is not None))
     seeds = [s for _, s in res]
     assert not set(seeds[0]) & set(seeds[1])  # disjoint per-rank ray streams
     from nerf_amd.dp import inv_count
@@ -100,7 +100,7 @@ def _flat_adam_worker(rank, world, port, q):
         for i, p in enumerate(ps):
             p.grad.copy_(torch.full_like(p, float(rank + 1) * (i + 1)))
     opt.allreduce_grads()
-    q.put((rank, [p.grad.clone() for p in ps]))
+    q.put((rank, [p.grad.clone().numpy() for p in ps]))
     dist.destroy_process_group()
 
 
@@ -117,7 +117,7 @@ def test_flat_adam_data_parallel_mean_gloo():
     for p in procs:
         p.join(timeout=60)
     for r in range(world):
-        g0, g1 = out[r]
+        g0, g1 = (torch.from_numpy(a) for a in out[r])
         assert torch.allclose(g0, torch.full((5, 3), 1.5)) and torch.allclose(g1, torch.full((7,), 3.0))
 
 
@@ -144,7 +144,7 @@ def _bucket_worker(rank, world, port, q):
                 tables[t].grad.fill_(float(10 * (t + 1) * (rank + 1)))
                 tables[t]._nerf_grad_ready(tables[t])
         opt.allreduce_grads()
-        q.put((rank, step, [p.grad.clone() for p in ps]))
+        q.put((rank, step, [p.grad.clone().numpy() for p in ps]))
     dist.destroy_process_group()
 
 
@@ -162,7 +162,7 @@ def test_flat_adam_buckets_data_dependent_firing_gloo():
     got = {}
     for _ in range(world * 3):
         r, step, g = q.get(timeout=120)
-        got[(r, step)] = g
+        got[(r, step)] = [torch.from_numpy(a) for a in g]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
