@@ -491,7 +491,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   int si_ = 0;
 #endif
   // one slab's k-steps on activation register set rj and weight buffer S
-  auto slab_mfma = [&](const float4 (&rj)[TM][KS][2], const nerf_bf16* S) __attribute__((always_inline)) {
+  auto slab_mfma = [&](const float4 (&rj)[TM][KS][2], const nerf_bf16* S, auto&& after_split) __attribute__((always_inline)) {
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           nerf_bf16x8 af[TM][3];
@@ -504,6 +504,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
             af[a][1] = __builtin_bit_cast(nerf_bf16x8, make_uint4(m0_.x, m0_.y, m1.x, m1.y));
             af[a][2] = __builtin_bit_cast(nerf_bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
           }
+          if (ks == KS - 1) after_split();  // the slab's activation registers are all split
           X6W_STAMP();
 #pragma unroll
           for (int bp = 0; bp < TN / BPG; ++bp) {  // groups of BPG column blocks: BPG x 3 B fragments live
@@ -546,7 +547,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
       // compiler and leave the counted weight wait short), so their weight wait drains the queue
       if (kt + 2 < NKC) X6W_ALOAD((kt + 2) % 3, (kt + 2) * BK);
       asm volatile("" ::: "memory");  // pinned here: hipcc otherwise sinks the loads to the end of the slab
-      slab_mfma(ra[j], smem + (kt & 1) * 3 * PL);
+      slab_mfma(ra[j], smem + (kt & 1) * 3 * PL, [] {});
       if (kt + 2 < NKC) {
         X6W_BWAIT();
       } else {
@@ -566,8 +567,17 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
       if (ASML || kt < nk) {
         X6W_BLOAD((kt + 1 < nk ? kt + 1 : kt) * BK, j ^ 1);
         const nerf_bf16* S = smem + j * 3 * PL;
-        slab_mfma(ra[j], S);
+#ifndef NERF_X6W_LATE_A  // set j's next loads issued right after its last split, pinned before the last k-step's MFMAs
+        // (profiles/r04/x6_early_a_ab.txt: fwd 0.582 -> 0.578 ms, C2 +0.5 %; with register-staged weights the same move
+        // was slower, x6_early_ab.txt).  NERF_X6W_LATE_A (A/B builds): after the slab's MFMAs
+        slab_mfma(ra[j], S, [&] {
+          X6W_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);
+          asm volatile("" ::: "memory");
+        });
+#else
+        slab_mfma(ra[j], S, [] {});
         X6W_ALOAD(j, (kt + 2 < nk ? kt + 2 : nk - 1) * BK);  // set j consumed: slab kt + 2 streams into it
+#endif
         X6W_BWAIT();
         X6W_STAMP();
         X6W_BSTORE(j ^ 1);
