@@ -23,6 +23,7 @@ for P in fp32 bf16; do
   python3 tools/step_timeline.py $O/prof_$P/run_kernel_trace.csv > $O/step_${P}.txt 2>&1 || true
   echo "prof $P: $(tail -1 $O/prof_$P.log | cut -c1-200)"
 done
+[ -n "$STOP_AFTER_PROF" ] && exit 0
 PMC_OUT=$O/pmc_fp32 PMC_BENCH_ARGS="--no-dropin --no-other-precision --no-native-ref" bash tools/pmc_traffic.sh > $O/pmc_fp32.txt 2>&1 || { tail -20 $O/pmc_fp32.txt; exit 1; }
 PMC_OUT=$O/pmc_bf16 PMC_PRECISION=bf16fused PMC_BENCH_ARGS="--precision bf16 --no-dropin --no-other-precision" bash tools/pmc_traffic.sh > $O/pmc_bf16.txt 2>&1 || { tail -20 $O/pmc_bf16.txt; exit 1; }
 PMC_OUT=$O/pmc_mfma PMC_BENCH_ARGS="--no-other-precision --no-native-ref" bash tools/pmc_mfma_bench.sh > $O/pmc_mfma.txt 2>&1 || { tail -20 $O/pmc_mfma.txt; exit 1; }
