@@ -31,6 +31,12 @@ Prints ONE JSON line on rank 0 (contract in the task statement), with
   llff          — BASELINE configs[3] (C4): the Fern-style 1008x756 NDC scene, same fp32 engine, --llff-steps steps.
   sweep         — BASELINE configs[4] (C5): 8 seeded scenes x --sweep-steps bf16 4096-ray steps, rank r training
                   scenes r, r+N, ...; aggregate rays/s vs the bf16 MFMA roofline and mean held-out PSNR.
+  ngp           — (N = 1) the reference's production expert (MetaNGP, 16 x 2^20 hash grid, 96 stratified samples) train
+                  step: rays/s, per-kernel times, the table scatter against the float-atomic request rate, CPU oracle
+                  beside it (tools/bench_ngp.py).
+  container     — (N = 1) the production MoE container (4 NGP experts + occupancy marching + background MLP,
+                  autograd + FlatAdam): rays/s, per-kernel-class times, the hash kernels' HBM roofline, CPU oracle
+                  (tools/bench_container.py).
   cpu_baseline  — the CPU oracle (a restatement of the reference's PyTorch path, pinned to its golden
                   vectors) running the same train step (4096 rays, 64+128, 2 nets), median of >= 5 steps
                   on this host's CPU share (rank 0, N=1); `all_cores` beside it at os.cpu_count() threads.
@@ -40,6 +46,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement), with
                   path, same workload, timed beside the fused engine.  --path dropin makes it the reported value.
 """
 import argparse
+import faulthandler
 import json
 import os
 import socket
@@ -54,6 +61,9 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402  (importing torch initialises no GPU)
 import torch.distributed as dist  # noqa: E402
+
+# a native fault (HIP runtime, profiler, ctypes) prints every thread's Python stack instead of a bare address list
+faulthandler.enable(all_threads=True)
 
 METRIC = "rays/sec (train step) + full-image PSNR, 800×800 Lego, 64+128 samples"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 / 16x16x4_f32, dense
@@ -120,6 +130,12 @@ def parse():
     ap.add_argument("--fp32-gemm", default="split", choices=["split", "native_dgrad", "native"],
                     help="fp32 trunk GEMMs: all as bf16 split products (gemm_x6.hpp, default), input gradients on the "
                          "fp32 MFMA (native_dgrad), or all on the fp32 MFMA kernels (native)")
+    ap.add_argument("--no-ngp", action="store_true",
+                    help="skip the Instant-NGP expert sub-record (SURVEY §8f row 1, tools/bench_ngp.py)")
+    ap.add_argument("--no-container", action="store_true",
+                    help="skip the production MoE-container sub-record (SURVEY §8f rows 1-3, tools/bench_container.py)")
+    ap.add_argument("--prod-cpu-seconds", type=float, default=12.0,
+                    help="CPU-oracle sample of the ngp / container sub-records (seconds)")
     ap.add_argument("--no-native-ref", action="store_true",
                     help="skip the fp32-MFMA (native) engine leg timed beside the split-GEMM engine")
     return ap.parse_args()
@@ -465,12 +481,14 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_
         dp = {"world_size": dist.get_world_size(), "backend": "nccl (RCCL)" if nccl else "gloo (rehearsal)",
               "step_ms_max": round(el / a.steps * 1e3, 3), "step_ms_min": round(min(r[0] for r in rows) / a.steps * 1e3, 3),
               "allreduce_ms_per_rank": [[round(r[1], 4), round(r[2], 4)] for r in rows],
-              "allreduce_note": "HIP events on the launching stream around each bucket's all_reduce (bucket 1 = coarse "
-                                "net gradient, issued on the side stream right after the coarse backward; bucket 2 = "
+              "allreduce_note": "HIP events on the consuming stream around each bucket's all_reduce (issued "
+                                "async_op=True, end event after work.wait() on that stream; bucket 1 = coarse net "
+                                "gradient, issued on the side stream right after the coarse backward; bucket 2 = "
                                 "fine gradient + loss, after the fine backward), mean over the event steps; includes "
                                 "the wait for the slowest rank",
               "bytes_per_step": int(tr.gbuf.numel() * 4)}
         dp.update(params_checksum(tr.params, world))
+        dp.update(exposed_exchange(a, tr, one, dev, world, barrier, el / a.steps * 1e3))
     rec = {"value": round(n_local * world * a.steps / el, 1), "ms_per_step": round(el / a.steps * 1e3, 3),
            "final_loss": round(float(loss.item()), 6),
            "roofline": dict(roofline(tm, precision == "bf16", False, tr.bf16_flags,
@@ -489,6 +507,41 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_
     if dp:
         rec["dp"] = dp
     return rec, tr, (coarse, fine)
+
+
+def exposed_exchange(a, tr, one, dev, world, barrier, step_ms):
+    """The exchange's exposed cost, measured rather than inferred from events: after the checksum, the same step runs
+    a.steps more times with the all-reduces skipped (tr.exchange_enabled = False: every rank applies its own
+    gradient), timed like the main region (barrier + synchronize, max over ranks); exposed = step time with the
+    exchange - step time without it.  The trainer's parameters / moments are restored afterwards."""
+    saved = [x.detach().clone() for x in (tr.params, tr.m, tr.v)]
+    count = tr.step_count
+    tr.exchange_enabled = False
+    s0 = a.warmup + a.steps + max(1, a.timing_steps)
+    try:
+        one(s0)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s in range(s0 + 1, s0 + 1 + a.steps):
+            one(s)
+        barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    finally:
+        tr.exchange_enabled = True
+        with torch.no_grad():
+            for x, y in zip((tr.params, tr.m, tr.v), saved):
+                x.copy_(y)
+        tr.step_count = count
+    mine = torch.tensor([el], dtype=torch.float64, device=dev)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    no_x = max(float(r.item()) for r in allr) / a.steps * 1e3
+    return {"step_ms_no_exchange": round(no_x, 3), "exposed_exchange_ms": round(step_ms - no_x, 3),
+            "exposed_exchange_note": "step time (max over ranks) with the two all-reduce buckets minus the same "
+                                     "steps with the all-reduces skipped, both timed over --steps steps"}
 
 
 def params_checksum(params, world):
@@ -553,6 +606,30 @@ def sweep_run(a, dev, world, rank):
     summ.update({"steps_per_scene": a.sweep_steps, "train_views": a.sweep_views, "test_views": 2,
                  "per_scene": [{k: r[k] for k in ("scene_seed", "psnr", "rays_per_s", "loss", "rank")} for r in res]})
     return summ
+
+
+def production_runs(a, dev):
+    """the reference's production path — its default expert is Instant-NGP (common/args.py:56-58) with
+    occupancy marching (models/inr/meta_ngp.py:389-443, nerfs/ray_rendering.py:494-558) inside the MoE container
+    (models/inr/meta_container.py:275-343).  The ngp and container sub-records time their train steps (inputs resident
+    in HBM), each with its dominant kernel against its own roofline and the CPU oracle beside it."""
+    from types import SimpleNamespace
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    out = {}
+    cpu = dict(cpu_seconds=a.prod_cpu_seconds, no_cpu_baseline=a.no_cpu_baseline)
+    if not a.no_ngp:
+        import bench_ngp
+        progress("ngp (Instant-NGP expert) leg")
+        out["ngp"] = bench_ngp.run(SimpleNamespace(steps=20, warmup=5, batch=4096, samples=96, train_views=100, **cpu),
+                                   dev)
+        torch.cuda.empty_cache()
+    if not a.no_container:
+        import bench_container
+        progress("container (MoE: 4 NGP experts + occupancy + bg MLP) leg")
+        out["container"] = bench_container.run(SimpleNamespace(steps=48, warmup=40, batch=4096, train_views=100,
+                                                               shard=False, no_bucket=False, **cpu), dev)
+        torch.cuda.empty_cache()
+    return out
 
 
 def psnr_run(a, rb, scene, runs, rank, world, n_local):
@@ -704,6 +781,8 @@ def main():
         sw = sweep_run(a, dev, world, rank)
         if rank == 0:
             out["sweep"] = sw
+    if world == 1 and a.path == "engine" and a.scene == "blender":
+        out.update(production_runs(a, dev))
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.samples, a.importance, a.cpu_batch, a.cpu_steps)
     elif rank == 0:

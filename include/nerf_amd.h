@@ -170,6 +170,22 @@ int nerf_mlp_bwd_bf16(const float* w, int64_t M, const float* d_rgb_sigma, float
                       int64_t ws_bytes, int flags, hipEvent_t* events, hipStream_t stream);
 /* events: as for nerf_mlp_fwd / nerf_mlp_bwd. */
 
+/* fp16 variants: the reference's AMP training loop (pipelines/online_stage/runtime_adapt.py:291-310,
+ * configs/train.json "use_amp": torch.autocast(float16) + GradScaler) on the same fused kernels as the bf16 entry
+ * points, with fp16 operands on v_mfma_f32_32x32x16_f16 (fp32 accumulation) and the reference's rounding points under
+ * autocast (models/metamodule/metamodule.py:150-156: `inputs.matmul(weight.t()) + bias`):
+ *   forward   every layer output = fp32(fp16(x16 W16^T)) + bias (fp32), ReLU, then fp16 as the next matmul's operand;
+ *             the heads / colour-out pre-activations (sigma's trunc_exp input, clamp 88.72) stay fp32;
+ *   backward  activation gradients fp16 (the matmul backward's fp16 outputs), weight gradients summed in fp32 and
+ *             rounded to fp16 once per call (the fp16 grad of the autocast weight cast, then fp32), bias gradients
+ *             fp32 sums; d_w is fp32 and accumulates in fp32 after the rounding.
+ * Workspace as nerf_mlp_workspace_bytes_bf16.  flags: 0 only (no layered form; other bits NERF_E_ENUM). */
+int64_t nerf_mlp_workspace_bytes_f16(int64_t M, int training);
+int nerf_mlp_fwd_f16(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws, int64_t ws_bytes,
+                     int training, int flags, hipEvent_t* events, hipStream_t stream);
+int nerf_mlp_bwd_f16(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
+                     int64_t ws_bytes, int flags, hipEvent_t* events, hipStream_t stream);
+
 /* ------------------------------------------------------------------ compositing + loss */
 
 /* volume_render (nerfs/ray_rendering.py:114-165, raw_rgb=raw_sigma=False).  rgb_sigma (n,S,4),

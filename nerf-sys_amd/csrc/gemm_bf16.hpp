@@ -21,26 +21,86 @@
 #pragma once
 #include "gemm.hpp"
 
+// The 16-bit MLP element of this translation unit.  mlp_bf16.hip is compiled twice: as mlp_bf16.o (bf16, the C3 engine
+// and autocast(bfloat16)) and with -DNERF_F16=1 as mlp_f16.o (fp16: the operands of the reference's AMP loop,
+// torch.autocast(float16), pipelines/online_stage/runtime_adapt.py:291-310, models/metamodule/metamodule.py:150-156).
+// Everything below and in the mlp_bf16_*.hpp kernels lives in a namespace named after the element, so the two builds'
+// kernels and helpers never meet at link time; "nerf_bf16" names the element type of the build.
+#ifndef NERF_F16
+#define NERF_F16 0
+#endif
+#if NERF_F16
+#define NERF_H16NS nerf_h16_f16
+#else
+#define NERF_H16NS nerf_h16_bf16
+#endif
+
+namespace NERF_H16NS {
+
+#if NERF_F16
+typedef _Float16 nerf_bf16;
+typedef _Float16 nerf_bf16x8 __attribute__((ext_vector_type(8)));
+#else
 typedef __bf16 nerf_bf16;
 typedef __bf16 nerf_bf16x8 __attribute__((ext_vector_type(8)));
+#endif
 typedef short nerf_s16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t nerf_pack_bf16x2(float a, float b) {
-  const nerf_bf16 x = (nerf_bf16)a, y = (nerf_bf16)b;  // v_cvt_pk_bf16_f32, round to nearest even
+  const nerf_bf16 x = (nerf_bf16)a, y = (nerf_bf16)b;  // round to nearest even (v_cvt_pk_bf16_f32 / v_cvt_f16_f32)
   return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
 }
 // sin / cos of the frequency encoding for the bf16 path, whose encoding is rounded to bf16 (8-bit mantissa): the
 // argument is reduced to [-1/2, 1/2] revolutions and fed to v_sin_f32 / v_cos_f32 (absolute error ~ |x| 6e-8 rad from
 // the fp32 product, 5e-5 rad at the top band of |x| = 1.5, far below the 2e-3 bf16 rounding of the result).  The fp32
-// path keeps the libm sincosf (pinned to the reference's torch.sin / torch.cos at 1e-5).
+// path keeps the libm sincosf (pinned to the reference's torch.sin / torch.cos at 1e-5), and so does the fp16 build:
+// the reference's encoding is fp32 torch.sin / torch.cos, rounded to fp16 only at the matmul (11-bit significand, so
+// the hardware sine's 5e-5 rad would move one rounding in ten at the top band).
 __device__ __forceinline__ void pe_sincos_bf16(float x, float* s, float* c) {
+#if NERF_F16
+  sincosf(x, s, c);
+#else
   const float r = x * 0.15915494309189535f;
   const float f = r - rintf(r);
   *s = __builtin_amdgcn_sinf(f);
   *c = __builtin_amdgcn_cosf(f);
+#endif
 }
-__device__ __forceinline__ float nerf_bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float nerf_bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+// the low / high element of a packed pair as fp32
+__device__ __forceinline__ float nerf_bf16_lo(uint32_t u) {
+#if NERF_F16
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu));
+#else
+  return __uint_as_float(u << 16);
+#endif
+}
+__device__ __forceinline__ float nerf_bf16_hi(uint32_t u) {
+#if NERF_F16
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16));
+#else
+  return __uint_as_float(u & 0xffff0000u);
+#endif
+}
+// 32x32x16 MFMA of the build's element (fp32 accumulation): v_mfma_f32_32x32x16_bf16 / v_mfma_f32_32x32x16_f16
+__device__ __forceinline__ nerf_f32x16 h16_mfma(nerf_bf16x8 a, nerf_bf16x8 b, nerf_f32x16 c) {
+#if NERF_F16
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+#else
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+// The layer output before its bias.  fp16 build: the reference's autocast matmul returns an fp16 tensor and the fp32
+// bias is added after it (metamodule.py:153-155: fp16 + fp32 promotes to fp32), so the accumulator is rounded to fp16
+// first and the bias added in fp32 (the accumulators start at zero, not at the bias).  bf16 build (the C3 engine's own
+// arithmetic): the accumulators start at the bias and nothing is rounded here.
+constexpr bool H16_BIAS_AFTER = NERF_F16 != 0;
+__device__ __forceinline__ float h16_out(float acc, float bias) {
+#if NERF_F16
+  return (float)(_Float16)acc + bias;
+#else
+  return acc;
+#endif
+}
 
 // epilogue of the bf16 NT GEMMs (C^T: lane li owns row mw + a*32 + li; register r = 4q + e is column
 // 8q + 4lh + e of the 32-column tile b).  bf16 outputs leave as one 16-B store per (q, q+1) pair after a
@@ -199,7 +259,7 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_bf16_kernel(const nerf_bf16
       for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b)  // swapped operands: the tile is C^T (i = n, j = m)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[b], af[a], acc[a][b], 0, 0, 0);
+          acc[a][b] = h16_mfma(bf[b], af[a], acc[a][b]);
     }
     NTB_SSTORE(cur ^ 1);
     __syncthreads();
@@ -356,7 +416,7 @@ __global__ __launch_bounds__(256, MINW) void gemm_nt_bf16_ring_kernel(const nerf
       for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[ks][b], af[ks][a], acc[a][b], 0, 0, 0);
+          acc[a][b] = h16_mfma(bf[ks][b], af[ks][a], acc[a][b]);
     const int ti = g / nk;
     if (g - ti * nk == nk - 1) {
       const int tile = t0 + ti * grid;
@@ -565,7 +625,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_bf16_wsr_kernel(const nerf_bf1
       for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int t = 0; t < TN; ++t)
-          acc[a][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[ks][t], af[ks][a], acc[a][t], 0, 0, 0);
+          acc[a][t] = h16_mfma(bf[ks][t], af[ks][a], acc[a][t]);
     if (kt == NK - 1) {
       const int64_t m0 = (int64_t)(grp + pi * n_groups) * BM;
       if (EPI == EPI_MASK) {
@@ -704,7 +764,7 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_bf16_kernel(const nerf_bf16
           for (int j = 0; j < 8; ++j) bsum[a] += (float)af[a][j];
         }
 #pragma unroll
-        for (int b = 0; b < TN; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bf[b], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < TN; ++b) acc[a][b] = h16_mfma(af[a], bf[b], acc[a][b]);
       }
     }
     WGB_SSTORE(cur ^ 1);
@@ -734,3 +794,6 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_bf16_kernel(const nerf_bf16
     }
   }
 }
+
+}  // namespace NERF_H16NS
+using namespace NERF_H16NS;

@@ -287,6 +287,13 @@ __device__ __forceinline__ void x6_epilogue_lds(nerf_f32x16 (&acc)[TM][TN], int6
         word |= __shfl_xor(word, 32, 64);
         if (lh == 0) mbits_out[m * ldmb + g] = word;
       }
+      // The read-back takes rows other lanes wrote.  What orders it: the wave's LDS operations execute in issue order,
+      // and the write and read addresses (lane-dependent offsets into the same tile) may alias for the compiler, so it
+      // can move neither the reads above these writes nor the next block's writes above these reads.  Explicit
+      // barriers were built and measured (round 5, profiles/r05/x6_epi_fence_ab.txt): wavefront-scope release / acquire
+      // fences cost 17 % of the launch (they wait for the block's global stores); "memory" asm clobbers and
+      // sched_barriers here stop SROA from keeping o in registers (80 B of scratch per lane, or 32 KiB of LDS once
+      // promoted).  Neither is kept.
       float4 o[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[i] = *reinterpret_cast<const float4*>(E + (rr + 8 * i) * X6E_PITCH + cc);
@@ -319,6 +326,16 @@ __device__ unsigned long long nerf_x6_stamps[2][8][128];
 // workgroup per CU): C2 step 204.0k -> 207.5-209.0k rays/s over BK = 16, NW = 4 (fwd / dgrad 0.65 -> 0.63 ms).
 // TM = 1 (32-row waves; the BIGSMALL input gradients, whose 256 accumulator registers per 64-row wave allowed only one
 // wave per SIMD): 256 x 128 tiles at two waves per SIMD.
+#ifndef NERF_X6W_PAIRB
+#define NERF_X6W_PAIRB 0
+#endif
+constexpr bool defined_regb() {
+#ifdef NERF_X6W_REGB
+  return true;
+#else
+  return false;
+#endif
+}
 template <int EPI, int BK = 32, int NW = 8, bool BIGSMALL = false, int TM = 2, int MINW = (BIGSMALL ? 1 : 8 / NW),
           int NKC = 0>
 __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float* __restrict__ A, int lda,
@@ -346,7 +363,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   auto sw = [](int r, int q) { return q; };
 #endif
   constexpr int PL = BN * LS;
-  __shared__ __attribute__((aligned(16))) nerf_bf16 smem[2 * 3 * PL];
+  // PB: one workgroup barrier per PAIR of slabs (four weight buffers: the next pair is DMA'd into the two the previous
+  // pair read, released by that pair's barrier) instead of one per slab — the waves arrive at a slab barrier skewed
+  // (s_memtime stamps, round 4: ~1.9k of a 9.55k-cycle forward slab), and a barrier every other slab pays that wait
+  // once per two slabs.  The two-set, non-A3 loop only.
+  constexpr bool PB = NERF_X6W_PAIRB && !(NKC > 0) && !defined_regb();
+  constexpr int NBUF = PB ? 4 : 2;
+  __shared__ __attribute__((aligned(16))) nerf_bf16 smem[NBUF * 3 * PL];
   static_assert(NW * X6E_WAVE_FLOATS * 4 <= 2 * 3 * PL * 2, "epilogue tiles fit in the weight images");
 
 #ifdef NERF_X6W_STAGGER  // probe builds: every other workgroup starts ~NERF_X6W_STAGGER x 64 clocks late
@@ -482,6 +505,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   {
     const int j = 0;
     X6W_BLOAD(0, 0);
+    if constexpr (PB) X6W_BLOAD(BK, 1);  // host: K % (2 BK) == 0, so slab 1 exists
     if constexpr (ASML) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   X6W_BSTORE(0);
@@ -557,6 +581,31 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
       __syncthreads();
       X6W_STAMP();
     }
+  } else if constexpr (PB) {
+    for (int kt0 = 0; kt0 < nk; kt0 += 2) {
+      const int b0 = kt0 & 3;  // this pair's buffers b0, b0 + 1; the next pair's b0 ^ 2, (b0 ^ 2) + 1
+      {
+        const int j = 0;  // (the DMA's touch: set 0 feeds this pair's first slab)
+        // past the end the last pair is DMA'd again into buffers nobody reads (the drain below covers it)
+        X6W_BLOAD((kt0 + 2 < nk ? kt0 + 2 : nk - 2) * BK, b0 ^ 2);
+        X6W_BLOAD((kt0 + 3 < nk ? kt0 + 3 : nk - 1) * BK, (b0 ^ 2) + 1);
+      }
+      asm volatile("" ::: "memory");
+      slab_mfma(ra[0], smem + b0 * 3 * PL, [&]() __attribute__((always_inline)) {
+        X6W_ALOAD(0, (kt0 + 2 < nk ? kt0 + 2 : nk - 1) * BK);
+        asm volatile("" ::: "memory");
+      });
+      slab_mfma(ra[1], smem + (b0 + 1) * 3 * PL, [&]() __attribute__((always_inline)) {
+        X6W_ALOAD(1, (kt0 + 3 < nk ? kt0 + 3 : nk - 1) * BK);
+        asm volatile("" ::: "memory");
+      });
+      // the next pair's two DMAs done; the two activation sets issued after them stay in flight
+      if constexpr (TM * KS * 2 == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      X6W_STAMP();
+      __syncthreads();
+      X6W_STAMP();
+    }
   } else
   for (int kt0 = 0; kt0 < nk; kt0 += 2) {
 #pragma unroll
@@ -591,6 +640,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
 #undef X6W_BWAIT
 #undef X6W_BSTORE
 
+  if constexpr (GLDS && !A3) {
+    // the two-set loop's last slab re-issued slab nk - 1's weight DMA into buffer 0, which the epilogue tiles below
+    // reuse; the loop's counted vmcnt covered it only while the (dead) activation loads after it were still issued.
+    // Drain every wave's DMA and meet before any wave writes its epilogue tile, independent of what hipcc keeps.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   if constexpr (BIGSMALL) {
 #pragma unroll
     for (int a = 0; a < TM; ++a)

@@ -19,6 +19,14 @@
 #include "mlp_tail.hpp"
 #include "mlp_common.hpp"
 
+// entry-point names of this build (gemm_bf16.hpp NERF_F16): nerf_mlp_*_bf16 or nerf_mlp_*_f16
+#if NERF_F16
+#define NERF_H16_FN(name) name##_f16
+#else
+#define NERF_H16_FN(name) name##_bf16
+#endif
+
+namespace NERF_H16NS {
 namespace {
 using namespace nerf_mlp;
 
@@ -389,6 +397,21 @@ int fused_forward(const float* w, const float* x_d, int64_t M, float* rgb_sigma,
   return nerf_launch_status();
 }
 
+// the 11 bias tensors of the packed layout (packed offsets / lengths): the fp16 build rounds every other sum
+struct BiasTab {
+  int64_t off[11];
+  int len[11];
+};
+inline BiasTab bias_tab() {
+  const Layout& L = layout();
+  BiasTab b{};
+  for (int t = 0; t < 11; ++t) {
+    b.off[t] = L.off[2 * t + 1];
+    b.len[t] = L.rows[2 * t + 1];
+  }
+  return b;
+}
+
 // Final reduce of the fused backward (fixed order, bitwise reproducible): element e of the packed gradient =
 //   trunk.0 W / b and trunk.4 W[:, 256:320]  sum over the S2 narrow sub-slabs (np);
 //   everything else                          sum over the S split slabs, plus (e >= off16: head / colour) the S
@@ -397,7 +420,7 @@ __global__ __launch_bounds__(256) void reduce_fused_bf16_kernel(const float* __r
                                                                 const float* __restrict__ partial2, int64_t slab2,
                                                                 int64_t off16, const float* __restrict__ np, int S2,
                                                                 float* __restrict__ dst, int64_t n4, int accumulate,
-                                                                int64_t off0, int64_t off1, int64_t off8) {
+                                                                int64_t off0, int64_t off1, int64_t off8, BiasTab bt) {
   // gemm.hpp's RG-group order (one wave per group of slabs, 64 elements per block; grid cdiv(n4, 64)): the 256-wide
   // trunk weights sum exactly as the layered path's reduce_splits_kernel does
   __shared__ float4 part[2][RG][64];
@@ -417,14 +440,37 @@ __global__ __launch_bounds__(256) void reduce_fused_bf16_kernel(const float* __r
   part[1][g][el] = two ? rg_group_sum(partial2 + (e - off16), slab2, S, g) : z;
   __syncthreads();
   if (g == 0 && live) {
-    float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : z;
+    if constexpr (NERF_F16) {
+      // the reference's weight gradient is an fp16 matmul output, cast to fp32 and then accumulated in fp32: this
+      // call's sum is rounded to fp16 once (overflow -> inf, which GradScaler then sees), biases stay fp32 sums
+      float4 a = z;
 #pragma unroll
-    for (int k = 0; k < RG; ++k) rg_add(a, part[0][k][el]);
-    if (two) {
+      for (int k = 0; k < RG; ++k) rg_add(a, part[0][k][el]);
+      if (two) {
 #pragma unroll
-      for (int k = 0; k < RG; ++k) rg_add(a, part[1][k][el]);
+        for (int k = 0; k < RG; ++k) rg_add(a, part[1][k][el]);
+      }
+      bool bias = false;
+#pragma unroll
+      for (int t = 0; t < 11; ++t) bias |= e >= bt.off[t] && e < bt.off[t] + bt.len[t];
+      if (!bias) {
+        a.x = (float)(_Float16)a.x; a.y = (float)(_Float16)a.y; a.z = (float)(_Float16)a.z; a.w = (float)(_Float16)a.w;
+      }
+      if (accumulate) {
+        const float4 d = reinterpret_cast<const float4*>(dst)[i];
+        a = make_float4(d.x + a.x, d.y + a.y, d.z + a.z, d.w + a.w);
+      }
+      reinterpret_cast<float4*>(dst)[i] = a;
+    } else {
+      float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : z;
+#pragma unroll
+      for (int k = 0; k < RG; ++k) rg_add(a, part[0][k][el]);
+      if (two) {
+#pragma unroll
+        for (int k = 0; k < RG; ++k) rg_add(a, part[1][k][el]);
+      }
+      reinterpret_cast<float4*>(dst)[i] = a;
     }
-    reinterpret_cast<float4*>(dst)[i] = a;
   }
 }
 
@@ -487,19 +533,22 @@ int fused_backward(const float* w, int64_t M, const float* d_rgb_sigma, float* d
   const int64_t n4 = L.total / 4;
   reduce_fused_bf16_kernel<<<(unsigned)nerf_cdiv(n4, 64), 256, 0, st>>>(
       W.partial, L.total, W.S, W.partial2, L.total - L.off[16], L.off[16], W.np, W.S2, d_w, n4, accumulate, L.off[0],
-      L.off[1], L.off[8]);
+      L.off[1], L.off[8], bias_tab());
   return nerf_launch_status();
 }
 
-extern "C" int64_t nerf_mlp_workspace_bytes_bf16(int64_t M, int training) {
+}  // namespace NERF_H16NS
+using namespace NERF_H16NS;
+
+extern "C" int64_t NERF_H16_FN(nerf_mlp_workspace_bytes)(int64_t M, int training) {
   if (M < 0) return -1;
   return carve_b(nullptr, M, training).bytes + 256;
 }
 
-extern "C" int nerf_mlp_fwd_bf16(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws,
+extern "C" int NERF_H16_FN(nerf_mlp_fwd)(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws,
                                  int64_t ws_bytes, int training, int flags, hipEvent_t* ev, hipStream_t st) {
   NERF_CHECK_ARG(w && x_d && rgb_sigma && ws && M >= 0);
-  if (flags & ~(NERF_BF16_LAYERED_FWD | NERF_BF16_LAYERED_BWD)) return NERF_E_ENUM;
+  if (flags & ~(NERF_F16 ? 0 : (NERF_BF16_LAYERED_FWD | NERF_BF16_LAYERED_BWD))) return NERF_E_ENUM;
   if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(rgb_sigma)) return NERF_E_ALIGN;
   const WSB W = carve_b(ws, M, training);
   if (ws_bytes < W.bytes) return NERF_E_WORKSPACE;
@@ -535,10 +584,10 @@ extern "C" int nerf_mlp_fwd_bf16(const float* w, const float* x_d, int64_t M, fl
   return nerf_launch_status();
 }
 
-extern "C" int nerf_mlp_bwd_bf16(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate,
+extern "C" int NERF_H16_FN(nerf_mlp_bwd)(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate,
                                  void* ws, int64_t ws_bytes, int flags, hipEvent_t* ev, hipStream_t st) {
   NERF_CHECK_ARG(w && d_rgb_sigma && d_w && ws && M >= 0);
-  if (flags & ~(NERF_BF16_LAYERED_FWD | NERF_BF16_LAYERED_BWD)) return NERF_E_ENUM;
+  if (flags & ~(NERF_F16 ? 0 : (NERF_BF16_LAYERED_FWD | NERF_BF16_LAYERED_BWD))) return NERF_E_ENUM;
   if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(d_w) || !nerf_aligned16(d_rgb_sigma))
     return NERF_E_ALIGN;
   const WSB W = carve_b(ws, M, 1);

@@ -44,6 +44,7 @@
 #include "gemm_bf16.hpp"
 #include "mlp_common.hpp"
 
+namespace NERF_H16NS {
 namespace nerf_bwd {
 
 constexpr int TR = 64;                  // rows per tile
@@ -219,7 +220,7 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, char* lds, int s
       asm volatile("" ::"v"(gf[cb][0]), "v"(gf[cb][1]), "v"(gf[cb][2]), "v"(gf[cb][3]), "v"(xf[cb]));
 #else
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf[cb][j], xf[cb], acc[j], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) acc[j] = h16_mfma(gf[cb][j], xf[cb], acc[j]);
 #endif
       SCHED_FENCE();
     });
@@ -248,7 +249,7 @@ __device__ __forceinline__ void bwd_compute(const LayerArgs& A, char* lds, int s
 #ifdef NERF_EXP_BWD_NODG
       asm volatile("" ::"v"(wf), "v"(g));
 #else
-      dacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, g, dacc, 0, 0, 0);
+      dacc = h16_mfma(wf, g, dacc);
 #endif
       SCHED_FENCE();
     });
@@ -347,8 +348,8 @@ __device__ __forceinline__ void bias_acc(const IoSet& R, float (&bs)[8]) {
     const io_u32x4 v = const_cast<IoSet&>(R).template at<i>();
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-      bs[2 * d] += __uint_as_float(v[d] << 16);
-      bs[2 * d + 1] += __uint_as_float(v[d] & 0xffff0000u);
+      bs[2 * d] += nerf_bf16_lo(v[d]);
+      bs[2 * d + 1] += nerf_bf16_hi(v[d]);
     }
   });
 }
@@ -468,3 +469,4 @@ __global__ __launch_bounds__(768, 3) void bwd_layer_bf16_kernel(LayerArgs A) {
 }
 
 }  // namespace nerf_bwd
+}  // namespace NERF_H16NS

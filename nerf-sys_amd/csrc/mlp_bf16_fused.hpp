@@ -24,6 +24,7 @@
 #include "gemm_bf16.hpp"
 #include "mlp_common.hpp"
 
+namespace NERF_H16NS {
 namespace nerf_fused {
 using namespace nerf_mlp;
 
@@ -158,12 +159,23 @@ __device__ __forceinline__ nerf_bf16x8 lds_frag(const nerf_bf16* p) { return *re
 // biases of every layer, staged in LDS once per workgroup: trunk.i at 256 i, head 2048, colour0 2080, colour1 2208
 constexpr int BOFF[FT] = {0, 256, 512, 768, 1024, 1280, 1536, 1792, 2048, 2080, 2208};
 constexpr int BTOT = 2240;
+// (fp16 build: zero — the bias is added after the matmul output's fp16 rounding, gemm_bf16.hpp h16_out)
 __device__ __forceinline__ void acc_bias(nerf_f32x16& acc, const float* bias, int col0, int lh) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const float4 b = *reinterpret_cast<const float4*>(bias + col0 + 8 * q + 4 * lh);
-    acc[4 * q + 0] = b.x; acc[4 * q + 1] = b.y; acc[4 * q + 2] = b.z; acc[4 * q + 3] = b.w;
+    if constexpr (H16_BIAS_AFTER) {
+      acc[4 * q + 0] = acc[4 * q + 1] = acc[4 * q + 2] = acc[4 * q + 3] = 0.f;
+    } else {
+      const float4 b = *reinterpret_cast<const float4*>(bias + col0 + 8 * q + 4 * lh);
+      acc[4 * q + 0] = b.x; acc[4 * q + 1] = b.y; acc[4 * q + 2] = b.z; acc[4 * q + 3] = b.w;
+    }
   }
+}
+// the layer output of accumulator register 4 q + e of a 32-column block starting at col0 (fp16 build: fp16-rounded
+// matmul output + fp32 bias; bf16 build: the accumulator, which started at the bias)
+__device__ __forceinline__ float acc_out(const nerf_f32x16& acc, int r, const float* bias, int col0, int lh) {
+  if constexpr (H16_BIAS_AFTER) return h16_out(acc[r], bias[col0 + 8 * (r >> 2) + 4 * lh + (r & 3)]);
+  return acc[r];
 }
 
 // k-step order of a stage (position p -> k-step kk), so that a wave starts on the columns IT wrote in the previous
@@ -254,7 +266,7 @@ __device__ __forceinline__ void stage(nerf_f32x16 (&acc)[4][2], Ring& ring, __am
     for (int a = 0; a < TA; ++a)
 #pragma unroll
       for (int b = 0; b < NBW; ++b)
-        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[b], af[a], acc[a][b], 0, 0, 0);
+        acc[a][b] = h16_mfma(bf[b], af[a], acc[a][b]);
 #endif
     if (p + 1 < KS && p + 1 != BAR) {
 #pragma unroll
@@ -267,7 +279,7 @@ __device__ __forceinline__ void stage(nerf_f32x16 (&acc)[4][2], Ring& ring, __am
 // LDS tile (pitch): two values per v_cvt_pk_bf16_f32, ReLU as v_pk_max_i16 on the bf16 bit patterns (rounding keeps
 // the sign, so round-then-clamp == clamp-then-round), 16-B stores after pairing the lane halves (gemm_bf16.hpp).
 typedef float nerf_f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 nerf_bf16x2 __attribute__((ext_vector_type(2)));
+typedef nerf_bf16 nerf_bf16x2 __attribute__((ext_vector_type(2)));
 typedef short nerf_s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t relu_pk(float x, float y) {
   const nerf_f32x2 f = {x, y};
@@ -278,7 +290,7 @@ __device__ __forceinline__ uint32_t relu_pk(float x, float y) {
 
 template <int TA, int NB>
 __device__ __forceinline__ void relu_to_lds(const nerf_f32x16 (&acc)[4][2], nerf_bf16* dst, int pitch, int ar0, int c0,
-                                            int li, int lh) {
+                                            int li, int lh, const float* bias) {
 #ifdef NERF_EXP_FWD_NOEPI
 #pragma unroll
   for (int a = 0; a < TA; ++a)
@@ -294,7 +306,8 @@ __device__ __forceinline__ void relu_to_lds(const nerf_f32x16 (&acc)[4][2], nerf
       uint2 pk[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        pk[q] = make_uint2(relu_pk(acc[a][b][4 * q], acc[a][b][4 * q + 1]), relu_pk(acc[a][b][4 * q + 2], acc[a][b][4 * q + 3]));
+        pk[q] = make_uint2(relu_pk(acc_out(acc[a][b], 4 * q, bias, c0 + 32 * b, lh), acc_out(acc[a][b], 4 * q + 1, bias, c0 + 32 * b, lh)),
+                           relu_pk(acc_out(acc[a][b], 4 * q + 2, bias, c0 + 32 * b, lh), acc_out(acc[a][b], 4 * q + 3, bias, c0 + 32 * b, lh)));
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
         uint2 x = pk[2 * pr], y = pk[2 * pr + 1];
@@ -517,41 +530,41 @@ __device__ __forceinline__ void compute_role(const FusedArgs& A, nerf_bf16* Hs, 
     // trunk: <KS, NBW, TA, KIND, ESRC, BAR, KSN, NBWN, KINDN>; epilogue k -> H[k & 1]
     bias_trunk(0);
     stage<4, 2, 4, K_ID, 1, -1, 16, 2, K_ROT16>(acc, ring, rs, F(0), 2 * w, F(1), 2 * w, H1, Es, HP, EP, 0, li, lh, lane, w);
-    relu_to_lds<4, 2>(acc, H0, HP, 0, 64 * w, li, lh);
+    relu_to_lds<4, 2>(acc, H0, HP, 0, 64 * w, li, lh, BI(0));
     bias_trunk(1);
     stage<16, 2, 4, K_ROT16, 0, 4, 16, 2, K_ROT16>(acc, ring, rs, F(1), 2 * w, F(2), 2 * w, H0, Es, HP, EP, 0, li, lh, lane, w);
-    relu_to_lds<4, 2>(acc, H1, HP, 0, 64 * w, li, lh);
+    relu_to_lds<4, 2>(acc, H1, HP, 0, 64 * w, li, lh, BI(1));
     bias_trunk(2);
     stage<16, 2, 4, K_ROT16, 0, 4, 16, 2, K_ROT16>(acc, ring, rs, F(2), 2 * w, F(3), 2 * w, H1, Es, HP, EP, 0, li, lh, lane, w);
-    relu_to_lds<4, 2>(acc, H0, HP, 0, 64 * w, li, lh);
+    relu_to_lds<4, 2>(acc, H0, HP, 0, 64 * w, li, lh, BI(2));
     bias_trunk(3);
     stage<16, 2, 4, K_ROT16, 0, 4, 20, 2, K_L4>(acc, ring, rs, F(3), 2 * w, F(4), 2 * w, H0, Es, HP, EP, 0, li, lh, lane, w);
-    relu_to_lds<4, 2>(acc, H1, HP, 0, 64 * w, li, lh);
+    relu_to_lds<4, 2>(acc, H1, HP, 0, 64 * w, li, lh, BI(3));
     bias_trunk(4);
     stage<20, 2, 4, K_L4, 2, 8, 16, 2, K_ROT16>(acc, ring, rs, F(4), 2 * w, F(5), 2 * w, H1, Es, HP, EP, 0, li, lh, lane, w);
-    relu_to_lds<4, 2>(acc, H0, HP, 0, 64 * w, li, lh);
+    relu_to_lds<4, 2>(acc, H0, HP, 0, 64 * w, li, lh, BI(4));
     bias_trunk(5);
     stage<16, 2, 4, K_ROT16, 0, 4, 16, 2, K_ROT16>(acc, ring, rs, F(5), 2 * w, F(6), 2 * w, H0, Es, HP, EP, 0, li, lh, lane, w);
-    relu_to_lds<4, 2>(acc, H1, HP, 0, 64 * w, li, lh);
+    relu_to_lds<4, 2>(acc, H1, HP, 0, 64 * w, li, lh, BI(5));
     bias_trunk(6);
     stage<16, 2, 4, K_ROT16, 0, 4, 16, 2, K_ROT16>(acc, ring, rs, F(6), 2 * w, F(7), 2 * w, H1, Es, HP, EP, 0, li, lh, lane, w);
-    relu_to_lds<4, 2>(acc, H0, HP, 0, 64 * w, li, lh);
+    relu_to_lds<4, 2>(acc, H0, HP, 0, 64 * w, li, lh, BI(6));
     bias_trunk(7);
     // the head's fragments are one 32-column block shared by every wave (nb 0)
     stage<16, 2, 4, K_ROT16, 0, 4, 16, 1, K_ROT16>(acc, ring, rs, F(7), 2 * w, F(8), 0, H0, Es, HP, EP, 0, li, lh, lane, w);
-    relu_to_lds<4, 2>(acc, H1, HP, 0, 64 * w, li, lh);
+    relu_to_lds<4, 2>(acc, H1, HP, 0, 64 * w, li, lh, BI(7));
 
     // ---- head: O16 = h7 W_head^T + b (sigma | 15 geo | 0), wave w -> rows 32w..32w+31 (own trunk.7 columns first)
     acc_bias(acc[0][0], BI(8), 0, lh);
     stage<16, 1, 1, K_ROT16, 0, 4, 4, 1, K_ID>(acc, ring, rs, F(8), 0, F(9), w, H1, Es, HP, EP, 32 * w, li, lh, lane, w);
     const int r = 32 * w + li;
-    if (lh == 0) Ssig[r] = acc[0][0][0];
+    if (lh == 0) Ssig[r] = acc_out(acc[0][0], 0, BI(8), 0, lh);
 #pragma unroll
     for (int q = 0; q < 2; ++q)  // geo (cols 1..15) -> colour input cols 0..14 (E holds the prefill since B_4)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int c = 8 * q + 4 * lh + e;
-        if (c >= 1) Es[r * EP + c - 1] = (nerf_bf16)acc[0][0][4 * q + e];
+        if (c >= 1) Es[r * EP + c - 1] = (nerf_bf16)acc_out(acc[0][0], 4 * q + e, BI(8), 0, lh);
       }
     bar();  // H2: colour input complete; every wave done reading H[1] (trunk.7 output)
 
@@ -559,7 +572,7 @@ __device__ __forceinline__ void compute_role(const FusedArgs& A, nerf_bf16* Hs, 
 #pragma unroll
     for (int a = 0; a < 4; ++a) acc_bias(acc[a][0], BI(9), 32 * w, lh);
     stage<4, 1, 4, K_ID, 1, -1, 8, 1, K_ROT8>(acc, ring, rs, F(9), w, F(10), 0, H1, Es, HP, EP, 0, li, lh, lane, w);
-    relu_to_lds<4, 1>(acc, H1, CP, 0, 32 * w, li, lh);
+    relu_to_lds<4, 1>(acc, H1, CP, 0, 32 * w, li, lh, BI(9));
 
     // ---- colour out: O3 = C0 W_c1^T + b, wave w -> rows 32w..32w+31 (barrier C after its own 2 k-steps);
     // the next tile's trunk.0 fragments are prefetched into the ring
@@ -568,6 +581,9 @@ __device__ __forceinline__ void compute_role(const FusedArgs& A, nerf_bf16* Hs, 
     const int64_t m = m0 + r;
     if (lh == 0) {
       const float sraw = Ssig[r];
+      if constexpr (H16_BIAS_AFTER)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[0][0][e] = acc_out(acc[0][0], e, BI(10), 0, 0);
       if (TRAIN) {
         // the backward reads sigma_raw (O16 col 0) and the colour-out pre-activations (O3 cols 0..2)
         A.O16[m * 32] = sraw;
@@ -612,3 +628,4 @@ __global__ __launch_bounds__(512, 1) void mlp_fwd_fused_bf16_kernel(FusedArgs A)
 }
 
 }  // namespace nerf_fused
+}  // namespace NERF_H16NS

@@ -19,6 +19,7 @@
 #pragma once
 #include "mlp_bf16_bwd.hpp"
 
+namespace NERF_H16NS {
 namespace nerf_tail {
 using nerf_bwd::raw_barrier;
 using nerf_bwd::static_for;
@@ -32,7 +33,8 @@ constexpr int O_OFF = G_OFF + 1024, S_OFF = O_OFF + 1024, STB = S_OFF + 256;
 constexpr int NSTG = 2;
 // work area: dO3 [64][32] bf16 | dO16 [64][32] bf16 | dC0 [64][128] bf16 | ds [64] f32 | shifted Wc0^T fragments (8 KiB)
 constexpr int D3_OFF = NSTG * STB, D16_OFF = D3_OFF + 4096, DC_OFF = D16_OFF + 4096, DS_OFF = DC_OFF + 16384;
-constexpr int WC0_OFF = DS_OFF + 256, LDS_BYTES = WC0_OFF + 8192;
+// (fp16 build: + the sigma head's weight row as fp16, WS_OFF, 512 B)
+constexpr int WC0_OFF = DS_OFF + 256, WS_OFF = WC0_OFF + 8192, LDS_BYTES = WS_OFF + (NERF_F16 ? 512 : 0);
 static_assert(LDS_BYTES <= 163840, "LDS");
 
 __device__ __forceinline__ int swz8(int r) { return 4 * ((r >> 1) & 1); }  // CIN rows (8 chunks): tr reads only
@@ -114,10 +116,15 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
     wc1[ks] = wfrag(W + A.off20, 128, 1, 32 * (w & 3), ks, lane);  // A[i = C0 col][kk = dO3 col] = Wc1[kk][i]
     wh[ks] = wfrag(W + A.off16, 256, 1, 32 * w, ks, lane);        // A[i = Y7 col][kk = dO16 col] = Wh[kk][i]
   }
+  if constexpr (NERF_F16)  // geo only: the sigma row (kk = 0: k-step 0, lane half 0, element 0) is added apart
+    if (lh == 0) wh[0][0] = (nerf_bf16)0.f;
   nerf_f32x16 ac1, ac0, ahd;  // dWc1 (waves 0-3: k-block w), dWc0 (n-block w >> 1, k-block w & 1), dWh (k-block w)
 #pragma unroll
   for (int r = 0; r < 16; ++r) ac1[r] = ac0[r] = ahd[r] = 0.f;
   float b1 = 0.f, b0 = 0.f, bh = 0.f;
+  // fp16 build: the sigma-head and colour-out bias gradients are sums of the fp32 pre-activation gradients (the bias
+  // add is fp32 in the reference, metamodule.py:153-155; only the matmul's operand is fp16), kept by wave 0 in P0
+  float fa = 0.f, fb = 0.f, fc = 0.f, fs = 0.f;
   // transposing-read bases (k-step 0): work tiles absolute, stage tiles relative to the stage (+ Lo per tile)
   const uint32_t lb = (uint32_t)(uintptr_t)lds;
   uint32_t t3a0, t3a1, tca0, tca1, tda0, tda1, tia0, tia1, t16a0, t16a1, tya0, tya1;
@@ -146,6 +153,9 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
         c = g.z * (s2 * (1.0f - s2));
         ds = g.w * expf(fminf(fmaxf(sr, -nerf_mlp::EXP_MAX), nerf_mlp::EXP_MAX));
       }
+      if constexpr (NERF_F16) {
+        fa += a; fb += b; fc += c; fs += ds;
+      }
       *reinterpret_cast<uint4*>(lds + a3(lane, 0)) = make_uint4(nerf_pack_bf16x2(a, b), nerf_pack_bf16x2(c, 0.f), 0u, 0u);
       *reinterpret_cast<float*>(lds + DS_OFF + 4 * lane) = ds;
     }
@@ -158,7 +168,7 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
 #pragma unroll
       for (int r = 0; r < 16; ++r) d[r] = 0.f;
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wc1[ks], ld16(lds + a3(row, 2 * ks + lh)), d, 0, 0, 0);
+      for (int ks = 0; ks < 2; ++ks) d = h16_mfma(wc1[ks], ld16(lds + a3(row, 2 * ks + lh)), d);
       uint4 o[2];
       pack_pairs(d, o);
 #pragma unroll
@@ -182,7 +192,7 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
 #pragma unroll
           for (int j = 0; j < 8; ++j) b1 += (float)ga[ks][j];
         }
-        ac1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ks], gb[ks], ac1, 0, 0, 0);
+        ac1 = h16_mfma(ga[ks], gb[ks], ac1);
       }
     }
     wait_lds();
@@ -195,8 +205,8 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
       for (int r = 0; r < 16; ++r) d[r] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks)
-        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld16(lds + WC0_OFF + ks * 1024 + 16 * lane), ld16(lds + adc(row, 2 * ks + lh)),
-                                                    d, 0, 0, 0);
+        d = h16_mfma(ld16(lds + WC0_OFF + ks * 1024 + 16 * lane), ld16(lds + adc(row, 2 * ks + lh)),
+                                                    d);
       uint4 o[2];
       pack_pairs(d, o);
       uint4 v = o[0];  // dO16 cols 8 lh .. 8 lh + 7 (col 0 = ds)
@@ -221,7 +231,7 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
 #pragma unroll
           for (int j = 0; j < 8; ++j) b0 += (float)ga[ks][j];
         }
-        ac0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ks], gb[ks], ac0, 0, 0, 0);
+        ac0 = h16_mfma(ga[ks], gb[ks], ac0);
       }
     }
     wait_lds();
@@ -235,7 +245,21 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
 #pragma unroll
         for (int r = 0; r < 16; ++r) d[r] = 0.f;
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[ks], ld16(lds + a16(row, 2 * ks + lh)), d, 0, 0, 0);
+        for (int ks = 0; ks < 2; ++ks) d = h16_mfma(wh[ks], ld16(lds + a16(row, 2 * ks + lh)), d);
+        if constexpr (NERF_F16) {
+          // the reference's h7 feeds two fp16 matmuls (sigma_head, geo_head): each input gradient is rounded to fp16,
+          // the two are added in fp32 and the sum rounded again where it enters trunk.7's matmul backward.  wh has its
+          // sigma row zeroed (geo only); the sigma part is the rank-1 product ds16 * Ws16 (exact in fp32), rounded
+          const float ds16 = (float)(nerf_bf16)*reinterpret_cast<const float*>(lds + DS_OFF + 4 * row);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint2 wv = *reinterpret_cast<const uint2*>(lds + WS_OFF + 2 * (32 * w + 8 * q + 4 * lh));
+            const float ws4[4] = {nerf_bf16_lo(wv.x), nerf_bf16_hi(wv.x), nerf_bf16_lo(wv.y), nerf_bf16_hi(wv.y)};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              d[4 * q + e] = (float)(nerf_bf16)d[4 * q + e] + (float)(nerf_bf16)(ds16 * ws4[e]);
+          }
+        }
         uint4 o[2];
         pack_pairs(d, o);
         nerf_bf16* dst = A.dZ7 + (r0 + (int64_t)t * TR + row) * 256 + 32 * w + 8 * lh;
@@ -264,7 +288,7 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
 #pragma unroll
           for (int j = 0; j < 8; ++j) bh += (float)ga[ks][j];
         }
-        ahd = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ks], gb[ks], ahd, 0, 0, 0);
+        ahd = h16_mfma(ga[ks], gb[ks], ahd);
       }
     }
   }
@@ -279,6 +303,14 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
   b1 += __shfl_xor(b1, 32, 64);
   b0 += __shfl_xor(b0, 32, 64);
   bh += __shfl_xor(bh, 32, 64);
+  if constexpr (NERF_F16) {
+    if (w == 0) {
+      fa = wave_sum(fa); fb = wave_sum(fb); fc = wave_sum(fc); fs = wave_sum(fs);
+      if (li == 0) { b1 = fa; bh = fs; }
+      if (li == 1) b1 = fb;
+      if (li == 2) b1 = fc;
+    }
+  }
   if (lh == 0) {
     if (w == 0) {
       P[A.off21 + li] = b1;
@@ -402,6 +434,8 @@ __global__ __launch_bounds__(768, 3) void bwd_tail_bf16_kernel(TailArgs A) {
     }
     *reinterpret_cast<nerf_bf16x8*>(lds + WC0_OFF + ks * 1024 + 16 * l) = v;
   }
+  if constexpr (NERF_F16)
+    for (int i = tid; i < 256; i += 768) reinterpret_cast<nerf_bf16*>(lds + WS_OFF)[i] = (nerf_bf16)A.w[A.off16 + i];
   wait_lds();
   if (w >= 8) {
     tail_io(A, lds, w - 8, nT, r0, lane);
@@ -412,3 +446,4 @@ __global__ __launch_bounds__(768, 3) void bwd_tail_bf16_kernel(TailArgs A) {
 }
 
 }  // namespace nerf_tail
+}  // namespace NERF_H16NS

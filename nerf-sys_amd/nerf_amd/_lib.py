@@ -49,6 +49,9 @@ def lib():
             "nerf_mlp_workspace_bytes_bf16": [I64, I],
             "nerf_mlp_fwd_bf16": [P, P, I64, P, P, I64, I, I, P, P],
             "nerf_mlp_bwd_bf16": [P, I64, P, P, I, P, I64, I, P, P],
+            "nerf_mlp_workspace_bytes_f16": [I64, I],
+            "nerf_mlp_fwd_f16": [P, P, I64, P, P, I64, I, I, P, P],
+            "nerf_mlp_bwd_f16": [P, I64, P, P, I, P, I64, I, P, P],
             "nerf_composite_fwd": [P, P, P, I64, I, F, P, P, P, P, P, I, F, P, P, P],
             "nerf_composite_bwd": [P, P, P, I64, I, F, P, P, P, P, P, P],
             "nerf_grad_sqnorm": [P, I64, P, P],
@@ -115,6 +118,7 @@ def lib():
         L.nerf_mlp_workspace_bytes.restype = c_int64
         L.nerf_mlp_workspace_bytes_2s.restype = c_int64
         L.nerf_mlp_workspace_bytes_bf16.restype = c_int64
+        L.nerf_mlp_workspace_bytes_f16.restype = c_int64
         L.nerf_version.restype = ctypes.c_char_p
         L.nerf_ngp_layout.restype = c_int64
         L.nerf_ngp_workspace_bytes.restype = c_int64
@@ -132,6 +136,7 @@ EXPORTS = ("nerf_rays_gen", "nerf_pick_pixels", "nerf_clamp_near_far", "nerf_ray
            "nerf_mlp_layout", "nerf_mlp_workspace_bytes", "nerf_mlp_fwd", "nerf_mlp_bwd",
            "nerf_mlp_workspace_bytes_2s", "nerf_mlp_bwd_2s", "nerf_mlp_fwd_ex", "nerf_mlp_bwd_ex", "nerf_mlp_bwd_2s_ex",
            "nerf_mlp_workspace_bytes_bf16", "nerf_mlp_fwd_bf16", "nerf_mlp_bwd_bf16",
+           "nerf_mlp_workspace_bytes_f16", "nerf_mlp_fwd_f16", "nerf_mlp_bwd_f16",
            "nerf_composite_fwd", "nerf_composite_bwd", "nerf_grad_sqnorm", "nerf_adam", "nerf_version",
            "nerf_hash_encode", "nerf_hash_encode_bwd", "nerf_sh_encode", "nerf_ngp_layout",
            "nerf_ngp_workspace_bytes", "nerf_ngp_fwd", "nerf_ngp_bwd", "nerf_moe_route",

@@ -20,7 +20,10 @@ def inv_count(n_local: int, world: int) -> float:
     return 1.0 / (3.0 * n_local * world)
 
 
-def allreduce_flat(buf: torch.Tensor, world: int) -> torch.Tensor:
-    if world > 1:
-        dist.all_reduce(buf, op=dist.ReduceOp.SUM)
-    return buf
+def allreduce_flat(buf: torch.Tensor, world: int, async_op: bool = False):
+    """SUM all-reduce of the flat buffer in place.  async_op=True returns the work handle (the caller waits on the
+    stream that consumes the result), else the buffer after a blocking call."""
+    if world <= 1:
+        return None if async_op else buf
+    work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, async_op=async_op)
+    return work if async_op else buf

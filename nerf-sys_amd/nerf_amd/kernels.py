@@ -113,7 +113,10 @@ def freq_encode(x, L, include_input=True):
 # ------------------------------------------------------------------ MLP
 
 
-PRECISIONS = ("fp32", "bf16")
+PRECISIONS = ("fp32", "bf16", "fp16")
+# the 16-bit builds of the fused MLP kernels (include/nerf_amd.h): bf16 (configs[2], autocast(bfloat16)) and fp16 (the
+# reference's autocast(float16) operands and rounding points, runtime_adapt.py:291-310)
+_H16 = {"bf16": "bf16", "fp16": "f16"}
 # bf16 path selection (include/nerf_amd.h): 0 = the fused production kernels; the layered launches are their
 # bitwise references.  A workspace's backward must use the NERF_BF16_LAYERED_BWD bit of its training forward.
 BF16_LAYERED_FWD = 1
@@ -127,8 +130,8 @@ def _check_precision(precision):
 
 def mlp_workspace_bytes(M, training, precision="fp32"):
     _check_precision(precision)
-    if precision == "bf16":
-        return lib().nerf_mlp_workspace_bytes_bf16(M, int(training))
+    if precision in _H16:
+        return getattr(lib(), f"nerf_mlp_workspace_bytes_{_H16[precision]}")(M, int(training))
     return lib().nerf_mlp_workspace_bytes(M, int(training))
 
 
@@ -159,9 +162,10 @@ def mlp_fwd(w_packed, x_d, ws, training, out=None, events=None, precision="fp32"
     M = x_d.shape[0]
     if out is None:
         out = _empty((M, 4), x_d)
-    if precision == "bf16":
-        check(lib().nerf_mlp_fwd_bf16(ptr(w_packed), ptr(x_d), M, ptr(out), ptr(ws), ws.numel(), int(training),
-                                      int(bf16_flags), _events_arg(events), stream()), "nerf_mlp_fwd_bf16")
+    if precision in _H16:
+        fn = f"nerf_mlp_fwd_{_H16[precision]}"
+        check(getattr(lib(), fn)(ptr(w_packed), ptr(x_d), M, ptr(out), ptr(ws), ws.numel(), int(training),
+                                 int(bf16_flags), _events_arg(events), stream()), fn)
         return out
     check(lib().nerf_mlp_fwd_ex(ptr(w_packed), ptr(x_d), M, ptr(out), ptr(ws), ws.numel(), int(training),
                                 int(fp32_flags) & MLP_NATIVE_FP32,  # MLP_NATIVE_DGRAD is a backward-only flag
@@ -178,9 +182,10 @@ def mlp_bwd(w_packed, M, d_rgb_sigma, ws, d_w=None, accumulate=False, events=Non
     if d_w is None:
         d_w = torch.empty_like(w_packed)
         accumulate = False
-    if precision == "bf16":
-        check(lib().nerf_mlp_bwd_bf16(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws),
-                                      ws.numel(), int(bf16_flags), _events_arg(events), stream()), "nerf_mlp_bwd_bf16")
+    if precision in _H16:
+        fn = f"nerf_mlp_bwd_{_H16[precision]}"
+        check(getattr(lib(), fn)(ptr(w_packed), M, ptr(d_rgb_sigma), ptr(d_w), int(accumulate), ptr(ws),
+                                 ws.numel(), int(bf16_flags), _events_arg(events), stream()), fn)
         return d_w
     if wgrad_stream is not None:
         if sync is None or len(sync) < 10:

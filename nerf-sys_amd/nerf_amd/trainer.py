@@ -106,6 +106,9 @@ class NeRFTrainer:
         self.bg_policy = bg
         self.sigma_scale = sigma_scale
         self.world_size = world_size
+        # False only for the bench's exposed-exchange measurement (bench.py dp record): the step then skips the
+        # all-reduce, so each rank applies its own gradient — a timing device, never a training mode
+        self.exchange_enabled = True
         self.step_count = 0
         self._ws = {}
         self._bg = {}
@@ -267,15 +270,19 @@ class NeRFTrainer:
         return self.loss_buf
 
     def _exchange(self, buf, ev, bucket):
-        """SUM all-reduce of one bucket of the flat [grad_coarse | grad_fine | loss] buffer over RCCL, on the current
-        stream; with timing events, events["ar"][2 bucket], [2 bucket + 1] bracket it (includes the wait for the
-        slowest rank)."""
-        if self.world_size <= 1:
+        """SUM all-reduce of one bucket of the flat [grad_coarse | grad_fine | loss] buffer over RCCL, issued with
+        async_op=True and waited on the current (consuming) stream; with timing events, events["ar"][2 bucket] is
+        recorded before the issue and [2 bucket + 1] after work.wait() on the same stream, so the pair brackets the
+        collective as that stream sees it (RCCL: its stream waits for the RCCL kernel; gloo rehearsal: the host copy
+        round trip), including the wait for the slowest rank."""
+        if self.world_size <= 1 or not self.exchange_enabled:
             return
         cur = torch.cuda.current_stream(self.device)
         if ev:
             ev["ar"][2 * bucket].record(cur)
-        allreduce_flat(buf, self.world_size)
+        work = allreduce_flat(buf, self.world_size, async_op=True)
+        if work is not None:
+            work.wait()
         if ev:
             ev["ar"][2 * bucket + 1].record(cur)
             ev["ar_used"] = ev.get("ar_used", 0) | (1 << bucket)

@@ -106,14 +106,18 @@ class PackedLayout:
 
 
 def amp_precision() -> str:
-    """The MLP precision the caller's autocast region asks for: "bf16" inside ``torch.autocast("cuda")`` with a
-    16-bit dtype (the reference trains under ``torch.cuda.amp.autocast(dtype=torch.float16)`` + GradScaler,
-    pipelines/online_stage/runtime_adapt.py:290-310, configs/train.json "use_amp": true), else "fp32".  Both fp16
-    and bf16 autocast run the bf16 MFMA kernels (fp32 accumulation, fp32 weight gradients): bf16 keeps fp32's
-    exponent range, so a scaled loss never overflows inside the MLP and the GradScaler sees no inf from it.
-    Compositing, loss and sampling stay fp32 either way ("bf16 MLP with fp32 compositing", configs[2])."""
-    if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") in (torch.float16, torch.bfloat16):
-        return "bf16"
+    """The MLP precision the caller's autocast region asks for (else "fp32").  The reference trains under
+    ``torch.cuda.amp.autocast(dtype=torch.float16)`` + GradScaler (pipelines/online_stage/runtime_adapt.py:290-310,
+    configs/train.json "use_amp": true): autocast(float16) runs the fp16 build of the fused MLP kernels ("fp16": fp16
+    operands, the reference's rounding points — include/nerf_amd.h nerf_mlp_fwd_f16), autocast(bfloat16) the bf16
+    build ("bf16", configs[2]).  Compositing, loss and sampling stay fp32 either way: the reference's volume_render
+    receives the expert's fp32 outputs (the heads add fp32 biases, metamodule.py:153-155)."""
+    if torch.is_autocast_enabled("cuda"):
+        dt = torch.get_autocast_dtype("cuda")
+        if dt == torch.float16:
+            return "fp16"
+        if dt == torch.bfloat16:
+            return "bf16"
     return "fp32"
 
 

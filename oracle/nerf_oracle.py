@@ -397,7 +397,9 @@ class OracleTrainer:
     amp="fp16": the use_amp=True body (runtime_adapt.py:290-310) — the MLPs under the autocast(float16) restatement
     of _lin, the loss scaled by ``loss_scale`` for the backward and the gradients unscaled (GradScaler.unscale_
     multiplies by 1/scale) before the clip; a step whose gradients hold an inf / nan is skipped, as GradScaler.step
-    does (the returned loss is still the step's)."""
+    does (the returned loss is still the step's), and the scale follows GradScaler.update's defaults (torch.amp
+    GradScaler: backoff_factor 0.5 on a skipped step, growth_factor 2.0 after growth_interval 2000 clean steps in a
+    row), so multi-step oracle AMP runs keep the reference's scale trajectory."""
 
     def __init__(self, p_coarse, p_fine=None, lr_sigma=2e-3, lr_color=2e-3, betas=(0.9, 0.999),
                  eps=1e-8, grad_clip=1.0, color_space="linear", amp=None, loss_scale=65536.0):
@@ -415,6 +417,7 @@ class OracleTrainer:
         self.color_space = color_space
         self.amp = amp
         self.loss_scale = float(loss_scale) if amp else 1.0
+        self._growth_tracker = 0  # GradScaler's count of consecutive finite steps
 
     def step(self, rays, gt, S, n_importance=0, training=True, u_strat=None, u_pdf=None, bg="white"):
         self.opt.zero_grad()
@@ -436,4 +439,13 @@ class OracleTrainer:
             torch.nn.utils.clip_grad_norm_(self.params, self.grad_clip)
         if finite:
             self.opt.step()
+        if self.amp:  # GradScaler.update (torch/amp/grad_scaler.py defaults)
+            if not finite:
+                self.loss_scale *= 0.5
+                self._growth_tracker = 0
+            else:
+                self._growth_tracker += 1
+                if self._growth_tracker == 2000:
+                    self.loss_scale *= 2.0
+                    self._growth_tracker = 0
         return float(loss.detach())

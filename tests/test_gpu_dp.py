@@ -214,3 +214,31 @@ def test_flat_adam_world2(mode):
         # the rank mean (a + b) / 2 vs the full batch's (a + b) * 0.5 is exact; the clip norm's partial sums are
         # grouped differently under sharding: rounding-level differences only
         torch.testing.assert_close(res[0][step], full[step], rtol=2e-6, atol=2e-7)
+
+
+def test_bench_engine_run_world2_gloo():
+    """bench.py's own data-parallel path (engine_run at --gpus 2, two ranks sharing cuda:0 over gloo): the line's dp
+    record says the replicas stayed bitwise equal (an all-gathered fp64 sum + bit hash of every rank's parameters),
+    both all-reduce buckets were bracketed by events on their consuming streams, and the exposed-exchange leg ran."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_PORT=str(_free_port()), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--steps", "3",
+           "--warmup", "1", "--train-views", "4", "--no-psnr", "--no-cpu-baseline", "--no-llff", "--no-sweep",
+           "--no-dropin", "--no-other-precision", "--no-native-ref"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    out = json.loads(line)
+    dp = out["dp"]
+    print(json.dumps({k: dp[k] for k in dp if "note" not in k}))
+    assert out["n_gpus"] == 2 and dp["world_size"] == 2 and dp["world_size_checked"] == 2
+    assert dp["params_equal_across_ranks"] is True
+    assert len(set(dp["params_bit_hash_per_rank"])) == 1
+    for rank_times in dp["allreduce_ms_per_rank"]:
+        assert len(rank_times) == 2 and all(t > 0.0 for t in rank_times), dp["allreduce_ms_per_rank"]
+    assert "exposed_exchange_ms" in dp and dp["step_ms_no_exchange"] > 0

@@ -16,14 +16,16 @@ an/pipelines/online_stage/runtime_adapt.py:286-310 —
   reference's golden train step): loss to 1e-5, both nets' clipped gradients to 1e-4 of their scale, post-Adam
   parameters within the update difference the two measured gradients imply (test_gpu_parity._adam_step1_close);
   then two more steps' losses.
-* AMP (configs/train.json "use_amp": true): inside ``autocast(fp16)`` the expert runs the bf16 MLP kernels
-  (bitwise ``nerf_mlp_fwd_bf16``), compositing stays fp32; the loop body as written with ``GradScaler`` trains,
-  its loss tracks the fp32 loop's from the same seed, and the scaler never finds an inf (its scale stays put).
+* AMP (configs/train.json "use_amp": true): inside ``autocast(fp16)`` the expert runs the fp16 build of the fused MLP
+  kernels (bitwise ``nerf_mlp_fwd_f16``; ``autocast(bfloat16)`` the bf16 build), compositing stays fp32; the loop body
+  as written with ``GradScaler`` trains and its loss tracks the fp32 loop's from the same seed.
 * AMP parity: the reference under autocast(float16) keeps trunc_exp's input fp32 (MetaLinear's fp32 bias promotes
   the fp16 matmul output; tests/golden/amp.npz from the imported reference), so sigma is NOT clamped at fp16's 11.09
   — known answers beyond +-11.09 through the drop-in expert under autocast; and the drop-in AMP hierarchical step's
   first unscaled gradients against OracleTrainer(amp="fp16"), the CPU restatement of the reference's autocast
-  numerics pinned to that fixture (tests/test_oracle_golden.py::test_amp_*)."""
+  numerics pinned to that fixture (tests/test_oracle_golden.py::test_amp_*): per tensor within 1e-2 relative error
+  norm and flat cosine >= 0.9999 (the kernels keep the reference's fp16 rounding points; what differs is the fp32
+  summation order inside each product, which moves an fp16 rounding now and then)."""
 import types
 
 import pytest
@@ -86,26 +88,29 @@ def test_dropin_hierarchical_step_vs_oracle(K):
                     _adam_step1_close(p, ref, p.grad, ref.grad, lr, what=f"net{k} post-Adam {n}")
 
 
-def test_autocast_dispatches_bf16_kernels(K):
-    """Inside autocast(fp16 or bf16) VanillaNeRF.forward is bitwise the bf16 kernel; outside it, the fp32 one."""
+def test_autocast_dispatches_16bit_kernels(K):
+    """Inside autocast(float16) VanillaNeRF.forward is bitwise the fp16 kernel build, inside autocast(bfloat16) the
+    bf16 one; outside autocast the fp32 engine."""
     from nerf_amd.vanilla import VanillaNeRF, amp_precision
     net = VanillaNeRF().load_reference_state(O.init_vanilla_params(3)).to(DEV)
     g = torch.Generator().manual_seed(3)
     x = torch.cat([torch.rand(3000, 3, generator=g) * 3 - 1.5,
                    torch.nn.functional.normalize(torch.randn(3000, 3, generator=g), dim=-1)], -1).to(DEV)
     w = net.packed().detach()
-    ref = {p: K.mlp_fwd(w, x, K.mlp_workspace(3000, False, DEV, p), False, precision=p) for p in ("fp32", "bf16")}
+    ref = {p: K.mlp_fwd(w, x, K.mlp_workspace(3000, False, DEV, p), False, precision=p)
+           for p in ("fp32", "bf16", "fp16")}
     assert amp_precision() == "fp32"
+    assert not torch.equal(ref["bf16"], ref["fp16"])
     with torch.no_grad():
         assert torch.equal(net(x), ref["fp32"])
-        for dt in (torch.float16, torch.bfloat16):
+        for dt, p in ((torch.float16, "fp16"), (torch.bfloat16, "bf16")):
             with torch.autocast("cuda", dtype=dt):
-                assert amp_precision() == "bf16"
+                assert amp_precision() == p
                 out = net(x)
-            assert out.dtype == torch.float32 and torch.equal(out, ref["bf16"]), dt
+            assert out.dtype == torch.float32 and torch.equal(out, ref[p]), dt
     with torch.autocast("cuda", dtype=torch.float16):   # training forward (autograd Function) as well
         out = net(x)
-    assert out.requires_grad and torch.equal(out.detach(), ref["bf16"])
+    assert out.requires_grad and torch.equal(out.detach(), ref["fp16"])
 
 
 def test_reference_amp_loop_body_with_gradscaler(K):
@@ -140,19 +145,21 @@ def test_reference_amp_loop_body_with_gradscaler(K):
             scaler.update()
             ls.append(float(loss.detach()))
         if use_amp:
-            assert scaler.get_scale() == 65536.0, f"GradScaler found an inf/nan (scale {scaler.get_scale()})"
+            print(f"GradScaler scale after 40 AMP steps: {scaler.get_scale()}")
+            assert scaler.get_scale() >= 2.0 ** 12, f"GradScaler skipped many steps (scale {scaler.get_scale()})"
         curves[use_amp] = torch.tensor(ls)
     a, b = curves[True], curves[False]
     assert torch.isfinite(a).all()
     assert a[-10:].mean() < 0.8 * a[:5].mean(), a   # it learns
     assert (a[-10:].mean() - b[-10:].mean()).abs() <= 0.15 * b[-10:].mean(), (a[-10:].mean(), b[-10:].mean())
-    assert not torch.equal(a, b)  # the AMP loop did run the bf16 kernels
+    assert not torch.equal(a, b)  # the AMP loop did run the 16-bit kernels
 
 
 def test_amp_trunc_exp_beyond_fp16_clamp_golden(K):
     """te16_x = [-30, -12, 0, 11, 12, 15, 30] as the sigma head's pre-activation (weights 0, bias x) under
     autocast(float16): sigma equals the imported reference's (tests/golden/amp.npz) to 1e-5 — exp(x) without fp16's
-    11.09 clamp (sigma(15) = 3.27e6) — and d sigma / d bias to the bf16 rounding of the backward's d sigma_raw."""
+    11.09 clamp (sigma(15) = 3.27e6) — and so does d sigma / d bias (the bias gradient is an fp32 sum in the reference
+    and in the fp16 kernels: only the matmul operands are rounded)."""
     from nerf_amd.vanilla import VanillaNeRF
     from golden_io import mlp_params
     z = load("amp")
@@ -169,18 +176,16 @@ def test_amp_trunc_exp_beyond_fp16_clamp_golden(K):
         net.zero_grad()
         out[:, 3].sum().backward()
         gb = net.sigma_head.bias.grad.item() / 64.0
-        # the bf16 backward carries d sigma_raw as a bf16 value (8 significant bits): within 2^-8 of the reference's
-        # fp32 gradient — and exp(x) past +-11.09, not the clamp's exp(11.09)
-        assert abs(gb - gref) <= 2.0 ** -8 * gref, f"x={x}: d sigma / d bias {gb} vs reference {gref}"
+        # exp(x) past +-11.09, not the clamp's exp(11.09); summed in fp32 as the reference's bias gradient
+        assert abs(gb - gref) <= 1e-5 * gref, f"x={x}: d sigma / d bias {gb} vs reference {gref}"
 
 
 def test_amp_dropin_step_gradients_vs_oracle_amp(K):
     """runtime_adapt.py:290-305 with use_amp=True on the drop-in surface (HierarchicalNeRF, compute_mse_loss,
     GradScaler at its initial 2^16), 1024 golden rays x (64 + 128), injected jitter: the unscaled first-step
-    gradient of each net against OracleTrainer(amp="fp16") — the reference's autocast(float16) restatement — at
-    flat cosine >= 0.999 (the bar of the C3 engine test, test_gpu_convergence.py), the loss within 1e-3.  The
-    drop-in's MLP is bf16 (8-bit significands) where the reference's is fp16 (11-bit); both are printed against the
-    fp32 oracle too."""
+    gradient of each net against OracleTrainer(amp="fp16") — the reference's autocast(float16) restatement — per
+    tensor within 1e-2 relative error norm and at flat cosine >= 0.9999, the loss within 1e-4.  Both are printed
+    against the fp32 oracle too."""
     from nerf_amd.losses import compute_mse_loss
     pc, pf = O.init_vanilla_params(1), O.init_vanilla_params(2)
     model = _model(pc, pf).train()
@@ -203,7 +208,7 @@ def test_amp_dropin_step_gradients_vs_oracle_amp(K):
         ot.opt.step = lambda: None
         refs[amp] = (ot.step(rays, gt, 64, n_importance=128, training=True, u_strat=us, u_pdf=up), ot)
     lref = refs["fp16"][0]
-    assert abs(loss.item() - lref) <= 1e-3 * lref, (loss.item(), lref)
+    assert abs(loss.item() - lref) <= 1e-4 * lref, (loss.item(), lref)
     for k, net in enumerate((model.coarse, model.fine)):
         names = [n for n, _ in net.named_parameters()]
         a = torch.cat([q.grad.detach().double().cpu().flatten() for q in net.parameters()])
@@ -216,4 +221,11 @@ def test_amp_dropin_step_gradients_vs_oracle_amp(K):
         ref_vs_fp32 = float(b16 @ b32 / (b16.norm() * b32.norm()))
         print(f"net {k}: cos(drop-in AMP, reference AMP) {cos['fp16']:.6f}, cos(drop-in AMP, fp32) {cos[None]:.6f}, "
               f"cos(reference AMP, fp32) {ref_vs_fp32:.6f}")
-        assert cos["fp16"] >= 0.999, f"net {k}: cosine vs the reference's AMP gradient {cos['fp16']:.5f}"
+        assert cos["fp16"] >= 0.9999, f"net {k}: cosine vs the reference's AMP gradient {cos['fp16']:.6f}"
+        worst = (0.0, "")
+        for n, q in net.named_parameters():
+            r = refs["fp16"][1].nets[k][n].grad.double()
+            err = float((q.grad.detach().double().cpu() - r).norm() / r.norm().clamp_min(1e-30))
+            worst = max(worst, (err, n))
+            assert err <= 1e-2, f"net {k} {n}: relative error norm {err:.3e} vs the reference's AMP gradient"
+        print(f"net {k}: worst per-tensor relative error norm {worst[0]:.3e} ({worst[1]})")

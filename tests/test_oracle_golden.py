@@ -185,3 +185,19 @@ def test_amp_train_loss_and_scaled_gradients_golden():
         ref = z[f"sg/{n}"].double()
         rel = float((q.grad.double() - ref).norm() / (ref.norm() + 1e-30))
         assert rel <= 1e-3 and _cos(q.grad, ref) >= 0.99999, f"{n}: rel {rel:.2e}"
+
+
+def test_amp_oracle_gradscaler_update():
+    """OracleTrainer(amp="fp16") follows GradScaler.update: a step whose scaled gradients overflow is skipped (the
+    parameters stay put) and halves the scale; 2000 clean steps in a row double it (torch.amp.GradScaler defaults)."""
+    z = load("amp")
+    ot = O.OracleTrainer(mlp_params("w/"), amp="fp16", grad_clip=None, loss_scale=3.0e38)  # x 3e38 overflows
+    before = {n: q.detach().clone() for n, q in ot.nets[0].items()}
+    ot.step(z["step_rays"][:8], z["step_gt"][:8], 32, training=True, u_strat=z["step_u"][:8])
+    assert ot.loss_scale == 1.5e38
+    assert all(torch.equal(q.detach(), before[n]) for n, q in ot.nets[0].items())
+    ot2 = O.OracleTrainer(mlp_params("w/"), amp="fp16", grad_clip=None)
+    ot2._growth_tracker = 1999
+    ot2.opt.step = lambda: None
+    ot2.step(z["step_rays"][:8], z["step_gt"][:8], 32, training=True, u_strat=z["step_u"][:8])
+    assert ot2.loss_scale == 131072.0 and ot2._growth_tracker == 0

@@ -155,16 +155,11 @@ def build_step(a, dev, rank=0, world=1):
     return one, model
 
 
-def main():
-    a = parse()
+def run(a, dev, rank=0, world=1):
+    """The container train-step bench on ``dev`` (process group already initialised when world > 1); returns the
+    record (bench.py's ``container`` sub-record).  ``a`` carries steps, warmup, batch, train_views, cpu_seconds,
+    no_cpu_baseline, shard, no_bucket."""
     import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local % torch.cuda.device_count())  # a gloo rehearsal may run more ranks than GPUs
-    torch.cuda.set_device(dev)
-    if world > 1:
-        dist.init_process_group(a.backend, device_id=dev if a.backend == "nccl" else None)
     from nerf_amd import ngp as G
 
     one, model = build_step(a, dev, rank, world)
@@ -248,6 +243,20 @@ def main():
     if exch:
         out["exchange"] = exch
     out["cpu_baseline"] = None if (a.no_cpu_baseline or world > 1) else cpu_baseline(a.cpu_seconds)
+    return out
+
+
+def main():
+    a = parse()
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local % torch.cuda.device_count())  # a gloo rehearsal may run more ranks than GPUs
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group(a.backend, device_id=dev if a.backend == "nccl" else None)
+    out = run(a, dev, rank, world)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -87,10 +87,9 @@ def cpu_baseline(seconds, S):
             "sample": f"{steps} oracle NGP train steps x {n} rays ({S} samples, fp32) in {el:.1f}s"}
 
 
-def main():
-    a = parse()
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
+def run(a, dev):
+    """The NGP train-step bench on device ``dev``; returns the record (bench.py's ``ngp`` sub-record).  ``a`` carries
+    steps, warmup, batch, samples, train_views, cpu_seconds, no_cpu_baseline."""
     from nerf_amd.ngp import InstantNGP
     from nerf_amd.ngp_trainer import NGPTrainer
     from nerf_amd.scene import make_blender_scene
@@ -172,7 +171,14 @@ def main():
         "final_loss": round(float(loss.item()), 6),
     }
     out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(a.cpu_seconds, a.samples)
-    print(json.dumps(out), flush=True)
+    return out
+
+
+def main():
+    a = parse()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    print(json.dumps(run(a, dev)), flush=True)
 
 
 if __name__ == "__main__":

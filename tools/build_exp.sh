@@ -17,6 +17,7 @@ for f in $SRC/*.hip; do
   { [ $b = adam ] || [ $b = mlp ]; } && X="$2"
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $X -c $f -o /tmp/exp_$1/$b.o &
 done
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mllvm -disable-promote-alloca-to-lds -DNERF_F16=1 $2 -c $SRC/mlp_bf16.hip -o /tmp/exp_$1/mlp_f16.o &
 for j in $(jobs -p); do wait $j; done
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 /tmp/exp_$1/*.o -o ../exp/$1.so
 echo built exp/$1.so

@@ -16,6 +16,7 @@ Prints one JSON line per scene and a summary: mean PSNR, aggregate rays/s (sum o
 training throughput), and the aggregate MFMA-roofline fraction (FLOP/ray of SURVEY §8d).
 """
 import argparse
+import faulthandler
 import json
 import os
 import sys
@@ -26,6 +27,9 @@ sys.path.insert(0, os.path.join(ROOT, "nerf-sys_amd"))
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
+
+# a native fault (HIP runtime, profiler, ctypes) prints every thread's Python stack instead of a bare address list
+faulthandler.enable(all_threads=True)
 
 FLOP_PER_RAY = 769327104
 PEAK = {"fp32": 157.3e12, "bf16": 2500e12}
