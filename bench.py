@@ -247,8 +247,8 @@ def dropin_run(rb, dev, a, world, rank, n_local, precision="fp32"):
     fine VanillaNeRF, autograd through the HIP MLP / compositing / sampling ops) -> compute_mse_loss (coarse +
     fine terms) -> backward -> clip_grad_norm_(1.0) -> torch.optim.Adam ('sigma' / 'color' groups).  precision
     "bf16" runs it as the reference's use_amp=True body (configs/train.json): autocast(fp16) around the loss ->
-    GradScaler scale / unscale_ / step / update; the expert then dispatches to the bf16 MLP kernels
-    (vanilla.amp_precision).  Adam is torch's fused implementation (no host sync inside GradScaler.step; foreach
+    GradScaler scale / unscale_ / step / update; the expert then dispatches to the fp16 build of the fused MLP kernels
+    (vanilla.amp_precision), beside the bf16 C3 engine.  Adam is torch's fused implementation (no host sync inside GradScaler.step; foreach
     if this torch build lacks it).  The ray batch comes from images resident in HBM (the reference's DataLoader +
     .to(device) is not timed)."""
     from types import SimpleNamespace
@@ -291,7 +291,8 @@ def dropin_run(rb, dev, a, world, rank, n_local, precision="fp32"):
            "path": "render_rays + HierarchicalNeRF(VanillaNeRF x2) autograd + compute_mse_loss + "
                    "clip_grad_norm_ + " + kind + " (runtime_adapt.py:286-310)"}
     if use_amp:
-        rec["amp"] = ("torch.autocast(fp16) -> bf16 MLP kernels + fp32 compositing; GradScaler scale "
+        rec["amp"] = ("torch.autocast(fp16) -> the fp16 build of the fused MLP kernels (the reference's autocast "
+                      "rounding points) + fp32 compositing; GradScaler scale "
                       f"{scaler.get_scale():.0f} after {a.warmup + a.steps} steps (halves on any inf)")
     return rec
 

@@ -329,6 +329,9 @@ __device__ unsigned long long nerf_x6_stamps[2][8][128];
 #ifndef NERF_X6W_PAIRB
 #define NERF_X6W_PAIRB 0
 #endif
+#ifndef NERF_X6W_PAIRB3
+#define NERF_X6W_PAIRB3 0
+#endif
 constexpr bool defined_regb() {
 #ifdef NERF_X6W_REGB
   return true;
@@ -368,7 +371,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   // (s_memtime stamps, round 4: ~1.9k of a 9.55k-cycle forward slab), and a barrier every other slab pays that wait
   // once per two slabs.  The two-set, non-A3 loop only.
   constexpr bool PB = NERF_X6W_PAIRB && !(NKC > 0) && !defined_regb();
-  constexpr int NBUF = PB ? 4 : 2;
+  // the same for the three-set (A3) input-gradient loop: pairs of the fully unrolled slab sequence
+  constexpr bool PB3 = NERF_X6W_PAIRB3 && (NKC > 0) && !defined_regb();
+  constexpr int NBUF = (PB || PB3) ? 4 : 2;
   __shared__ __attribute__((aligned(16))) nerf_bf16 smem[NBUF * 3 * PL];
   static_assert(NW * X6E_WAVE_FLOATS * 4 <= 2 * 3 * PL * 2, "epilogue tiles fit in the weight images");
 
@@ -505,7 +510,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   {
     const int j = 0;
     X6W_BLOAD(0, 0);
-    if constexpr (PB) X6W_BLOAD(BK, 1);  // host: K % (2 BK) == 0, so slab 1 exists
+    if constexpr (PB || PB3) {  // host: K % (2 BK) == 0, so slab 1 exists
+      X6W_BLOAD(BK, 1);
+    }
     if constexpr (ASML) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   X6W_BSTORE(0);
@@ -562,7 +569,40 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
         }
   };
   X6W_STAMP();
-  if constexpr (A3) {
+  if constexpr (PB3) {
+    static_assert(NKC % 2 == 0, "slab pairs");
+    // pair (kt0, kt0 + 1) in buffers b0, b0 + 1: the next pair's DMAs and slab kt0 + 2's activations go out at the
+    // pair's start (after the touch of set kt0 % 3), slab kt0 + 3's after slab kt0 (into the set it freed); one
+    // barrier per pair, which the next pair's DMAs wait on (vmcnt(8): the 8 activation loads issued after them stay
+    // in flight); the last pair loads nothing and drains
+#pragma unroll
+    for (int p = 0; p < NKC / 2; ++p) {
+      const int kt0 = 2 * p, b0 = kt0 & 3;
+      const bool more = kt0 + 2 < NKC;  // compile time (unrolled)
+      {
+        const int j = kt0 % 3;
+        if (more) {
+          X6W_BLOAD((kt0 + 2) * BK, b0 ^ 2);
+          X6W_BLOAD((kt0 + 3) * BK, (b0 ^ 2) + 1);
+        }
+      }
+      if (more) X6W_ALOAD((kt0 + 2) % 3, (kt0 + 2) * BK);
+      asm volatile("" ::: "memory");
+      slab_mfma(ra[kt0 % 3], smem + b0 * 3 * PL, [] {});
+      if (more) X6W_ALOAD((kt0 + 3) % 3, (kt0 + 3) * BK);
+      asm volatile("" ::: "memory");
+      slab_mfma(ra[(kt0 + 1) % 3], smem + (b0 + 1) * 3 * PL, [] {});
+      if (more) {
+        if constexpr (TM * KS * 2 == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      X6W_STAMP();
+      __syncthreads();
+      X6W_STAMP();
+    }
+  } else if constexpr (A3) {
 #pragma unroll
     for (int kt = 0; kt < NKC; ++kt) {
       const int j = kt % 3;

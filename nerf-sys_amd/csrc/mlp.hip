@@ -269,6 +269,17 @@ int nt_x6(const float* A, int lda, const nerf_bf16* Bp, int ldb, int64_t bplane,
       return NERF_OK;
     }
   }
+#ifndef NERF_X6_K64_NW  // trunk.0 (K = 64: two slabs, the tile's 256 KiB of stores dominate): waves per workgroup
+#define NERF_X6_K64_NW 8
+#endif
+  if constexpr (NERF_X6_K64_NW != NERF_X6W_NW) {
+    if (K == 64 && EPI == EPI_BIAS_RELU && M % (64 * NERF_X6_K64_NW) == 0) {
+      gemm_nt_x6w_kernel<EPI, NERF_X6W_BK, NERF_X6_K64_NW><<<(unsigned)((M / (64 * NERF_X6_K64_NW)) * ntn),
+                                                             64 * NERF_X6_K64_NW, 0, st>>>(
+          A, lda, Bp, ldb, bplane, bias, C, ldc, mbits, N / 32, mbits_out, K, ntn);
+      return NERF_OK;
+    }
+  }
   if (M % (64 * NERF_X6W_NW) == 0 && K % (2 * NERF_X6W_BK) == 0) {
     gemm_nt_x6w_kernel<EPI, NERF_X6W_BK, NERF_X6W_NW><<<(unsigned)((M / (64 * NERF_X6W_NW)) * ntn), 64 * NERF_X6W_NW, 0,
                                                         st>>>(A, lda, Bp, ldb, bplane, bias, C, ldc, mbits, N / 32,

@@ -55,7 +55,11 @@ def _worker(rank, world, port, q):
     n_local = rays.shape[0] // world
     sl = slice(rank * n_local, (rank + 1) * n_local)
     buf = _flat_grad(O.init_vanilla_params(3), rays[sl], gt[sl], us[sl], inv_count(n_local, world))
+    buf_async = buf.clone()
     allreduce_flat(buf, world)
+    work = allreduce_flat(buf_async, world, async_op=True)  # the trainer's form: issue, then wait where consumed
+    work.wait()
+    assert torch.equal(buf, buf_async)
     seeds = [shard_seed(s, rank, world) for s in range(5)]
     if rank == 0:
         q.put((buf.numpy(), seeds))  # numpy: pickled by value (a tensor's shared-memory handle dies with the worker)

@@ -8,7 +8,7 @@ timeout -k 10 500 python -u -m pytest tests/test_gpu_fp16.py tests/test_gpu_drop
   -m gpu -v -s --timeout 200 --timeout-method thread > $O/pytest_c2.log 2>&1; rc=$?
 grep -E "passed|failed|PASS|FAIL|Error|cosine|relative|rgb|GradScaler" $O/pytest_c2.log | tail -60
 [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit 1
-BENCH_EXTRA="--no-llff --no-sweep" VARIANTS="base new pb" ROUNDS=2 bash tools/ab_x6.sh > $O/ab_epi_fence2.txt 2>&1 || { tail -20 $O/ab_epi_fence2.txt; exit 1; }
+BENCH_EXTRA="--no-llff --no-sweep" VARIANTS="base new pb pb3 k64nw4 sr2048" ROUNDS=2 bash tools/ab_x6.sh > $O/ab_epi_fence2.txt 2>&1 || { tail -20 $O/ab_epi_fence2.txt; exit 1; }
 cat $O/ab_epi_fence2.txt
 [ -n "$NO_REPRO" ] && exit 0
 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE \
