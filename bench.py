@@ -471,10 +471,18 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_
     el = el_local
     dp = None
     if world > 1:
-        ar = tm.get("allreduce") or []
-        nb = max((len(x) for x in ar), default=0)
-        ar_mean = [sum(x[b] for x in ar if len(x) > b) / max(1, len(ar)) for b in range(2)] if nb else [0.0, 0.0]
-        mine = torch.tensor([el_local] + ar_mean, dtype=torch.float64, device=dev)
+        # the exchange as it runs in production: a.timing_steps more steps with the side stream on and events around the
+        # two buckets only (bucket 0 = coarse gradient on the side stream, bucket 1 = fine gradient + loss); the kernel
+        # pass above ran without the side stream, i.e. with ONE all-reduce of the whole buffer (reported beside it)
+        single = [x[0] for x in (tm.get("allreduce") or []) if x]
+        tr.enable_exchange_timing(n_ev)
+        for s in range(a.warmup + a.steps + n_ev, a.warmup + a.steps + 2 * n_ev):
+            one(s)
+        torch.cuda.synchronize()
+        ex = tr.collect_exchange_timing()
+        ar_mean = [sum(x[b] for x in ex if x[b] is not None) / max(1, sum(x[b] is not None for x in ex)) for b in range(2)]
+        single_mean = sum(single) / len(single) if single else 0.0
+        mine = torch.tensor([el_local] + ar_mean + [single_mean], dtype=torch.float64, device=dev)
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         rows = [x.tolist() for x in allr]
@@ -482,11 +490,14 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_
         dp = {"world_size": dist.get_world_size(), "backend": "nccl (RCCL)" if nccl else "gloo (rehearsal)",
               "step_ms_max": round(el / a.steps * 1e3, 3), "step_ms_min": round(min(r[0] for r in rows) / a.steps * 1e3, 3),
               "allreduce_ms_per_rank": [[round(r[1], 4), round(r[2], 4)] for r in rows],
+              "allreduce_single_bucket_ms_per_rank": [round(r[3], 4) for r in rows],
               "allreduce_note": "HIP events on the consuming stream around each bucket's all_reduce (issued "
-                                "async_op=True, end event after work.wait() on that stream; bucket 1 = coarse net "
-                                "gradient, issued on the side stream right after the coarse backward; bucket 2 = "
-                                "fine gradient + loss, after the fine backward), mean over the event steps; includes "
-                                "the wait for the slowest rank",
+                                "async_op=True, end event after work.wait() on that stream), in timing_steps extra "
+                                "production-form steps: [bucket 1 = coarse net gradient, issued on the side stream right "
+                                "after the coarse backward; bucket 2 = fine gradient + loss, after the fine backward], "
+                                "mean over the steps, including the wait for the slowest rank; "
+                                "allreduce_single_bucket_ms_per_rank: the kernel-timing pass (no side stream), one "
+                                "all-reduce of the whole buffer",
               "bytes_per_step": int(tr.gbuf.numel() * 4)}
         dp.update(params_checksum(tr.params, world))
         dp.update(exposed_exchange(a, tr, one, dev, world, barrier, el / a.steps * 1e3))

@@ -99,7 +99,9 @@ int64_t nerf_mlp_layout(int64_t* table);
 int64_t nerf_mlp_workspace_bytes(int64_t M, int training);
 
 /* expert(x_d (M,6), params) -> (M,4) [sigmoid rgb, trunc_exp sigma]  (meta_vanilla.py:123-154,
- * metamodule.py:140-156, trunc_exp.py:43-61).  w: packed weights.  ws: workspace (16B aligned). */
+ * metamodule.py:140-156, trunc_exp.py:43-61).  w: packed weights.  ws: workspace (16B aligned).
+ * M = 0 is an empty call: x_d / rgb_sigma (and the backward's d_rgb_sigma) may be null; the backward then zero-fills
+ * d_w (accumulate = 0) or leaves it untouched.  The same holds for the _bf16 / _f16 entry points. */
 int nerf_mlp_fwd(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws, int64_t ws_bytes,
                  int training, hipEvent_t* events, hipStream_t stream);
 

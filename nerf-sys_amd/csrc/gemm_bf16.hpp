@@ -37,18 +37,30 @@
 
 namespace NERF_H16NS {
 
+// nerf_bf16: the scalar element (memory arrays, conversions).  nerf_bf16x8: eight 16-bit elements as a REGISTER
+// CONTAINER, the bf16 vector type in both builds — the fp16 build reinterprets it only inside h16_mfma and the element
+// accessors below.  (As a half vector, hipcc treated the fragments as packed-fp16 values and the fused layer backward
+// spilled 70 VGPRs where the bf16 build spills none.)
 #if NERF_F16
 typedef _Float16 nerf_bf16;
-typedef _Float16 nerf_bf16x8 __attribute__((ext_vector_type(8)));
 #else
 typedef __bf16 nerf_bf16;
-typedef __bf16 nerf_bf16x8 __attribute__((ext_vector_type(8)));
 #endif
+typedef __bf16 nerf_bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 nerf_f16x8 __attribute__((ext_vector_type(8)));
 typedef short nerf_s16x4 __attribute__((ext_vector_type(4)));
 
+#if NERF_F16
+typedef float nerf_f32x2h __attribute__((ext_vector_type(2)));
+typedef _Float16 nerf_f16x2 __attribute__((ext_vector_type(2)));
+#endif
 __device__ __forceinline__ uint32_t nerf_pack_bf16x2(float a, float b) {
-  const nerf_bf16 x = (nerf_bf16)a, y = (nerf_bf16)b;  // round to nearest even (v_cvt_pk_bf16_f32 / v_cvt_f16_f32)
+#if NERF_F16  // one v_cvt_pk_f16_f32 (round to nearest even); the scalar casts became two converts and a repack
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(nerf_f32x2h{a, b}, nerf_f16x2));
+#else
+  const nerf_bf16 x = (nerf_bf16)a, y = (nerf_bf16)b;  // v_cvt_pk_bf16_f32, round to nearest even
   return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+#endif
 }
 // sin / cos of the frequency encoding for the bf16 path, whose encoding is rounded to bf16 (8-bit mantissa): the
 // argument is reduced to [-1/2, 1/2] revolutions and fed to v_sin_f32 / v_cos_f32 (absolute error ~ |x| 6e-8 rad from
@@ -84,11 +96,21 @@ __device__ __forceinline__ float nerf_bf16_hi(uint32_t u) {
 // 32x32x16 MFMA of the build's element (fp32 accumulation): v_mfma_f32_32x32x16_bf16 / v_mfma_f32_32x32x16_f16
 __device__ __forceinline__ nerf_f32x16 h16_mfma(nerf_bf16x8 a, nerf_bf16x8 b, nerf_f32x16 c) {
 #if NERF_F16
-  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(nerf_f16x8, a), __builtin_bit_cast(nerf_f16x8, b), c,
+                                                0, 0, 0);
 #else
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 #endif
 }
+// element j of a container as fp32 / element j := round(x) (the build's element type); macros, so the bf16 build's
+// expressions are the round-4 ones token for token (same ISA)
+#if NERF_F16
+#define H16_GET(v, j) ((float)__builtin_bit_cast(nerf_bf16, (v)[j]))
+#define H16_SET(v, j, x) ((v)[j] = __builtin_bit_cast(__bf16, (nerf_bf16)(x)))
+#else
+#define H16_GET(v, j) ((float)(v)[j])
+#define H16_SET(v, j, x) ((v)[j] = (nerf_bf16)(x))
+#endif
 // The layer output before its bias.  fp16 build: the reference's autocast matmul returns an fp16 tensor and the fp32
 // bias is added after it (metamodule.py:153-155: fp16 + fp32 promotes to fp32), so the accumulator is rounded to fp16
 // first and the bias added in fp32 (the accumulators start at zero, not at the bias).  bf16 build (the C3 engine's own
@@ -761,7 +783,7 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_bf16_kernel(const nerf_bf16
       for (int a = 0; a < TM; ++a) {
         if (do_bias) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) bsum[a] += (float)af[a][j];
+          for (int j = 0; j < 8; ++j) bsum[a] += H16_GET(af[a], j);
         }
 #pragma unroll
         for (int b = 0; b < TN; ++b) acc[a][b] = h16_mfma(af[a], bf[b], acc[a][b]);

@@ -352,7 +352,7 @@ extern "C" int64_t nerf_mlp_workspace_bytes(int64_t M, int training) {
 
 extern "C" int nerf_mlp_fwd_ex(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws,
                                int64_t ws_bytes, int training, int flags, hipEvent_t* ev, hipStream_t st) {
-  NERF_CHECK_ARG(w && x_d && rgb_sigma && ws && M >= 0);
+  NERF_CHECK_ARG(w && ws && M >= 0 && (M == 0 || (x_d && rgb_sigma)));  // an empty batch may pass null rows
   if (flags & ~NERF_MLP_NATIVE_FP32) return NERF_E_ENUM;
   const bool native = flags & NERF_MLP_NATIVE_FP32;
   if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(rgb_sigma)) return NERF_E_ALIGN;
@@ -434,7 +434,7 @@ namespace {
 // one-stream result.
 int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate, void* ws,
                  int64_t ws_bytes, int flags, hipEvent_t* ev, hipStream_t st, hipStream_t stw, hipEvent_t* sync) {
-  NERF_CHECK_ARG(w && d_rgb_sigma && d_w && ws && M >= 0);
+  NERF_CHECK_ARG(w && d_w && ws && M >= 0 && (M == 0 || d_rgb_sigma));
   NERF_CHECK_ARG(!stw || sync);
   if (flags & ~(NERF_MLP_NATIVE_FP32 | NERF_MLP_NATIVE_DGRAD)) return NERF_E_ENUM;
   const bool native = flags & NERF_MLP_NATIVE_FP32;

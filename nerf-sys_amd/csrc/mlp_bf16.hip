@@ -547,7 +547,7 @@ extern "C" int64_t NERF_H16_FN(nerf_mlp_workspace_bytes)(int64_t M, int training
 
 extern "C" int NERF_H16_FN(nerf_mlp_fwd)(const float* w, const float* x_d, int64_t M, float* rgb_sigma, void* ws,
                                  int64_t ws_bytes, int training, int flags, hipEvent_t* ev, hipStream_t st) {
-  NERF_CHECK_ARG(w && x_d && rgb_sigma && ws && M >= 0);
+  NERF_CHECK_ARG(w && ws && M >= 0 && (M == 0 || (x_d && rgb_sigma)));  // an empty batch may pass null rows
   if (flags & ~(NERF_F16 ? 0 : (NERF_BF16_LAYERED_FWD | NERF_BF16_LAYERED_BWD))) return NERF_E_ENUM;
   if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(rgb_sigma)) return NERF_E_ALIGN;
   const WSB W = carve_b(ws, M, training);
@@ -586,7 +586,7 @@ extern "C" int NERF_H16_FN(nerf_mlp_fwd)(const float* w, const float* x_d, int64
 
 extern "C" int NERF_H16_FN(nerf_mlp_bwd)(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w, int accumulate,
                                  void* ws, int64_t ws_bytes, int flags, hipEvent_t* ev, hipStream_t st) {
-  NERF_CHECK_ARG(w && d_rgb_sigma && d_w && ws && M >= 0);
+  NERF_CHECK_ARG(w && d_w && ws && M >= 0 && (M == 0 || d_rgb_sigma));
   if (flags & ~(NERF_F16 ? 0 : (NERF_BF16_LAYERED_FWD | NERF_BF16_LAYERED_BWD))) return NERF_E_ENUM;
   if (!nerf_aligned16(w) || !nerf_aligned16(ws) || !nerf_aligned16(d_w) || !nerf_aligned16(d_rgb_sigma))
     return NERF_E_ALIGN;

@@ -348,8 +348,17 @@ __device__ __forceinline__ void bias_acc(const IoSet& R, float (&bs)[8]) {
     const io_u32x4 v = const_cast<IoSet&>(R).template at<i>();
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
+#if NERF_F16
+      // fp16 build: v_dot2_f32_f16 with (1, 0) / (0, 1) adds one half to the fp32 sum in one instruction (exact product,
+      // one rounding).  Converting with v_cvt_f32_f16 first made hipcc spill 70 VGPRs of the io register sets.
+      typedef _Float16 h2_ __attribute__((ext_vector_type(2)));
+      const h2_ x = __builtin_bit_cast(h2_, v[d]);
+      bs[2 * d] = __builtin_amdgcn_fdot2(x, h2_{(_Float16)1.0f, (_Float16)0.0f}, bs[2 * d], false);
+      bs[2 * d + 1] = __builtin_amdgcn_fdot2(x, h2_{(_Float16)0.0f, (_Float16)1.0f}, bs[2 * d + 1], false);
+#else
       bs[2 * d] += nerf_bf16_lo(v[d]);
       bs[2 * d + 1] += nerf_bf16_hi(v[d]);
+#endif
     }
   });
 }

@@ -76,16 +76,17 @@ __global__ void frag_pack_kernel(const float* __restrict__ w, nerf_bf16* __restr
 // xyz PE (models/encodings.py:437-444, L = 10, include_input) -> X3E cols 256..319 (bf16) and the colour-input
 // prefill CIN[m] = [0 x 15, d, dir PE (L = 4), 0 ...] (meta_vanilla.py:109-121; the fused kernel fills the
 // 15 geo columns).  Rows M..Mp-1 are zero.
-__global__ void pe_prefill_bf16_kernel(const float* __restrict__ xd, int64_t M, int64_t Mp, nerf_bf16* __restrict__ X3E,
+__global__ __launch_bounds__(256) void pe_prefill_bf16_kernel(const float* __restrict__ xd, int64_t M, int64_t Mp, nerf_bf16* __restrict__ X3E,
                                        nerf_bf16* __restrict__ CIN) {
   const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= Mp) return;
-  float v[64], c[64];
+  // two phases (xyz encoding, then the colour-input prefill), each packed and stored before the next: one 64-value
+  // array live at a time (the fp16 build's libm sincosf spilled 60 VGPRs with both arrays live)
+  float v[64];
 #pragma unroll
-  for (int i = 0; i < 64; ++i) v[i] = c[i] = 0.f;
+  for (int i = 0; i < 64; ++i) v[i] = 0.f;
   if (m < M) {
     const float x[3] = {xd[m * 6], xd[m * 6 + 1], xd[m * 6 + 2]};
-    const float d[3] = {xd[m * 6 + 3], xd[m * 6 + 4], xd[m * 6 + 5]};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       v[k] = x[k];
@@ -98,27 +99,36 @@ __global__ void pe_prefill_bf16_kernel(const float* __restrict__ xd, int64_t M, 
         v[3 + k * 20 + 10 + l] = s;
         band *= 2.0f;
       }
-      c[15 + k] = d[k];
-      band = 1.0f;
+    }
+  }
+  uint4* q = reinterpret_cast<uint4*>(X3E + m * 320 + 256);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    q[i] = make_uint4(nerf_pack_bf16x2(v[8 * i], v[8 * i + 1]), nerf_pack_bf16x2(v[8 * i + 2], v[8 * i + 3]),
+                      nerf_pack_bf16x2(v[8 * i + 4], v[8 * i + 5]), nerf_pack_bf16x2(v[8 * i + 6], v[8 * i + 7]));
+#pragma unroll
+  for (int i = 0; i < 64; ++i) v[i] = 0.f;
+  if (m < M) {
+    const float d[3] = {xd[m * 6 + 3], xd[m * 6 + 4], xd[m * 6 + 5]};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      v[15 + k] = d[k];
+      float band = 1.0f;
 #pragma unroll
       for (int l = 0; l < 4; ++l) {
         float s, cs;
         pe_sincos_bf16(d[k] * band, &s, &cs);
-        c[18 + k * 8 + l] = cs;
-        c[18 + k * 8 + 4 + l] = s;
+        v[18 + k * 8 + l] = cs;
+        v[18 + k * 8 + 4 + l] = s;
         band *= 2.0f;
       }
     }
   }
-  uint4* q = reinterpret_cast<uint4*>(X3E + m * 320 + 256);
   uint4* r = reinterpret_cast<uint4*>(CIN + m * 64);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    q[i] = make_uint4(nerf_pack_bf16x2(v[8 * i], v[8 * i + 1]), nerf_pack_bf16x2(v[8 * i + 2], v[8 * i + 3]),
+  for (int i = 0; i < 8; ++i)
+    r[i] = make_uint4(nerf_pack_bf16x2(v[8 * i], v[8 * i + 1]), nerf_pack_bf16x2(v[8 * i + 2], v[8 * i + 3]),
                       nerf_pack_bf16x2(v[8 * i + 4], v[8 * i + 5]), nerf_pack_bf16x2(v[8 * i + 6], v[8 * i + 7]));
-    r[i] = make_uint4(nerf_pack_bf16x2(c[8 * i], c[8 * i + 1]), nerf_pack_bf16x2(c[8 * i + 2], c[8 * i + 3]),
-                      nerf_pack_bf16x2(c[8 * i + 4], c[8 * i + 5]), nerf_pack_bf16x2(c[8 * i + 6], c[8 * i + 7]));
-  }
 }
 
 struct FusedArgs {

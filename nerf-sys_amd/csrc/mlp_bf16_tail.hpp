@@ -80,7 +80,7 @@ __device__ __forceinline__ nerf_bf16x8 ld16(const char* p) { return *reinterpret
 __device__ __forceinline__ nerf_bf16x8 wfrag(const float* src, int ld_k, int ld_i, int i0, int ks, int lane) {
   nerf_bf16x8 v;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (nerf_bf16)src[(int64_t)(16 * ks + 8 * (lane >> 5) + j) * ld_k + (int64_t)(i0 + (lane & 31)) * ld_i];
+  for (int j = 0; j < 8; ++j) H16_SET(v, j, src[(int64_t)(16 * ks + 8 * (lane >> 5) + j) * ld_k + (int64_t)(i0 + (lane & 31)) * ld_i]);
   return v;
 }
 
@@ -117,7 +117,7 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
     wh[ks] = wfrag(W + A.off16, 256, 1, 32 * w, ks, lane);        // A[i = Y7 col][kk = dO16 col] = Wh[kk][i]
   }
   if constexpr (NERF_F16)  // geo only: the sigma row (kk = 0: k-step 0, lane half 0, element 0) is added apart
-    if (lh == 0) wh[0][0] = (nerf_bf16)0.f;
+    if (lh == 0) H16_SET(wh[0], 0, 0.f);
   nerf_f32x16 ac1, ac0, ahd;  // dWc1 (waves 0-3: k-block w), dWc0 (n-block w >> 1, k-block w & 1), dWh (k-block w)
 #pragma unroll
   for (int r = 0; r < 16; ++r) ac1[r] = ac0[r] = ahd[r] = 0.f;
@@ -190,7 +190,7 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
       for (int ks = 0; ks < 4; ++ks) {
         if (w == 0) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) b1 += (float)ga[ks][j];
+          for (int j = 0; j < 8; ++j) b1 += H16_GET(ga[ks], j);
         }
         ac1 = h16_mfma(ga[ks], gb[ks], ac1);
       }
@@ -229,7 +229,7 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
       for (int ks = 0; ks < 4; ++ks) {
         if ((w & 1) == 0) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) b0 += (float)ga[ks][j];
+          for (int j = 0; j < 8; ++j) b0 += H16_GET(ga[ks], j);
         }
         ac0 = h16_mfma(ga[ks], gb[ks], ac0);
       }
@@ -286,7 +286,7 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
       for (int ks = 0; ks < 4; ++ks) {
         if (w == 0) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) bh += (float)ga[ks][j];
+          for (int j = 0; j < 8; ++j) bh += H16_GET(ga[ks], j);
         }
         ahd = h16_mfma(ga[ks], gb[ks], ahd);
       }
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(768, 3) void bwd_tail_bf16_kernel(TailArgs A) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int kk = 16 * ks + 8 * (l >> 5) + j;
-      v[j] = (col >= 1 && col <= 15) ? (nerf_bf16)A.w[A.off18 + (int64_t)kk * 64 + col - 1] : (nerf_bf16)0.f;
+      H16_SET(v, j, (col >= 1 && col <= 15) ? A.w[A.off18 + (int64_t)kk * 64 + col - 1] : 0.f);
     }
     *reinterpret_cast<nerf_bf16x8*>(lds + WC0_OFF + ks * 1024 + 16 * l) = v;
   }

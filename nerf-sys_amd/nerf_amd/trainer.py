@@ -178,6 +178,28 @@ class NeRFTrainer:
         torch.cuda.synchronize()
         self.timing = {"pool": sets, "used": [], "M": None, "skip": int(skip)}
 
+    def enable_exchange_timing(self, n_steps: int):
+        """HIP events around the all-reduce buckets only (no GEMM events), for n_steps steps run as in production
+        (the coarse backward and its bucket on the side stream): collect_exchange_timing() then gives each step's
+        bucket times.  The kernel-timing pass (enable_timing) runs without the side stream, so its steps have ONE
+        exchange of the whole buffer."""
+        mk = lambda k: [torch.cuda.Event(enable_timing=True) for _ in range(k)]
+        sets = [{"fwd": None, "bwd": None, "ar": mk(4)} for _ in range(max(0, n_steps))]
+        for st in sets:
+            for e in st["ar"]:
+                e.record()
+        torch.cuda.synchronize()
+        self.timing = {"pool": sets, "used": [], "M": None, "skip": 0} if sets else None
+
+    def collect_exchange_timing(self):
+        """[[bucket-0 ms or None, bucket-1 ms or None] per step] of the enable_exchange_timing steps."""
+        out = []
+        for ev in self.timing["used"]:
+            used = ev.get("ar_used", 0)
+            out.append([ev["ar"][2 * b].elapsed_time(ev["ar"][2 * b + 1]) if used >> b & 1 else None for b in range(2)])
+        self.timing = None
+        return out
+
     def _next_events(self):
         if not self.timing or not self.timing["pool"]:
             return None
@@ -235,7 +257,7 @@ class NeRFTrainer:
             xd_f = K.build_xd(rays, t_f)
             ws_f = self._workspace("f", N * (S + NI), two_stream=self.split_wgrad)
             ev = ev_box[0]
-            rs_f = K.mlp_fwd(self.w(fine_k), xd_f, ws_f, True, events=ev["fwd"] if ev else None,
+            rs_f = K.mlp_fwd(self.w(fine_k), xd_f, ws_f, True, events=ev["fwd"] if ev and ev["fwd"] else None,
                              precision=self.precision, bf16_flags=self.bf16_flags,
                           fp32_flags=self.fp32_flags)
             if self.overlap and self.overlap_with == "bwd":
@@ -245,7 +267,7 @@ class NeRFTrainer:
                                                     loss_sum=self.loss_buf)
             d_rs_f = K.composite_bwd(rs_f, t_f, bg, drgb_f, sigma_scale=self.sigma_scale)
             K.mlp_bwd(self.w(fine_k), N * (S + NI), d_rs_f, ws_f, d_w=self.g(fine_k), accumulate=False,
-                      events=ev["bwd"] if ev else None, precision=self.precision, bf16_flags=self.bf16_flags,
+                      events=ev["bwd"] if ev and ev["bwd"] else None, precision=self.precision, bf16_flags=self.bf16_flags,
                       fp32_flags=self.fp32_flags, wgrad_stream=self._wg if self.split_wgrad else None,
                       sync=self._wg_sync if self.split_wgrad else None)
             if ev:

@@ -144,3 +144,17 @@ def test_mlp_fp16_refuses_layered_flags(K, wpk):
                                 None)
     assert rc == -3  # NERF_E_ENUM: the fp16 build has only the fused kernels
     assert K.mlp_workspace_bytes(M, True, "fp16") == K.mlp_workspace_bytes(M, True, "bf16")
+
+
+def test_mlp_fp16_empty_and_accumulate_zero_rows(K, wpk):
+    """M = 0: the forward is a no-op and the backward zero-fills d_w (or leaves an accumulated d_w untouched)."""
+    x = torch.empty(0, 6, device=DEV)
+    ws = K.mlp_workspace(0, True, DEV, "fp16")
+    out = K.mlp_fwd(wpk, x, ws, True, precision="fp16")
+    assert out.shape == (0, 4)
+    d_w = K.mlp_bwd(wpk, 0, torch.empty(0, 4, device=DEV), ws, precision="fp16")
+    assert torch.count_nonzero(d_w) == 0
+    base = torch.randn_like(wpk)
+    acc = base.clone()
+    K.mlp_bwd(wpk, 0, torch.empty(0, 4, device=DEV), ws, d_w=acc, accumulate=True, precision="fp16")
+    assert torch.equal(acc, base)
