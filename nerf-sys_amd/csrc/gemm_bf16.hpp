@@ -105,8 +105,19 @@ __device__ __forceinline__ nerf_f32x16 h16_mfma(nerf_bf16x8 a, nerf_bf16x8 b, ne
 // element j of a container as fp32 / element j := round(x) (the build's element type); macros, so the bf16 build's
 // expressions are the round-4 ones token for token (same ISA)
 #if NERF_F16
-#define H16_GET(v, j) ((float)__builtin_bit_cast(nerf_bf16, (v)[j]))
-#define H16_SET(v, j, x) ((v)[j] = __builtin_bit_cast(__bf16, (nerf_bf16)(x)))
+// through a u16 view: hipcc (ROCm 7.2) folds a bit_cast of a __bf16 vector element to _Float16 into element 0 for every
+// j (the narrow weight gradient's bias summed element 0 eight times: trunk.0 bias 2.5x off)
+typedef unsigned short nerf_u16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ float h16_get_f16(const nerf_bf16x8 v, int j) {
+  return (float)__builtin_bit_cast(_Float16, (unsigned short)__builtin_bit_cast(nerf_u16x8, v)[j]);
+}
+__device__ __forceinline__ void h16_set_f16(nerf_bf16x8& v, int j, float x) {
+  nerf_u16x8 t = __builtin_bit_cast(nerf_u16x8, v);
+  t[j] = __builtin_bit_cast(unsigned short, (_Float16)x);
+  v = __builtin_bit_cast(nerf_bf16x8, t);
+}
+#define H16_GET(v, j) h16_get_f16((v), (j))
+#define H16_SET(v, j, x) h16_set_f16((v), (j), (x))
 #else
 #define H16_GET(v, j) ((float)(v)[j])
 #define H16_SET(v, j, x) ((v)[j] = (nerf_bf16)(x))
