@@ -346,20 +346,28 @@ __device__ __forceinline__ void bias_acc(const IoSet& R, float (&bs)[8]) {
   static_for<0, 8>([&](auto I) {
     constexpr int i = decltype(I)::value;
     const io_u32x4 v = const_cast<IoSet&>(R).template at<i>();
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
 #if NERF_F16
-      // fp16 build: v_dot2_f32_f16 with (1, 0) / (0, 1) adds one half to the fp32 sum in one instruction (exact product,
-      // one rounding).  Converting with v_cvt_f32_f16 first made hipcc spill 70 VGPRs of the io register sets.
+    // fp16 build: each dword as a half2 added to the two fp32 sums with v_dot2c_f32_f16 against (1, 0) / (0, 1) (the
+    // exact x + sum with one rounding, no conversion temporaries).  The dword goes through a scalar first: hipcc
+    // compiled __builtin_bit_cast(half2, v[d]) on the vector-element lvalue as a read of v[0] for every d (all four
+    // column pairs summed column pair 0: trunk bias 1.18 relative error; the fault H16_GET avoids, gemm_bf16.hpp).
+    // Measured and not kept: v_cvt_f32_f16 + fp32 adds (hipcc hoists the 64 conversions of a tile set: 70 VGPRs of the
+    // io register sets spilled), integer fp16 -> fp32 decoding (296 VGPRs spilled)
+    static_for<0, 4>([&](auto D) {
+      constexpr int d = decltype(D)::value;
       typedef _Float16 h2_ __attribute__((ext_vector_type(2)));
-      const h2_ x = __builtin_bit_cast(h2_, v[d]);
+      const unsigned int u = v[d];
+      const h2_ x = __builtin_bit_cast(h2_, u);
       bs[2 * d] = __builtin_amdgcn_fdot2(x, h2_{(_Float16)1.0f, (_Float16)0.0f}, bs[2 * d], false);
       bs[2 * d + 1] = __builtin_amdgcn_fdot2(x, h2_{(_Float16)0.0f, (_Float16)1.0f}, bs[2 * d + 1], false);
+    });
 #else
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
       bs[2 * d] += nerf_bf16_lo(v[d]);
       bs[2 * d + 1] += nerf_bf16_hi(v[d]);
-#endif
     }
+#endif
   });
 }
 

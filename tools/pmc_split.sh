@@ -10,7 +10,7 @@ for v in ${VARIANTS:-split}; do
   mkdir -p $OUT
   timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE \
     --kernel-trace --output-format csv -d $OUT/p1 -o run -- \
-    python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-psnr --no-dropin --no-native-ref --no-other-precision ${LEG_ARGS:---sweep-steps 50} --train-views 4 --fp32-gemm $v > $OUT/p1.log 2>&1 || { tail -20 $OUT/p1.log; exit 1; }
+    python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-psnr --no-dropin --no-native-ref --no-other-precision --no-ngp --no-container ${LEG_ARGS:---sweep-steps 50} --train-views 4 --fp32-gemm $v > $OUT/p1.log 2>&1 || { tail -20 $OUT/p1.log; exit 1; }
   python3 tools/gemm_pmc_parse.py $OUT/p1 | grep -v rocclr | grep -E "x6|wgrad" > $OUT/summary.txt
   echo "== $v"; cut -c1-330 $OUT/summary.txt
 done

@@ -10,6 +10,6 @@ OUT=${PMC_OUT:-gpurun_out/pmc}
 mkdir -p $OUT
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/$C -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-psnr ${LEG_ARGS:---sweep-steps 50} --train-views 4 $PMC_BENCH_ARGS > $OUT/$C.log 2>&1 || { tail -20 $OUT/$C.log; exit 1; }
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-psnr --no-ngp --no-container ${LEG_ARGS:---sweep-steps 50} --train-views 4 $PMC_BENCH_ARGS > $OUT/$C.log 2>&1 || { tail -20 $OUT/$C.log; exit 1; }
 done
 python3 tools/pmc_parse.py $OUT $PMC_PRECISION

@@ -1,0 +1,32 @@
+#!/bin/bash
+# Round-5 evidence on one GPU box: the default bench line, rocprof kernel stats of the bench command (fp32 and bf16),
+# PMC HBM traffic (FETCH_SIZE / WRITE_SIZE passes) and MFMA busy of the bench's kernels.  Outputs under gpurun_out/r05.
+set -o pipefail
+cd "$(dirname "$0")/.."
+O=gpurun_out/r05; mkdir -p $O; export TMPDIR=/tmp
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu_all.log 2>&1 || { tail -30 $O/pytest_gpu_all.log; exit 1; }
+  tail -1 $O/pytest_gpu_all.log
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+  tail -1 $O/smoke.log
+fi
+if [ -z "$SKIP_BENCH" ]; then
+  timeout -k 10 560 python bench.py > $O/bench_default.log 2>&1 || { tail -30 $O/bench_default.log; exit 1; }
+  tail -1 $O/bench_default.log | cut -c1-400
+fi
+[ -n "$STOP_AFTER_BENCH" ] && exit 0
+for P in fp32 bf16; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$P -o run --output-format csv -- \
+    python3 bench.py --precision $P --steps 20 --warmup 5 --no-cpu-baseline --no-psnr --no-dropin --no-other-precision --no-native-ref --no-ngp --no-container ${LEG_ARGS:---sweep-steps 50} \
+    > $O/prof_$P.log 2>&1 || { tail -20 $O/prof_$P.log; exit 1; }
+  python3 tools/prof_summary.py $O/prof_$P/run_kernel_stats.csv 28 3 > $O/prof_${P}_summary.txt 2>&1
+  python3 tools/step_timeline.py $O/prof_$P/run_kernel_trace.csv > $O/step_${P}.txt 2>&1 || true
+  echo "prof $P: $(tail -1 $O/prof_$P.log | cut -c1-200)"
+done
+[ -n "$STOP_AFTER_PROF" ] && exit 0
+PMC_OUT=$O/pmc_fp32 PMC_BENCH_ARGS="--no-dropin --no-other-precision --no-native-ref" bash tools/pmc_traffic.sh > $O/pmc_fp32.txt 2>&1 || { tail -20 $O/pmc_fp32.txt; exit 1; }
+PMC_OUT=$O/pmc_bf16 PMC_PRECISION=bf16fused PMC_BENCH_ARGS="--precision bf16 --no-dropin --no-other-precision" bash tools/pmc_traffic.sh > $O/pmc_bf16.txt 2>&1 || { tail -20 $O/pmc_bf16.txt; exit 1; }
+PMC_OUT=$O/pmc_mfma PMC_BENCH_ARGS="--no-other-precision --no-native-ref" bash tools/pmc_mfma_bench.sh > $O/pmc_mfma.txt 2>&1 || { tail -20 $O/pmc_mfma.txt; exit 1; }
+for f in $O/pmc_fp32.txt $O/pmc_bf16.txt $O/pmc_mfma.txt; do tail -n 3 $f; done
+VARIANTS=split bash tools/pmc_split.sh > $O/pmc_split.txt 2>&1 || { tail -20 $O/pmc_split.txt; exit 1; }
+cp -r gpurun_out/pmc_split_split $O/ 2>/dev/null; tail -n 4 $O/pmc_split.txt | cut -c1-200
