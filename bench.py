@@ -242,7 +242,7 @@ def cpu_baseline(S, NI, n, steps):
     return rec
 
 
-def dropin_run(rb, dev, a, world, rank, n_local, precision="fp32"):
+def dropin_run(rb, dev, a, world, rank, n_local, precision="fp32", amp_dtype=torch.float16):
     """The reference loop body (runtime_adapt.py:286-310) on the drop-in surface: HierarchicalNeRF (coarse +
     fine VanillaNeRF, autograd through the HIP MLP / compositing / sampling ops) -> compute_mse_loss (coarse +
     fine terms) -> backward -> clip_grad_norm_(1.0) -> torch.optim.Adam ('sigma' / 'color' groups).  precision
@@ -250,7 +250,8 @@ def dropin_run(rb, dev, a, world, rank, n_local, precision="fp32"):
     GradScaler scale / unscale_ / step / update; the expert then dispatches to the fp16 build of the fused MLP kernels
     (vanilla.amp_precision), beside the bf16 C3 engine.  Adam is torch's fused implementation (no host sync inside GradScaler.step; foreach
     if this torch build lacks it).  The ray batch comes from images resident in HBM (the reference's DataLoader +
-    .to(device) is not timed)."""
+    .to(device) is not timed).  amp_dtype=torch.bfloat16 (tools/amp_kernels_ab.py only) runs the same body under
+    autocast(bfloat16), i.e. on the bf16 build of the kernels."""
     from types import SimpleNamespace
     from nerf_amd.losses import compute_mse_loss
     from nerf_amd.vanilla import HierarchicalNeRF
@@ -269,7 +270,7 @@ def dropin_run(rb, dev, a, world, rank, n_local, precision="fp32"):
     def one(step):
         rays, gt = _batch(rb, a, step, rank, world, n_local)
         opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.float16, enabled=use_amp):
+        with torch.autocast("cuda", dtype=amp_dtype, enabled=use_amp):
             loss = compute_mse_loss(P, model, {"rays": rays, "rgbs": gt})
         scaler.scale(loss).backward()
         scaler.unscale_(opt)

@@ -89,8 +89,8 @@ def task_adapt(P, model, support, inner_lr, iterations, active_module: Optional[
     """meta_core.py:14-68. Returns (fast OrderedDict, [detached loss per iteration]).
 
     First order only (P.algo in {"fomaml", "reptile"}).  Like the reference (:30-38) each inner forward runs under
-    autocast(fp16) when P.use_amp (default True) and a GPU is present: vanilla experts then take their bf16 MLP
-    kernels (vanilla.amp_precision); the Instant-NGP kernels stay fp32."""
+    autocast(fp16) when P.use_amp (default True) and a GPU is present: vanilla experts then take the fp16 build of
+    their MLP kernels (vanilla.amp_precision); the Instant-NGP kernels stay fp32."""
     algo = str(getattr(P, "algo", "")).lower()
     if algo not in ("fomaml", "reptile"):
         raise NotImplementedError(f"task_adapt: algo {algo!r} needs second-order gradients (create_graph=True), "

@@ -217,8 +217,8 @@ def render_image(model, *, H: int, W: int, fx: float, fy: float, cx: float, cy: 
                  fine_model=None):
     """ray_rendering.py:577-627 — rays from the fused HIP kernel, rendered in ray chunks.
     ``ndc=(focal, near_plane)`` converts rays to forward-facing NDC first (LLFF config).  ``use_amp`` renders under
-    ``torch.autocast("cuda", torch.float16)`` as the reference does (:611): the MLP runs its bf16 kernels
-    (vanilla.amp_precision), compositing stays fp32."""
+    ``torch.autocast("cuda", torch.float16)`` as the reference does (:611): the MLP runs the fp16 build of its
+    fused kernels (vanilla.amp_precision), compositing stays fp32."""
     if use_amp:
         with torch.autocast("cuda", dtype=torch.float16):
             return render_image(model, H=H, W=W, fx=fx, fy=fy, cx=cx, cy=cy, c2w=c2w, scene_box=scene_box, near=near,

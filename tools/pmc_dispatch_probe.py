@@ -15,13 +15,16 @@ faulthandler.enable(all_threads=True)
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=200000)
 ap.add_argument("--every", type=int, default=2000)
+ap.add_argument("--streams", type=int, default=1, help="alternate the launches over this many HIP streams")
 a = ap.parse_args()
-x = torch.zeros(1024, device="cuda")
+xs = [torch.zeros(1024, device="cuda") for _ in range(a.streams)]
+ss = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(a.streams - 1)]
 t0 = time.perf_counter()
 for i in range(1, a.n + 1):
-    x.add_(1.0)
+    with torch.cuda.stream(ss[i % a.streams]):
+        xs[i % a.streams].add_(1.0)
     if i % a.every == 0:
         torch.cuda.synchronize()
         print(f"[probe {time.perf_counter() - t0:7.1f}s] {i} dispatches", flush=True)
 torch.cuda.synchronize()
-print(f"probe done: {a.n} dispatches, x[0] = {x[0].item()}", flush=True)
+print(f"probe done: {a.n} dispatches over {a.streams} stream(s), sum = {sum(x[0].item() for x in xs)}", flush=True)

@@ -4,6 +4,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 O=gpurun_out/r05; mkdir -p $O; export TMPDIR=/tmp
+if [ -n "$PMC_ONLY" ]; then SKIP_TESTS=1; SKIP_BENCH=1; SKIP_PROF=1; fi
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu_all.log 2>&1 || { tail -30 $O/pytest_gpu_all.log; exit 1; }
   tail -1 $O/pytest_gpu_all.log
@@ -15,14 +16,22 @@ if [ -z "$SKIP_BENCH" ]; then
   tail -1 $O/bench_default.log | cut -c1-400
 fi
 [ -n "$STOP_AFTER_BENCH" ] && exit 0
-for P in fp32 bf16; do
+for P in ${SKIP_PROF:+none} ${SKIP_PROF:-fp32 bf16}; do
+  [ "$P" = none ] && break
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$P -o run --output-format csv -- \
-    python3 bench.py --precision $P --steps 20 --warmup 5 --no-cpu-baseline --no-psnr --no-dropin --no-other-precision --no-native-ref --no-ngp --no-container ${LEG_ARGS:---sweep-steps 50} \
+    python3 bench.py --precision $P --steps 20 --warmup 5 --no-cpu-baseline --no-psnr --no-dropin --no-other-precision --no-native-ref --no-ngp --no-container $LEG_ARGS \
     > $O/prof_$P.log 2>&1 || { tail -20 $O/prof_$P.log; exit 1; }
   python3 tools/prof_summary.py $O/prof_$P/run_kernel_stats.csv 28 3 > $O/prof_${P}_summary.txt 2>&1
   python3 tools/step_timeline.py $O/prof_$P/run_kernel_trace.csv > $O/step_${P}.txt 2>&1 || true
   echo "prof $P: $(tail -1 $O/prof_$P.log | cut -c1-200)"
 done
+if [ -z "$SKIP_PROF" ]; then
+# the reference's AMP loop body under autocast(float16) (fp16 build) and autocast(bfloat16) (bf16 build), kernel stats
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_amp -o run --output-format csv -- python3 tools/amp_kernels_ab.py \
+  > $O/amp_ab.log 2>&1 || { tail -20 $O/amp_ab.log; exit 1; }
+python3 tools/prof_summary.py $O/prof_amp/run_kernel_stats.csv 40 3 > $O/prof_amp_summary.txt 2>&1
+grep -E "^(fp16|bf16)" $O/amp_ab.log
+fi
 [ -n "$STOP_AFTER_PROF" ] && exit 0
 PMC_OUT=$O/pmc_fp32 PMC_BENCH_ARGS="--no-dropin --no-other-precision --no-native-ref" bash tools/pmc_traffic.sh > $O/pmc_fp32.txt 2>&1 || { tail -20 $O/pmc_fp32.txt; exit 1; }
 PMC_OUT=$O/pmc_bf16 PMC_PRECISION=bf16fused PMC_BENCH_ARGS="--precision bf16 --no-dropin --no-other-precision" bash tools/pmc_traffic.sh > $O/pmc_bf16.txt 2>&1 || { tail -20 $O/pmc_bf16.txt; exit 1; }
@@ -30,3 +39,19 @@ PMC_OUT=$O/pmc_mfma PMC_BENCH_ARGS="--no-other-precision --no-native-ref" bash t
 for f in $O/pmc_fp32.txt $O/pmc_bf16.txt $O/pmc_mfma.txt; do tail -n 3 $f; done
 VARIANTS=split bash tools/pmc_split.sh > $O/pmc_split.txt 2>&1 || { tail -20 $O/pmc_split.txt; exit 1; }
 cp -r gpurun_out/pmc_split_split $O/ 2>/dev/null; tail -n 4 $O/pmc_split.txt | cut -c1-200
+# one PMC pass over the whole default bench (every leg: C2, C3 + drop-ins, C4, C5 sweep, NGP, container, PSNR) with the
+# counters on this library's MLP kernels (DESIGN.md §4 "rocprofv3 PMC")
+F="x6|gemm|bwd_layer|mlp_fwd_fused|tail|color_bwd|head_bwd|reduce_"
+timeout -s KILL 1000 rocprofv3 --kernel-include-regex "$F" --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
+  --kernel-trace --output-format csv -d $O/pmc_full -o run -- python3 bench.py > $O/pmc_full_bench.log 2>&1
+rc=$?; echo "PMC pass over the full bench: rc=$rc"; tail -1 $O/pmc_full_bench.log | cut -c1-300
+python3 - <<'PY'
+import csv, glob
+for f in glob.glob("gpurun_out/r05/pmc_full/**/*counter_collection.csv", recursive=True):
+    d = set(r["Dispatch_Id"] for r in csv.DictReader(open(f)))
+    print("counted dispatches:", len(d))
+for f in glob.glob("gpurun_out/r05/pmc_full/**/*kernel_trace.csv", recursive=True):
+    print("traced dispatches:", sum(1 for _ in open(f)) - 1)
+PY
+rm -rf $O/pmc_full/*.csv $O/pmc_full/*/*.csv 2>/dev/null
+exit $rc
