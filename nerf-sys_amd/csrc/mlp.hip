@@ -280,6 +280,14 @@ int nt_x6(const float* A, int lda, const nerf_bf16* Bp, int ldb, int64_t bplane,
       return NERF_OK;
     }
   }
+#ifdef NERF_X6_FWD_W12  // A/B builds: forward on 32-row waves, NERF_X6_FWD_W12 (12 or 16) per workgroup (3 / 4 per SIMD)
+  if (EPI == EPI_BIAS_RELU && M % (32 * NERF_X6_FWD_W12) == 0 && K % 64 == 0) {
+    gemm_nt_x6w_kernel<EPI, 32, NERF_X6_FWD_W12, false, 1, 1><<<(unsigned)((M / (32 * NERF_X6_FWD_W12)) * ntn),
+                                                                64 * NERF_X6_FWD_W12, 0, st>>>(
+        A, lda, Bp, ldb, bplane, bias, C, ldc, mbits, N / 32, mbits_out, K, ntn);
+    return NERF_OK;
+  }
+#endif
   if (M % (64 * NERF_X6W_NW) == 0 && K % (2 * NERF_X6W_BK) == 0) {
     gemm_nt_x6w_kernel<EPI, NERF_X6W_BK, NERF_X6W_NW><<<(unsigned)((M / (64 * NERF_X6W_NW)) * ntn), 64 * NERF_X6W_NW, 0,
                                                         st>>>(A, lda, Bp, ldb, bplane, bias, C, ldc, mbits, N / 32,

@@ -23,6 +23,7 @@ for P in ${SKIP_PROF:+none} ${SKIP_PROF:-fp32 bf16}; do
     > $O/prof_$P.log 2>&1 || { tail -20 $O/prof_$P.log; exit 1; }
   python3 tools/prof_summary.py $O/prof_$P/run_kernel_stats.csv 28 3 > $O/prof_${P}_summary.txt 2>&1
   python3 tools/step_timeline.py $O/prof_$P/run_kernel_trace.csv > $O/step_${P}.txt 2>&1 || true
+  rm -f $O/prof_$P/run_kernel_trace.csv  # (the C5 leg's trace alone is tens of MB; gpurun returns <= 64 MiB)
   echo "prof $P: $(tail -1 $O/prof_$P.log | cut -c1-200)"
 done
 if [ -z "$SKIP_PROF" ]; then
@@ -30,15 +31,21 @@ if [ -z "$SKIP_PROF" ]; then
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_amp -o run --output-format csv -- python3 tools/amp_kernels_ab.py \
   > $O/amp_ab.log 2>&1 || { tail -20 $O/amp_ab.log; exit 1; }
 python3 tools/prof_summary.py $O/prof_amp/run_kernel_stats.csv 40 3 > $O/prof_amp_summary.txt 2>&1
+rm -f $O/prof_amp/run_kernel_trace.csv
 grep -E "^(fp16|bf16)" $O/amp_ab.log
 fi
 [ -n "$STOP_AFTER_PROF" ] && exit 0
+# the per-kernel PMC passes need only the C2 / C3 legs (the full-bench pass at the end runs every leg)
+export LEG_ARGS="--no-llff --no-sweep"
 PMC_OUT=$O/pmc_fp32 PMC_BENCH_ARGS="--no-dropin --no-other-precision --no-native-ref" bash tools/pmc_traffic.sh > $O/pmc_fp32.txt 2>&1 || { tail -20 $O/pmc_fp32.txt; exit 1; }
 PMC_OUT=$O/pmc_bf16 PMC_PRECISION=bf16fused PMC_BENCH_ARGS="--precision bf16 --no-dropin --no-other-precision" bash tools/pmc_traffic.sh > $O/pmc_bf16.txt 2>&1 || { tail -20 $O/pmc_bf16.txt; exit 1; }
 PMC_OUT=$O/pmc_mfma PMC_BENCH_ARGS="--no-other-precision --no-native-ref" bash tools/pmc_mfma_bench.sh > $O/pmc_mfma.txt 2>&1 || { tail -20 $O/pmc_mfma.txt; exit 1; }
 for f in $O/pmc_fp32.txt $O/pmc_bf16.txt $O/pmc_mfma.txt; do tail -n 3 $f; done
+find $O/pmc_fp32 $O/pmc_bf16 $O/pmc_mfma -name "*.csv" -size +4M -delete 2>/dev/null
 VARIANTS=split bash tools/pmc_split.sh > $O/pmc_split.txt 2>&1 || { tail -20 $O/pmc_split.txt; exit 1; }
-cp -r gpurun_out/pmc_split_split $O/ 2>/dev/null; tail -n 4 $O/pmc_split.txt | cut -c1-200
+tail -n 4 $O/pmc_split.txt | cut -c1-200
+find $O gpurun_out/pmc_split_split -name "*.csv" -size +4M -delete 2>/dev/null
+unset LEG_ARGS
 # one PMC pass over the whole default bench (every leg: C2, C3 + drop-ins, C4, C5 sweep, NGP, container, PSNR) with the
 # counters on this library's MLP kernels (DESIGN.md §4 "rocprofv3 PMC")
 F="x6|gemm|bwd_layer|mlp_fwd_fused|tail|color_bwd|head_bwd|reduce_"
