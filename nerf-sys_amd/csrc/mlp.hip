@@ -86,7 +86,7 @@ WS carve(void* base, int64_t M, int training) {
     w.S = n_splits(Mp);
     w.rps = round_up(nerf_cdiv(Mp, w.S), 64);  // whole slabs for every wgrad MR
     w.partial = take((int64_t)w.S * layout().total);
-    w.partial2 = take((int64_t)w.S * (layout().total - P2BASE));  // head + colour sums of the second halves
+    w.partial2 = take((int64_t)(TAIL_NQ - 1) * w.S * (layout().total - P2BASE));  // head + colour sums, parts 1..
   }
   w.bytes = (int64_t)((char*)p - (char*)base);
   return w;
@@ -488,17 +488,17 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
   }
   if (nj) transpose_kernel<<<dim3(8, 8, nj), 256, 0, st>>>(jobs);
 
-  // colour branch + head activations in one kernel: dO16 and the colour weight / bias slabs (two workgroups per
-  // split; the second halves' colour sums go to W.partial2 and are added by the final reduce)
+  // colour branch + head activations in one kernel: dO16 and the colour weight / bias slabs (TAIL_NQ workgroups per
+  // split; the colour sums of parts 1.. go to W.partial2 and are added by the final reduce)
   float* dcur = W.dA;
   float* dnext = W.dB;
   // events 2/3 (layer 0 has no input gradient) bracket the backward tail (colour branch + heads -> dZ7)
   if (ev) (void)hipEventRecord(ev[2], st);
   // colour branch -> dO16 [Mp][16]; then ONE pass over Y7 for dZ7 and the head weight / bias sums (mlp_tail.hpp)
-  color_bwd_kernel<float, float><<<2 * W.S, 256, 0, st>>>(d_rgb_sigma, W.HO, W.C0, W.CIN, Wt(18), Wt(20), W.dO16,
+  color_bwd_kernel<float, float><<<TAIL_NQ * W.S, 256, 0, st>>>(d_rgb_sigma, W.HO, W.C0, W.CIN, Wt(18), Wt(20), W.dO16,
                                                           W.partial, L.total, L.off[18], L.off[19], L.off[20], L.off[21],
                                                           W.rps, M, Mp, W.partial2, L.total - P2BASE, P2BASE, 16);
-  head_bwd_kernel<<<2 * W.S, 256, 0, st>>>(W.dO16, W.Y[7], Wt(16), dcur, W.partial, L.total, W.partial2,
+  head_bwd_kernel<<<TAIL_NQ * W.S, 256, 0, st>>>(W.dO16, W.Y[7], Wt(16), dcur, W.partial, L.total, W.partial2,
                                            L.total - P2BASE, P2BASE, L.off[16], L.off[17], W.rps, Mp);
   if (ev) (void)hipEventRecord(ev[3], st);
   TRY(handoff(1));  // dZ7 and the head / colour slabs are complete

@@ -298,6 +298,20 @@ __device__ __forceinline__ uint32_t relu_pk(float x, float y) {
   return __builtin_bit_cast(uint32_t, r);
 }
 
+// fp16 build: the output pair of accumulator registers (r, r + 1) — both fp16-rounded in one v_cvt_pk_f16_f32,
+// widened, the fp32 bias pair added in one v_pk_add_f32 — then relu_pk.  The scalar form (acc_out per element: two
+// converts and an add each) made the fp16 training forward 20 % slower than the bf16 one (750 vs 627 us per launch,
+// profiles/r05/prof_amp_summary.txt).  bf16 build: relu_pk of the accumulators (the bias is in them already).
+__device__ __forceinline__ uint32_t relu_pk_out(float a0, float a1, float b0, float b1) {
+#if NERF_F16
+  const nerf_f16x2 h = __builtin_convertvector(nerf_f32x2{a0, a1}, nerf_f16x2);
+  const nerf_f32x2 x = __builtin_convertvector(h, nerf_f32x2) + nerf_f32x2{b0, b1};
+  return relu_pk(x[0], x[1]);
+#else
+  return relu_pk(a0, a1);
+#endif
+}
+
 template <int TA, int NB>
 __device__ __forceinline__ void relu_to_lds(const nerf_f32x16 (&acc)[4][2], nerf_bf16* dst, int pitch, int ar0, int c0,
                                             int li, int lh, const float* bias) {
@@ -315,9 +329,12 @@ __device__ __forceinline__ void relu_to_lds(const nerf_f32x16 (&acc)[4][2], nerf
     for (int b = 0; b < NB; ++b) {
       uint2 pk[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        pk[q] = make_uint2(relu_pk(acc_out(acc[a][b], 4 * q, bias, c0 + 32 * b, lh), acc_out(acc[a][b], 4 * q + 1, bias, c0 + 32 * b, lh)),
-                           relu_pk(acc_out(acc[a][b], 4 * q + 2, bias, c0 + 32 * b, lh), acc_out(acc[a][b], 4 * q + 3, bias, c0 + 32 * b, lh)));
+      for (int q = 0; q < 4; ++q) {
+        float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);  // columns c0 + 32 b + 8 q + 4 lh .. + 3
+        if constexpr (H16_BIAS_AFTER) b4 = *reinterpret_cast<const float4*>(bias + c0 + 32 * b + 8 * q + 4 * lh);
+        pk[q] = make_uint2(relu_pk_out(acc[a][b][4 * q], acc[a][b][4 * q + 1], b4.x, b4.y),
+                           relu_pk_out(acc[a][b][4 * q + 2], acc[a][b][4 * q + 3], b4.z, b4.w));
+      }
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
         uint2 x = pk[2 * pr], y = pk[2 * pr + 1];

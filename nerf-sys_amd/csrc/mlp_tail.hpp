@@ -27,6 +27,25 @@
 // ran on 32x32x2 tiles with 17 of 32 columns unused plus an LDS sum of two contraction halves (5 barriers per tile,
 // now 3).
 namespace nerf_mlp {
+// row parts per split of color_bwd / head_bwd: part 0 writes its sums into the split's slab, parts 1 .. TAIL_NQ - 1
+// into rows (q - 1) S + s of partial2, added by reduce_splits2 after the slab terms.  Measured (C2, one box,
+// profiles/r05/x6_variants_ab.txt): 2 parts 224.4-225.4k, 4 parts 224.0-224.1k, 8 parts 222.7-223.2k rays/s — the
+// extra parts' partial slabs and reduce terms cost more than the second workgroup per CU gains; 2 is kept
+#ifndef NERF_TAIL_NQ
+#define NERF_TAIL_NQ 2
+#endif
+constexpr int TAIL_NQ = NERF_TAIL_NQ;
+// rows [r0, r1) of part q of split sp (rps and the part length are multiples of `unit` rows)
+__device__ __forceinline__ void tail_part_rows(int64_t sp, int q, int64_t rps, int64_t Mp, int unit, int64_t& r0,
+                                               int64_t& r1) {
+  const int64_t rpq = ((rps + (int64_t)TAIL_NQ * unit - 1) / ((int64_t)TAIL_NQ * unit)) * unit;
+  const int64_t s0 = sp * rps, s1 = s0 + rps;
+  r0 = s0 + q * rpq;
+  r1 = (q == TAIL_NQ - 1) ? s1 : r0 + rpq;
+  if (r1 > s1) r1 = s1;
+  if (r1 > Mp) r1 = Mp;
+  if (r0 > r1) r0 = r1;
+}
 constexpr int CB_ROWS = 64;
 constexpr int CB_C0 = 132, CB_CIN = 68;
 
@@ -54,26 +73,25 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
                                                         int64_t Mp, float* __restrict__ partial2, int64_t cslab,
                                                         int64_t p2base, int ldd) {
   // dC0 overwrites C0 in place (each element by the thread that read it, so without a barrier between): 52 KB of LDS,
-  // two workgroups per CU, three barriers per tile.  Workgroup 2s + h walks half h of split s; half 0 writes the
-  // colour sums into slab s, half 1 into row s of partial2 (cslab floats: packed offsets p2base .. total of one slab;
-  // p2base <= off_w0).  dO16 rows have pitch ldd: 32 (columns 16..31 written as zeros) or 16.
+  // two workgroups per CU, three barriers per tile.  Workgroup TAIL_NQ s + q walks part q of split s; part 0 writes the
+  // colour sums into slab s, part q > 0 into row (q - 1) S + s of partial2 (cslab floats: packed offsets p2base ..
+  // total of one slab; p2base <= off_w0).  dO16 rows have pitch ldd: 32 (columns 16..31 written as zeros) or 16.
   __shared__ __attribute__((aligned(16))) float s_c0[CB_ROWS * CB_C0];
   float* const s_dc0 = s_c0;
   __shared__ __attribute__((aligned(16))) float s_cin[CB_ROWS * CB_CIN];
   __shared__ __attribute__((aligned(16))) float s_do3[CB_ROWS * 4];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 31, lh = lane >> 5;
-  const int64_t sp = blockIdx.x >> 1, half = blockIdx.x & 1;
-  const int64_t rph = ((rps + 2 * CB_ROWS - 1) / (2 * CB_ROWS)) * CB_ROWS;  // rows of half 0
-  const int64_t r0 = sp * rps + half * rph;
-  int64_t r1 = half ? sp * rps + rps : r0 + rph;
-  if (r1 > Mp) r1 = Mp;
+  const int64_t sp = blockIdx.x / TAIL_NQ, S = gridDim.x / TAIL_NQ;
+  const int q = blockIdx.x % TAIL_NQ;
+  int64_t r0, r1;
+  tail_part_rows(sp, q, rps, Mp, CB_ROWS, r0, r1);
 
   // register prefetch of one tile: C0 = 2048 float4 (8 / thread), CIN = 1024 float4 (4 / thread); wave 0 also
   // prefetches the tile's head outputs: d_rgb_sigma (M rows: the row index is clamped, the value zeroed below for
   // m >= M) and the HO row (the three colour pre-activations, sigma_raw).
   float4 pc[8], pi[4], pg = make_float4(0.f, 0.f, 0.f, 0.f), po = pg;
-  // r0, r1, rps and the half length are multiples of CB_ROWS (the host rounds rps to 64; Mp is a multiple of 256),
+  // r0, r1, rps and the part length are multiples of CB_ROWS (the host rounds rps to 64; Mp is a multiple of 256),
   // so every row of a tile is < r1 and the loads carry no row guard (a guarded load became a branch with a
   // vmcnt(0) drain after it); a uniform tile base + 32-bit lane offsets keeps no 64-bit address per load live
   auto fetch = [&](int64_t t0) {
@@ -185,7 +203,7 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
     if (jw == 0) { s_c0[512] = b1a; s_c0[513] = b1b; s_c0[514] = b1c; }
   }
   __syncthreads();
-  float* P = half ? partial2 + sp * cslab - p2base : partial + sp * slab;
+  float* P = q ? partial2 + ((q - 1) * S + sp) * cslab - p2base : partial + sp * slab;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int n = (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -216,7 +234,7 @@ __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restri
 // read of a Y7 float4 is both the ReLU mask of the lane's own dZ7 float4 and a weight-gradient MFMA operand.  It
 // replaces the head input-gradient GEMM and the head weight-gradient GEMM, which streamed Y7 / dZ7 separately
 // (fine net, round 3: 258 + 216 us; this pass moves 2.1 KB per row: dO16 64 B + Y7 1 KB in, dZ7 1 KB out).
-// Same split walk as color_bwd (workgroup 2s + h, 64-row tiles, sums in registers, half 1 into partial2).  Lane
+// Same split walk as color_bwd (workgroup TAIL_NQ s + q, 64-row tiles, sums in registers, parts q > 0 into partial2).  Lane
 // (g, j) of wave w owns columns hc = 64 w + 4 j .. + 3 and, in row group u, row 4 u + g: its dZ7 float4 is a
 // 16-term VALU dot against its register slice of Wh, and its Y7 float4 is the B operand of four 16x16x4 MFMAs
 // (column hc + q, q = 0..3) whose A operand is dO16[4 u + g][n = j] — output lane (g, j) register v then holds
@@ -233,11 +251,10 @@ static __global__ __launch_bounds__(256, 2) void head_bwd_kernel(const float* __
   __shared__ __attribute__((aligned(16))) float s_d[2][HB_ROWS * 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, j = lane & 15;
   const int hc = 64 * wave + 4 * j;
-  const int64_t sp = blockIdx.x >> 1, half = blockIdx.x & 1;
-  const int64_t rph = ((rps + 2 * HB_ROWS - 1) / (2 * HB_ROWS)) * HB_ROWS;  // rows of half 0
-  const int64_t r0 = sp * rps + half * rph;
-  int64_t r1 = half ? sp * rps + rps : r0 + rph;
-  if (r1 > Mp) r1 = Mp;
+  const int64_t sp = blockIdx.x / TAIL_NQ, S = gridDim.x / TAIL_NQ;
+  const int q = blockIdx.x % TAIL_NQ;
+  int64_t r0, r1;
+  tail_part_rows(sp, q, rps, Mp, HB_ROWS, r0, r1);
   // every tile row is < r1 (r0, r1 multiples of 64, as in color_bwd); "next tile" loads past the last tile re-read it
   const int64_t last = r1 - HB_ROWS;
 
@@ -305,7 +322,7 @@ static __global__ __launch_bounds__(256, 2) void head_bwd_kernel(const float* __
     buf ^= 1;
   }
 
-  float* P = half ? partial2 + sp * cslab - p2base : partial + sp * slab;
+  float* P = q ? partial2 + ((q - 1) * S + sp) * cslab - p2base : partial + sp * slab;
 #pragma unroll
   for (int v = 0; v < 4; ++v)
     *reinterpret_cast<float4*>(P + off_wh + (int64_t)(4 * g + v) * 256 + hc) =
@@ -318,18 +335,22 @@ static __global__ __launch_bounds__(256, 2) void head_bwd_kernel(const float* __
   if (tid >= 16 && tid < 32) P[off_bh + tid] = 0.f;
 }
 
-// reduce_splits plus the second-half colour sums: float4 i >= c0 of the packed gradient also adds the S terms of src2
+// reduce_splits plus the colour / head sums of parts 1.. : float4 i >= c0 of the packed gradient also adds the S terms of src2
 // (src2[s][i - c0]) after the slab terms, both in gemm.hpp's RG-group order (bitwise reproducible); grid cdiv(n4, 64)
+// (TAIL_NQ - 1 sets of S rows in src2: parts 1, 2, ... of color_bwd / head_bwd, each added in that order)
 static __global__ __launch_bounds__(256) void reduce_splits2_kernel(const float* __restrict__ src, int64_t slab, int S,
                                                                     float* __restrict__ dst, int64_t n4, int accumulate,
                                                                     const float* __restrict__ src2, int64_t slab2,
                                                                     int64_t c0) {
-  __shared__ float4 part[2][RG][64];
+  __shared__ float4 part[TAIL_NQ][RG][64];
   const int e = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 64 + e;
   const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
   part[0][g][e] = i < n4 ? rg_group_sum(src + 4 * i, slab, S, g) : z;
-  part[1][g][e] = (i < n4 && i >= c0) ? rg_group_sum(src2 + 4 * (i - c0), slab2, S, g) : z;
+#pragma unroll
+  for (int q = 1; q < TAIL_NQ; ++q)
+    part[q][g][e] = (i < n4 && i >= c0) ? rg_group_sum(src2 + (int64_t)(q - 1) * S * slab2 + 4 * (i - c0), slab2, S, g)
+                                        : z;
   __syncthreads();
   if (g == 0 && i < n4) {
     float4 a = accumulate ? reinterpret_cast<const float4*>(dst)[i] : z;
@@ -337,7 +358,9 @@ static __global__ __launch_bounds__(256) void reduce_splits2_kernel(const float*
     for (int k = 0; k < RG; ++k) rg_add(a, part[0][k][e]);
     if (i >= c0) {
 #pragma unroll
-      for (int k = 0; k < RG; ++k) rg_add(a, part[1][k][e]);
+      for (int q = 1; q < TAIL_NQ; ++q)
+#pragma unroll
+        for (int k = 0; k < RG; ++k) rg_add(a, part[q][k][e]);
     }
     reinterpret_cast<float4*>(dst)[i] = a;
   }

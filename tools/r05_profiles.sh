@@ -19,7 +19,7 @@ fi
 for P in ${SKIP_PROF:+none} ${SKIP_PROF:-fp32 bf16}; do
   [ "$P" = none ] && break
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$P -o run --output-format csv -- \
-    python3 bench.py --precision $P --steps 20 --warmup 5 --no-cpu-baseline --no-psnr --no-dropin --no-other-precision --no-native-ref --no-ngp --no-container $LEG_ARGS \
+    python3 bench.py --precision $P --steps 20 --warmup 5 --no-cpu-baseline --no-psnr --no-dropin --no-other-precision --no-native-ref --no-ngp --no-container ${LEG_ARGS---no-llff --no-sweep} \
     > $O/prof_$P.log 2>&1 || { tail -20 $O/prof_$P.log; exit 1; }
   python3 tools/prof_summary.py $O/prof_$P/run_kernel_stats.csv 28 3 > $O/prof_${P}_summary.txt 2>&1
   python3 tools/step_timeline.py $O/prof_$P/run_kernel_trace.csv > $O/step_${P}.txt 2>&1 || true
