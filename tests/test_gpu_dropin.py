@@ -229,3 +229,58 @@ def test_amp_dropin_step_gradients_vs_oracle_amp(K):
             worst = max(worst, (err, n))
             assert err <= 1e-2, f"net {k} {n}: relative error norm {err:.3e} vs the reference's AMP gradient"
         print(f"net {k}: worst per-tensor relative error norm {worst[0]:.3e} ({worst[1]})")
+
+
+def test_amp_dropin_loop_vs_oracle_amp_multistep(K):
+    """Six steps of the use_amp=True loop body (runtime_adapt.py:286-310: autocast(float16) -> GradScaler scale ->
+    backward -> unscale_ -> clip_grad_norm_(1.0) -> step -> update) on the drop-in surface against
+    OracleTrainer(amp="fp16"), which mirrors GradScaler's unscale / skip / update, from the same weights with the
+    same rays, targets and jitter every step: each step's loss within 1e-3 relative, the GradScaler scale equal, and
+    after the last step every parameter tensor within 5e-3 relative error norm of the oracle's (Adam's first steps
+    move a weight by ~lr whatever its gradient's size, so a gradient near zero whose sign an fp16 rounding flip
+    changes moves by 2 lr), and the whole parameter vector closer to the AMP oracle's than to the fp32 oracle's
+    trajectory from the same inputs."""
+    from nerf_amd.losses import compute_mse_loss
+    pc, pf = O.init_vanilla_params(1), O.init_vanilla_params(2)
+    model = _model(pc, pf).train()
+    opt = _adam(model, 2e-3, 1e-3)
+    scaler = torch.amp.GradScaler("cuda")
+    ot = O.OracleTrainer(pc, pf, lr_sigma=2e-3, lr_color=1e-3, amp="fp16")
+    o32 = O.OracleTrainer(pc, pf, lr_sigma=2e-3, lr_color=1e-3)
+    P = types.SimpleNamespace(ray_samples=64, n_importance=128, chunk_points=1 << 22, color_space="linear")
+    rays_all = load("render")["rays"]
+    for step in range(6):
+        g = torch.Generator().manual_seed(100 + step)
+        idx = torch.randperm(rays_all.shape[0], generator=g)[:512]
+        rays = rays_all[idx].contiguous()
+        gt = torch.rand(rays.shape[0], 3, generator=g) * 0.5 + 0.25
+        us, up = torch.rand(rays.shape[0], 64, generator=g), torch.rand(rays.shape[0], 128, generator=g)
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.float16):
+            loss = compute_mse_loss(P, model, {"rays": rays.to(DEV), "rgbs": gt.to(DEV)}, u_strat=us.to(DEV),
+                                    u_pdf=up.to(DEV))
+        scaler.scale(loss).backward()
+        scaler.unscale_(opt)
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        scaler.step(opt)
+        scaler.update()
+        lref = ot.step(rays, gt, 64, n_importance=128, training=True, u_strat=us, u_pdf=up)
+        o32.step(rays, gt, 64, n_importance=128, training=True, u_strat=us, u_pdf=up)
+        print(f"step {step}: loss {loss.item():.7f} vs oracle AMP {float(lref):.7f}, scale {scaler.get_scale():.0f} / "
+              f"{ot.loss_scale:.0f}")
+        assert abs(loss.item() - float(lref)) <= 1e-3 * float(lref), (step, loss.item(), float(lref))
+        assert scaler.get_scale() == ot.loss_scale
+    worst = (0.0, "")
+    d16, d32 = 0.0, 0.0
+    for k, net in enumerate((model.coarse, model.fine)):
+        for n, q in net.named_parameters():
+            a = q.detach().double().cpu()
+            r = ot.nets[k][n].detach().double()
+            err = float((a - r).norm() / r.norm().clamp_min(1e-30))
+            worst = max(worst, (err, f"net{k} {n}"))
+            assert err <= 5e-3, f"net {k} {n}: relative error norm {err:.3e} after 6 AMP steps"
+            d16 += float((a - r).pow(2).sum())
+            d32 += float((a - o32.nets[k][n].detach().double()).pow(2).sum())
+    print(f"after 6 AMP steps: worst per-tensor parameter relative error norm {worst[0]:.3e} ({worst[1]}); "
+          f"distance to the AMP oracle {d16 ** 0.5:.3e}, to the fp32 oracle {d32 ** 0.5:.3e}")
+    assert d16 < d32, (d16, d32)

@@ -4,8 +4,9 @@
 set -o pipefail
 # Counters are collected on this library's MLP kernels only (PMC_FILTER -> --kernel-include-regex; PMC_FILTER= collects
 # on every dispatch): with every dispatch counted, rocprofv3 7.2 faults inside librocprofiler-sdk after a few hundred to
-# a few thousand train steps (DESIGN.md §4 "rocprofv3 PMC"), so round 4 had to drop the C4 / C5 legs; with the filter
-# the full bench, C4 and C5 legs included, completes.  LEG_ARGS adds leg flags (e.g. "--no-llff --no-sweep").
+# a few thousand train steps (DESIGN.md §4 "rocprofv3 PMC"), so round 4 had to drop the C4 / C5 legs.  The filter
+# lowers the rate; these short passes (2-3 steps per leg) stay far below it.  A pass over the whole bench also needs
+# --kernel-iteration-range (tools/r05_profiles.sh).  LEG_ARGS adds leg flags (e.g. "--no-llff --no-sweep").
 PMC_FILTER=${PMC_FILTER-"x6|gemm|bwd_layer|mlp_fwd_fused|tail|color_bwd|head_bwd|reduce_"}
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp

@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 O=gpurun_out/r05; mkdir -p $O; export TMPDIR=/tmp
-if [ -n "$PMC_ONLY" ]; then SKIP_TESTS=1; SKIP_BENCH=1; SKIP_PROF=1; fi
+if [ -n "$PMC_ONLY" ] || [ -n "$FULL_PMC_ONLY" ]; then SKIP_TESTS=1; SKIP_BENCH=1; SKIP_PROF=1; fi
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu_all.log 2>&1 || { tail -30 $O/pytest_gpu_all.log; exit 1; }
   tail -1 $O/pytest_gpu_all.log
@@ -35,6 +35,7 @@ rm -f $O/prof_amp/run_kernel_trace.csv
 grep -E "^(fp16|bf16)" $O/amp_ab.log
 fi
 [ -n "$STOP_AFTER_PROF" ] && exit 0
+if [ -z "$FULL_PMC_ONLY" ]; then
 # the per-kernel PMC passes need only the C2 / C3 legs (the full-bench pass at the end runs every leg)
 export LEG_ARGS="--no-llff --no-sweep"
 PMC_OUT=$O/pmc_fp32 PMC_BENCH_ARGS="--no-dropin --no-other-precision --no-native-ref" bash tools/pmc_traffic.sh > $O/pmc_fp32.txt 2>&1 || { tail -20 $O/pmc_fp32.txt; exit 1; }
@@ -46,10 +47,13 @@ VARIANTS=split bash tools/pmc_split.sh > $O/pmc_split.txt 2>&1 || { tail -20 $O/
 tail -n 4 $O/pmc_split.txt | cut -c1-200
 find $O gpurun_out/pmc_split_split -name "*.csv" -size +4M -delete 2>/dev/null
 unset LEG_ARGS
+fi
+[ -n "$SKIP_FULL_PMC" ] && exit 0
 # one PMC pass over the whole default bench (every leg: C2, C3 + drop-ins, C4, C5 sweep, NGP, container, PSNR) with the
-# counters on this library's MLP kernels (DESIGN.md §4 "rocprofv3 PMC")
+# counters on the first 100 dispatches of each of this library's MLP kernels (DESIGN.md §4 "rocprofv3 PMC": the kernel
+# filter alone still faulted, 800 steps into the fp32 PSNR training)
 F="x6|gemm|bwd_layer|mlp_fwd_fused|tail|color_bwd|head_bwd|reduce_"
-timeout -s KILL 1000 rocprofv3 --kernel-include-regex "$F" --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
+timeout -s KILL 1000 rocprofv3 --kernel-include-regex "$F" --kernel-iteration-range "${PMC_ITER:-[1-100]}" --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
   --kernel-trace --output-format csv -d $O/pmc_full -o run -- python3 bench.py > $O/pmc_full_bench.log 2>&1
 rc=$?; echo "PMC pass over the full bench: rc=$rc"; tail -1 $O/pmc_full_bench.log | cut -c1-300
 python3 - <<'PY'
