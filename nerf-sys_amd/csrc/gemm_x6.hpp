@@ -33,6 +33,11 @@ __device__ __forceinline__ void x6_split4(const float4 v, uint2& h, uint2& m, ui
   h = m = l = make_uint2(__float_as_uint(v.x), __float_as_uint(v.y));
   return;
 #endif
+#ifdef NERF_X6_CHEAPSPLIT  // ablation builds only: the hi pieces as all three (realistic operand values, 1/5 of the
+  // split's VALU; wrong results) — does the split's VALU hold the kernels?
+  h = m = l = make_uint2(x6_pack(v.x, v.y), x6_pack(v.z, v.w));
+  return;
+#endif
   const uint32_t h0 = x6_pack(v.x, v.y), h1 = x6_pack(v.z, v.w);
   const float r0 = v.x - nerf_bf16_lo(h0), r1 = v.y - nerf_bf16_hi(h0);
   const float r2 = v.z - nerf_bf16_lo(h1), r3 = v.w - nerf_bf16_hi(h1);
