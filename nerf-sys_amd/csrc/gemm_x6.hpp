@@ -27,7 +27,17 @@ __device__ __forceinline__ uint32_t x6_pack(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(x6_f32x2{a, b}, x6_bf16x2));
 }
 
-// four fp32 values -> their hi / mid / lo bf16 pieces, packed in pairs (v_cvt_pk_bf16_f32 rounds to nearest even)
+// four fp32 values -> their hi / mid / lo bf16 pieces, packed in pairs (v_cvt_pk_bf16_f32 rounds to nearest even).
+// DOT2: each residual x - piece by one v_dot2c_f32_bf16 against (-1, 0) / (0, -1) instead of widening the piece
+// (shift / mask) and a packed subtract: 7 VALU instructions per pair instead of 9, exact (the difference is an fp32
+// number), so the pieces are bitwise the same.  Measured (C2, profiles/r05/x6_variants_ab.txt): on every split kernel
+// forward 0.574 -> 0.566 ms, input gradient unchanged, weight gradient 0.479 -> 0.515 ms (its split sits in the staging
+// path, where the dot's longer latency shows); on the forward alone within the noise (C2 224.0-224.9k either way).
+// Off by default (NERF_X6_DOT2_FWD=1: the forward on the dot form).
+#ifndef NERF_X6_DOT2_FWD
+#define NERF_X6_DOT2_FWD 0
+#endif
+template <bool DOT2 = false>
 __device__ __forceinline__ void x6_split4(const float4 v, uint2& h, uint2& m, uint2& l) {
 #ifdef NERF_X6_NOSPLIT  // ablation builds only: split cost probe (wrong results)
   h = m = l = make_uint2(__float_as_uint(v.x), __float_as_uint(v.y));
@@ -38,6 +48,34 @@ __device__ __forceinline__ void x6_split4(const float4 v, uint2& h, uint2& m, ui
   h = m = l = make_uint2(x6_pack(v.x, v.y), x6_pack(v.z, v.w));
   return;
 #endif
+#ifdef NERF_X6_DOT2SPLIT  // A/B builds: every split kernel on the dot form
+  if constexpr (true) {
+#else
+  if constexpr (DOT2) {
+#endif
+    typedef __bf16 b2_ __attribute__((ext_vector_type(2)));
+    // the (-1, 0) / (0, -1) pairs as SGPR values: as a VOP2 inline constant "-1.0" the hardware does not read (-1, 0)
+    uint32_t c0_, c1_;
+    asm("s_mov_b32 %0, 0xbf80" : "=s"(c0_));  // (not volatile: hoisted out of the loops)
+    asm("s_mov_b32 %0, 0xbf800000" : "=s"(c1_));
+    const b2_ e0 = __builtin_bit_cast(b2_, c0_), e1 = __builtin_bit_cast(b2_, c1_);
+    auto res = [&](uint32_t p, float x0, float x1, float& y0, float& y1) __attribute__((always_inline)) {
+      const b2_ q = __builtin_bit_cast(b2_, p);
+      y0 = __builtin_amdgcn_fdot2_f32_bf16(q, e0, x0, false);
+      y1 = __builtin_amdgcn_fdot2_f32_bf16(q, e1, x1, false);
+    };
+    const uint32_t h0 = x6_pack(v.x, v.y), h1 = x6_pack(v.z, v.w);
+    float r0, r1, r2, r3, s0, s1, s2, s3;
+    res(h0, v.x, v.y, r0, r1);
+    res(h1, v.z, v.w, r2, r3);
+    const uint32_t m0 = x6_pack(r0, r1), m1 = x6_pack(r2, r3);
+    res(m0, r0, r1, s0, s1);
+    res(m1, r2, r3, s2, s3);
+    h = make_uint2(h0, h1);
+    m = make_uint2(m0, m1);
+    l = make_uint2(x6_pack(s0, s1), x6_pack(s2, s3));
+    return;
+  }
   const uint32_t h0 = x6_pack(v.x, v.y), h1 = x6_pack(v.z, v.w);
   const float r0 = v.x - nerf_bf16_lo(h0), r1 = v.y - nerf_bf16_hi(h0);
   const float r2 = v.z - nerf_bf16_lo(h1), r3 = v.w - nerf_bf16_hi(h1);
@@ -539,8 +577,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
 #pragma unroll
           for (int a = 0; a < TM; ++a) {
             uint2 h0, m0_, l0, h1, m1, l1;
-            x6_split4(rj[a][ks][0], h0, m0_, l0);
-            x6_split4(rj[a][ks][1], h1, m1, l1);
+            x6_split4<NERF_X6_DOT2_FWD && !BIGSMALL>(rj[a][ks][0], h0, m0_, l0);
+            x6_split4<NERF_X6_DOT2_FWD && !BIGSMALL>(rj[a][ks][1], h1, m1, l1);
             af[a][0] = __builtin_bit_cast(nerf_bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
             af[a][1] = __builtin_bit_cast(nerf_bf16x8, make_uint4(m0_.x, m0_.y, m1.x, m1.y));
             af[a][2] = __builtin_bit_cast(nerf_bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
