@@ -97,34 +97,57 @@ inline int ld_of(const WS& w, int i) { return (i == 3) ? 320 : 256; }
 // ------------------------------------------------------------------ elementwise kernels
 
 // xyz positional encoding of x_d[:, :3] into X3E cols 256..319 (pad col 319 = 0; rows >= M zero).
-// One thread per sample row: the 64 encoded values leave as 16 float4 stores (256 contiguous bytes).
-__global__ void pe_xyz_kernel(const float* __restrict__ xd, int64_t M, int64_t Mp, float* __restrict__ X3E) {
-  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= Mp) return;
-  float4* q4 = reinterpret_cast<float4*>(X3E + m * 320 + 256);
-  if (m >= M) {
-#pragma unroll
-    for (int c = 0; c < 16; ++c) q4[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-    return;
-  }
+// One thread per sample row computes its 64 values; a wave's 64 rows then leave through a per-wave LDS tile, 32 columns
+// at a time, so that each store instruction writes 8 rows x 128 B (whole lines) instead of one 16-B piece of each of
+// 64 rows 1280 B apart.  Same values, same bits.  Against the row-per-lane stores it measured within the noise (C2
+// 225.3k vs 225.2k, profiles/r05/x6_variants_ab.txt): the kernel is bound by its 30 libm sincosf per row.  Tile pitch
+// 33 floats: the row-per-lane writes of a column hit 64 distinct banks.
+constexpr int PE_TP = 33;
+__global__ __launch_bounds__(256) void pe_xyz_kernel(const float* __restrict__ xd, int64_t M, int64_t Mp,
+                                                     float* __restrict__ X3E) {
+  __shared__ float tile[4][64 * PE_TP];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t m0 = ((int64_t)blockIdx.x * 4 + wv) * 64;  // this wave's first row (Mp is a multiple of 256)
+  if (m0 >= Mp) return;  // wave-uniform
+  const int64_t m = m0 + lane;
   float v[64];
-  const float x[3] = {xd[m * 6], xd[m * 6 + 1], xd[m * 6 + 2]};
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    v[k] = x[k];
-    float band = 1.0f;
+  for (int c = 0; c < 64; ++c) v[c] = 0.f;
+  if (m < M) {
+    const float x[3] = {xd[m * 6], xd[m * 6 + 1], xd[m * 6 + 2]};
 #pragma unroll
-    for (int l = 0; l < 10; ++l) {
-      float s, c;
-      sincosf(x[k] * band, &s, &c);
-      v[3 + k * 20 + l] = c;
-      v[3 + k * 20 + 10 + l] = s;
-      band *= 2.0f;
+    for (int k = 0; k < 3; ++k) {
+      v[k] = x[k];
+      float band = 1.0f;
+#pragma unroll
+      for (int l = 0; l < 10; ++l) {
+        float s, c;
+        sincosf(x[k] * band, &s, &c);
+        v[3 + k * 20 + l] = c;
+        v[3 + k * 20 + 10 + l] = s;
+        band *= 2.0f;
+      }
     }
   }
-  v[63] = 0.f;
+  float* t = tile[wv];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) q4[c] = make_float4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
+  for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+    for (int c = 0; c < 32; ++c) t[lane * PE_TP + c] = v[32 * hf + c];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // store i: rows 8 i + (lane >> 3), float4 (lane & 7) of the half
+      const int r = 8 * i + (lane >> 3), q = lane & 7;
+      const float* src = t + r * PE_TP + 4 * q;
+      *reinterpret_cast<float4*>(X3E + (m0 + r) * 320 + 256 + 32 * hf + 4 * q) =
+          make_float4(src[0], src[1], src[2], src[3]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
 }
 
 // batched transpose: dst_i[c][r] = src_i[r][c] for r < rows_i, c < cols_i  (src pitch lds_i)
@@ -371,7 +394,7 @@ extern "C" int nerf_mlp_fwd_ex(const float* w, const float* x_d, int64_t M, floa
   const int64_t Mp = W.Mp;
   auto Wt = [&](int t) { return w + L.off[t]; };
 
-  pe_xyz_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(x_d, M, Mp, W.X3E);
+  pe_xyz_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(x_d, M, Mp, W.X3E);  // 4 waves x 64 rows
   if (!native) {  // this call's weights as bf16 piece planes
     X6Jobs jobs{};
     for (int i = 0; i < 8; ++i)
