@@ -299,9 +299,10 @@ __device__ __forceinline__ uint32_t relu_pk(float x, float y) {
 }
 
 // fp16 build: the output pair of accumulator registers (r, r + 1) — both fp16-rounded in one v_cvt_pk_f16_f32,
-// widened, the fp32 bias pair added in one v_pk_add_f32 — then relu_pk.  The scalar form (acc_out per element: two
-// converts and an add each) made the fp16 training forward 20 % slower than the bf16 one (750 vs 627 us per launch,
-// profiles/r05/prof_amp_summary.txt).  bf16 build: relu_pk of the accumulators (the bias is in them already).
+// widened, the fp32 bias pair added in one v_pk_add_f32 — then relu_pk.  (hipcc had already paired the scalar form
+// the same way; written on pairs, 5 spilled VGPRs went away and the time stayed: 750 us per training launch against
+// 656 us for the bf16 build, whose bias sits in the accumulators — profiles/r05/prof_amp_summary.txt)
+// bf16 build: relu_pk of the accumulators.
 __device__ __forceinline__ uint32_t relu_pk_out(float a0, float a1, float b0, float b1) {
 #if NERF_F16
   const nerf_f16x2 h = __builtin_convertvector(nerf_f32x2{a0, a1}, nerf_f16x2);
