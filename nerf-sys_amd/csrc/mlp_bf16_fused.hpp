@@ -304,7 +304,16 @@ __device__ __forceinline__ uint32_t relu_pk(float x, float y) {
 // 656 us for the bf16 build, whose bias sits in the accumulators — profiles/r05/prof_amp_summary.txt)
 // bf16 build: relu_pk of the accumulators.
 __device__ __forceinline__ uint32_t relu_pk_out(float a0, float a1, float b0, float b1) {
-#if NERF_F16
+#if NERF_F16 && !defined(NERF_F16_NOMIX)
+  // fp32(fp16 value) + bias in ONE v_fma_mix_f32 per element (f16 source x 1.0 + f32 bias, one fp32 rounding of the
+  // exact sum = the fp32 add), instead of a widening convert + half a v_pk_add_f32: hipcc folds fmaf(x, 1, b) into an
+  // add and never selects the mixed form
+  const uint32_t hb = __builtin_bit_cast(uint32_t, __builtin_convertvector(nerf_f32x2{a0, a1}, nerf_f16x2));
+  float z0, z1;
+  asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(z0) : "v"(hb), "v"(b0));
+  asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(z1) : "v"(hb), "v"(b1));
+  return relu_pk(z0, z1);
+#elif NERF_F16
   const nerf_f16x2 h = __builtin_convertvector(nerf_f32x2{a0, a1}, nerf_f16x2);
   const nerf_f32x2 x = __builtin_convertvector(h, nerf_f32x2) + nerf_f32x2{b0, b1};
   return relu_pk(x[0], x[1]);
