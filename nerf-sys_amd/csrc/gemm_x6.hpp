@@ -382,8 +382,11 @@ constexpr bool defined_regb() {
   return false;
 #endif
 }
+// TN_: 32-column blocks per wave (= the workgroup's columns / 32).  TN_ = 8 with TM = 1 (A/B builds,
+// NERF_X6_FWD_TN8): 256 x 256 tiles of 32 x 256 waves, so each activation row is split by ONE workgroup instead of one
+// per 128-column tile, at the same per-accumulator MFMA order (bitwise the same outputs).
 template <int EPI, int BK = 32, int NW = 8, bool BIGSMALL = false, int TM = 2, int MINW = (BIGSMALL ? 1 : 8 / NW),
-          int NKC = 0>
+          int NKC = 0, int TN_ = 4>
 __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float* __restrict__ A, int lda,
                                                                      const nerf_bf16* __restrict__ Bp, int ldb,
                                                                      int64_t bplane, const float* __restrict__ bias,
@@ -392,7 +395,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
                                                                      uint32_t* __restrict__ mbits_out, int K,
                                                                      int n_ntiles) {
   constexpr int NT = 64 * NW;                     // threads
-  constexpr int WTM = 32 * TM, BM = WTM * NW, BN = 128, WTN = 128, TN = 4;
+  constexpr int WTM = 32 * TM, BM = WTM * NW, TN = TN_, BN = 32 * TN_, WTN = BN;
   constexpr int KS = BK / 16, CPR = BK / 8;       // MFMA k-steps / 16-B weight chunks per row, per slab
   constexpr int BCH = 3 * BN * CPR / NT;          // weight chunks per thread per slab
 #ifndef NERF_X6W_REGB

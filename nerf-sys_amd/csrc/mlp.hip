@@ -276,6 +276,14 @@ int nt_x6(const float* A, int lda, const nerf_bf16* Bp, int ldb, int64_t bplane,
 #define NERF_X6_DG_NW 8
 #endif
     constexpr int DGM = 32 * NERF_X6_DG_NW;
+#ifdef NERF_X6_DG_TN8  // A/B builds: input gradient on 128 x 256 tiles of 32 x 256 waves, one wave per SIMD (both
+    // accumulator sets, 256 registers, need the whole register file): each row split once instead of twice
+    if (M % 128 == 0 && K == 256 && N % 256 == 0) {
+      gemm_nt_x6w_kernel<EPI, 32, 4, true, 1, 1, 8, 8><<<(unsigned)((M / 128) * (N / 256)), 256, 0, st>>>(
+          A, lda, Bp, ldb, bplane, bias, C, ldc, mbits, N / 32, mbits_out, K, N / 256);
+      return NERF_OK;
+    }
+#endif
 #ifndef NERF_X6W_NOA3  // three activation register sets, K = 256 unrolled (NERF_X6W_NOA3: the two-set loop, A/B builds)
     // (profiles/r04/x6_a3_ab.txt: 0.597 -> 0.584 ms per fine launch, C2 +0.5 %, bitwise the same)
     if (M % DGM == 0 && K == 256) {
@@ -303,6 +311,19 @@ int nt_x6(const float* A, int lda, const nerf_bf16* Bp, int ldb, int64_t bplane,
       return NERF_OK;
     }
   }
+#ifndef NERF_X6_FWD_TN8  // forward on 256 x 256 tiles of 32 x 256 waves: each activation row is split by one workgroup
+// instead of two (one per 128-column tile), at the same per-accumulator MFMA order — bitwise the same outputs.  C2 on
+// one box (profiles/r05/x6_variants_ab.txt): fwd 0.572 -> 0.539 ms per fine layer, 228.6k -> 233.0k rays/s.
+// NERF_X6_FWD_TN8=0 (A/B builds): the 512 x 128 tiles of 64 x 128 waves.
+#define NERF_X6_FWD_TN8 1
+#endif
+#if NERF_X6_FWD_TN8
+  if (EPI == EPI_BIAS_RELU && N % 256 == 0 && M % 256 == 0 && K % 64 == 0) {
+    gemm_nt_x6w_kernel<EPI, 32, 8, false, 1, 1, 0, 8><<<(unsigned)((M / 256) * (N / 256)), 512, 0, st>>>(
+        A, lda, Bp, ldb, bplane, bias, C, ldc, mbits, N / 32, mbits_out, K, N / 256);
+    return NERF_OK;
+  }
+#endif
 #ifdef NERF_X6_FWD_W12  // A/B builds: forward on 32-row waves, NERF_X6_FWD_W12 (12 or 16) per workgroup (3 / 4 per SIMD)
   if (EPI == EPI_BIAS_RELU && M % (32 * NERF_X6_FWD_W12) == 0 && K % 64 == 0) {
     gemm_nt_x6w_kernel<EPI, 32, NERF_X6_FWD_W12, false, 1, 1><<<(unsigned)((M / (32 * NERF_X6_FWD_W12)) * ntn),
