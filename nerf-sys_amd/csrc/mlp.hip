@@ -318,6 +318,13 @@ int nt_x6(const float* A, int lda, const nerf_bf16* Bp, int ldb, int64_t bplane,
 #define NERF_X6_FWD_TN8 1
 #endif
 #if NERF_X6_FWD_TN8
+#ifdef NERF_X6_FWD_A3  // A/B builds: the K = 256 forward layers on three activation register sets (the A3 loop)
+  if (EPI == EPI_BIAS_RELU && N % 256 == 0 && M % 256 == 0 && K == 256) {
+    gemm_nt_x6w_kernel<EPI, 32, 8, false, 1, 1, 8, 8><<<(unsigned)((M / 256) * (N / 256)), 512, 0, st>>>(
+        A, lda, Bp, ldb, bplane, bias, C, ldc, mbits, N / 32, mbits_out, K, N / 256);
+    return NERF_OK;
+  }
+#endif
   if (EPI == EPI_BIAS_RELU && N % 256 == 0 && M % 256 == 0 && K % 64 == 0) {
     gemm_nt_x6w_kernel<EPI, 32, 8, false, 1, 1, 0, 8><<<(unsigned)((M / 256) * (N / 256)), 512, 0, st>>>(
         A, lda, Bp, ldb, bplane, bias, C, ldc, mbits, N / 32, mbits_out, K, N / 256);
