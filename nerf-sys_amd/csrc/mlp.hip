@@ -16,6 +16,7 @@
 //   transposed trunk weights, and S split-M partial slabs of the packed gradient.
 #include "gemm.hpp"
 #include "gemm_x6.hpp"
+#include "gemm_x6s.hpp"
 #include "mlp_common.hpp"
 #include "mlp_tail.hpp"
 #include "mlp_fwd_tail.hpp"
@@ -276,6 +277,12 @@ int nt_x6(const float* A, int lda, const nerf_bf16* Bp, int ldb, int64_t bplane,
 #define NERF_X6_DG_NW 8
 #endif
     constexpr int DGM = 32 * NERF_X6_DG_NW;
+#ifdef NERF_X6_DG_SHARED  // A/B builds: 128 x 256 tiles, each activation slab split once and shared (gemm_x6s.hpp)
+    if (M % 128 == 0 && K == 256 && N == 256 && EPI == EPI_MASK) {
+      gemm_nt_x6s_kernel<EPI, 8><<<(unsigned)(M / 128), 512, 0, st>>>(A, lda, Bp, ldb, bplane, C, ldc, mbits, N / 32);
+      return NERF_OK;
+    }
+#endif
 #ifdef NERF_X6_DG_TN8  // A/B builds: input gradient on 128 x 256 tiles of 32 x 256 waves, one wave per SIMD (both
     // accumulator sets, 256 registers, need the whole register file): each row split once instead of twice
     if (M % 128 == 0 && K == 256 && N % 256 == 0) {

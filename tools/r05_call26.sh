@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 5, call 26: the input gradient with each activation slab split once and shared by two column halves (-DNERF_X6_DG_SHARED):
+# parity on the variant, bitwise fp32 outputs of the two builds, then the C2 A/B.
+set -o pipefail
+cd "$(dirname "$0")/.."
+O=gpurun_out/r05; mkdir -p $O; export TMPDIR=/tmp
+NERF_AMD_LIB=exp/dgsh.so timeout -k 10 300 python -u -m pytest tests/test_gpu_split_gemm.py tests/test_gpu_c2_backward.py tests/test_gpu_parity.py -m gpu -q \
+  --timeout 240 --timeout-method thread > $O/pytest_dgsh.log 2>&1; rc=$?; tail -2 $O/pytest_dgsh.log; grep -E "FAIL|Error" $O/pytest_dgsh.log | head -5
+[ $rc -ne 0 ] && exit 1
+NERF_AMD_LIB=exp/dgsh.so timeout -k 10 120 python tools/lib_outputs.py --precision fp32 --out $O/dgsh.pt > $O/lo_dgsh.log 2>&1 || { tail $O/lo_dgsh.log; exit 1; }
+NERF_AMD_LIB=exp/x6base.so timeout -k 10 120 python tools/lib_outputs.py --precision fp32 --out $O/base.pt > $O/lo_base.log 2>&1 || { tail $O/lo_base.log; exit 1; }
+python tools/lib_outputs.py --compare $O/dgsh.pt $O/base.pt; rm -f $O/dgsh.pt $O/base.pt
+VARIANTS="x6base dgsh" ROUNDS=3 timeout -k 10 800 bash tools/ab_x6.sh
