@@ -937,8 +937,8 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_x6_kernel(const float* __re
 // 128 x 128-tile form reads them twice, PMC 2.30 GB against 1.68 GB algorithmic per fine launch) and every element is
 // split once; eight waves of 64 (n) x 128 (k) (2 x 4 MFMA tiles) amortise each G fragment over four X fragments.
 // 16-row slabs, six piece images [16][288] bf16 per stage, double-buffered (108 KiB: one workgroup per CU, two waves
-// per SIMD); the loads of slab it + 2 are issued at iteration it (two register sets).  The tiles of waves wk == 0 also
-// sum the bias columns.  Requirements: rows_per_split % 16 == 0, M % 16 == 0, ldg / ldx % 4 == 0, K >= 256 (the first
+// per SIMD); the loads of slab it + 2 are issued at iteration it (two register sets; three were slower,
+// 0.477 -> 0.512 ms, NERF_X6W_PF3).  Tile a == wk of each wave also sums its bias columns.  Requirements: rows_per_split % 16 == 0, M % 16 == 0, ldg / ldx % 4 == 0, K >= 256 (the first
 // 256 columns of X).
 __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __restrict__ G, int ldg,
                                                                const float* __restrict__ X, int ldx,
@@ -957,10 +957,19 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave >> 1, wk = wave & 1;
   const int li = lane & 31, lh = lane >> 5;
-  const bool do_bias = (Pb != nullptr) && wk == 0;
+  // bias columns: wave (wn, wk) sums those of its G tile a == wk, so both waves of a column pair do half of the VALU
+  // work (summing both tiles in the wk == 0 waves left the wk == 1 waves idle at each slab's barrier: 0.477 -> 0.445 ms
+  // per fine layer, bitwise the same, profiles/r05/x6_variants_ab.txt)
+  const bool do_bias = Pb != nullptr;
+  auto bias_tile = [&](int a) { return a == wk; };
 
   // staging: a 16 x 256 fp32 slab = 1024 float4, thread f = tid + 512 i: row f >> 6, float4 f & 63
-  float4 rg[2][2], rx[2][2];
+#ifdef NERF_X6W_PF3  // A/B builds: three register sets, the loads of slab it + 3 issued at iteration it
+  constexpr int PF = 3;
+#else
+  constexpr int PF = 2;
+#endif
+  float4 rg[PF][2], rx[PF][2];
 #define WX6W_GLOAD(set_, m_)                                                                               \
   _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                          \
     const int f = tid + 512 * i;                                                                           \
@@ -1006,18 +1015,19 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
 
   const int64_t nit = (r1 - r0) / MR;
   if (nit > 0) {
-    WX6W_GLOAD(0, r0);
-    WX6W_GLOAD(1, r0 + (nit > 1 ? 1 : 0) * MR);
+#pragma unroll
+    for (int j = 0; j < PF; ++j) WX6W_GLOAD(j, r0 + (j < nit ? j : nit - 1) * MR);
     WX6W_SSTORE(0, 0);
   }
   __syncthreads();
-  for (int64_t it0 = 0; it0 < nit; it0 += 2) {
+  for (int64_t it0 = 0; it0 < nit; it0 += PF) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {  // slab it = it0 + j: LDS buffer j, register set j
+    for (int j = 0; j < PF; ++j) {  // slab it = it0 + j: LDS buffer it & 1, register set j
       const int64_t it = it0 + j;
       if (it >= nit) break;
-      WX6W_GLOAD(j, r0 + (it + 2 < nit ? it + 2 : nit - 1) * MR);
-      const nerf_bf16* Gs = smem + j * STAGE;
+      WX6W_GLOAD(j, r0 + (it + PF < nit ? it + PF : nit - 1) * MR);
+      const int buf = PF == 2 ? j : (int)(it & 1);
+      const nerf_bf16* Gs = smem + buf * STAGE;
       const nerf_bf16* Xs = Gs + 3 * IMG;
       nerf_bf16x8 af[TM][3];
 #pragma unroll
@@ -1027,7 +1037,7 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
       if (do_bias) {
 #pragma unroll
         for (int a = 0; a < TM; ++a)
-          {  // the slab's 8 rows summed first, then added to the running sum
+          if (bias_tile(a)) {  // the slab's 8 rows summed first, then added to the running sum
             float t8 = 0.f;
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) t8 += ((float)af[a][0][jj] + (float)af[a][1][jj]) + (float)af[a][2][jj];
@@ -1040,7 +1050,7 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
         // slab they fill the free buffer), and the group barriers below interleave their VALU work one MFMA at a time
         // with the second pair's MFMAs instead of leaving it between the last MFMA and the barrier: 0.52 -> 0.47 ms
         // per fine layer on MI355X (profiles/r03/x6_wgrad_interleave_ab.txt), bitwise the same results
-        if (bp == 1) WX6W_SSTORE((j + 1) & 1, (j + 1) & 1);
+        if (bp == 1) WX6W_SSTORE((j + 1) % PF, buf ^ 1);
         nerf_bf16x8 bf[2][3];
 #pragma unroll
         for (int pc = 0; pc < 3; ++pc)
@@ -1088,7 +1098,7 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
       const float v = bsum[a] + __shfl_xor(bsum[a], 32, 64);
-      if (lh == 0) Pb[(int64_t)s * slab + wn * WTN + a * 32 + li] = v;
+      if (lh == 0 && bias_tile(a)) Pb[(int64_t)s * slab + wn * WTN + a * 32 + li] = v;
     }
   }
 }
