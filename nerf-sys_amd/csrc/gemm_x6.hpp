@@ -938,7 +938,7 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_x6_kernel(const float* __re
 // split once; eight waves of 64 (n) x 128 (k) (2 x 4 MFMA tiles) amortise each G fragment over four X fragments.
 // 16-row slabs, six piece images [16][288] bf16 per stage, double-buffered (108 KiB: one workgroup per CU, two waves
 // per SIMD); the loads of slab it + 2 are issued at iteration it (two register sets; three were slower,
-// 0.477 -> 0.512 ms, NERF_X6W_PF3).  Tile a == wk of each wave also sums its bias columns.  Requirements: rows_per_split % 16 == 0, M % 16 == 0, ldg / ldx % 4 == 0, K >= 256 (the first
+// 0.477 -> 0.512 ms, NERF_X6W_PF3).  The bias columns are summed from the raw staging registers.  Requirements: rows_per_split % 16 == 0, M % 16 == 0, ldg / ldx % 4 == 0, K >= 256 (the first
 // 256 columns of X).
 __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __restrict__ G, int ldg,
                                                                const float* __restrict__ X, int ldx,
@@ -957,11 +957,14 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave >> 1, wk = wave & 1;
   const int li = lane & 31, lh = lane >> 5;
-  // bias columns: wave (wn, wk) sums those of its G tile a == wk, so both waves of a column pair do half of the VALU
-  // work (summing both tiles in the wk == 0 waves left the wk == 1 waves idle at each slab's barrier: 0.477 -> 0.445 ms
-  // per fine layer, bitwise the same, profiles/r05/x6_variants_ab.txt)
-  const bool do_bias = Pb != nullptr;
-  auto bias_tile = [&](int a) { return a == wk; };
+  // bias columns: summed from the raw fp32 G values in the staging registers, 8 FMAs per thread and slab (thread tid
+  // holds columns 4 (tid & 63) .. + 3 of rows tid >> 6 (mod 8)), the eight waves' partials added in wave order at the
+  // end.  Round 4 summed the three pieces of each MFMA fragment in the wk == 0 waves (48 VALU per tile and slab, the
+  // wk == 1 waves idle at the barrier meanwhile): 0.477 ms per fine layer -> 0.445 with the tiles shared by both waves
+  // -> 0.426 ms summed raw (profiles/r05/x6_variants_ab.txt; the bias gradients' summation order changed, ~1e-7 of
+  // their scale)
+  const bool braw = Pb != nullptr;
+  float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
   // staging: a 16 x 256 fp32 slab = 1024 float4, thread f = tid + 512 i: row f >> 6, float4 f & 63
 #ifdef NERF_X6W_PF3  // A/B builds: three register sets, the loads of slab it + 3 issued at iteration it
@@ -991,6 +994,13 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
     *reinterpret_cast<uint2*>(S_ + 4 * IMG + o) = m;                                                       \
     *reinterpret_cast<uint2*>(S_ + 5 * IMG + o) = l;                                                       \
   }
+#define WX6W_BACC(set_, sc_)                                                                               \
+  _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                          \
+    b4.x = fmaf(rg[set_][i].x, (sc_), b4.x);                                                               \
+    b4.y = fmaf(rg[set_][i].y, (sc_), b4.y);                                                               \
+    b4.z = fmaf(rg[set_][i].z, (sc_), b4.z);                                                               \
+    b4.w = fmaf(rg[set_][i].w, (sc_), b4.w);                                                               \
+  }
 
   nerf_f32x16 acc[TM][TN];
 #pragma unroll
@@ -999,10 +1009,6 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
     for (int b = 0; b < TN; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  float bsum[TM];
-#pragma unroll
-  for (int a = 0; a < TM; ++a) bsum[a] = 0.f;
-
   const int grp = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
   const int trow = 8 * (grp >> 1) + q, tcol = 16 * (grp & 1) + 4 * p4;
   auto tr_frag = [&](const nerf_bf16* base) {
@@ -1018,6 +1024,7 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
 #pragma unroll
     for (int j = 0; j < PF; ++j) WX6W_GLOAD(j, r0 + (j < nit ? j : nit - 1) * MR);
     WX6W_SSTORE(0, 0);
+    if (braw) WX6W_BACC(0, 1.f);
   }
   __syncthreads();
   for (int64_t it0 = 0; it0 < nit; it0 += PF) {
@@ -1034,16 +1041,6 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
       for (int pc = 0; pc < 3; ++pc)
 #pragma unroll
         for (int a = 0; a < TM; ++a) af[a][pc] = tr_frag(Gs + pc * IMG + trow * PT + wn * WTN + a * 32 + tcol);
-      if (do_bias) {
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-          if (bias_tile(a)) {  // the slab's 8 rows summed first, then added to the running sum
-            float t8 = 0.f;
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj) t8 += ((float)af[a][0][jj] + (float)af[a][1][jj]) + (float)af[a][2][jj];
-            bsum[a] += t8;
-          }
-      }
 #pragma unroll
       for (int bp = 0; bp < TN / 2; ++bp) {  // column-block pairs: 2 x 3 X fragments live
         // the next slab's split + LDS stores go between the two column-block pairs (unconditionally: past the last
@@ -1051,6 +1048,8 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
         // with the second pair's MFMAs instead of leaving it between the last MFMA and the barrier: 0.52 -> 0.47 ms
         // per fine layer on MI355X (profiles/r03/x6_wgrad_interleave_ab.txt), bitwise the same results
         if (bp == 1) WX6W_SSTORE((j + 1) % PF, buf ^ 1);
+        // slab it + 1's G values (a clamped repeat past the last slab: weight 0); x * 1 + s is the exact sum
+        if (bp == 1 && braw) WX6W_BACC((j + 1) % PF, it + 1 < nit ? 1.f : 0.f);
         nerf_bf16x8 bf[2][3];
 #pragma unroll
         for (int pc = 0; pc < 3; ++pc)
@@ -1080,6 +1079,18 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
   }
 #undef WX6W_GLOAD
 #undef WX6W_SSTORE
+#undef WX6W_BACC
+  if (braw) {  // the eight waves' partials meet in LDS (free after the loop's last barrier), added in wave order
+    float* part = reinterpret_cast<float*>(smem);
+    *reinterpret_cast<float4*>(part + wave * 256 + 4 * lane) = b4;
+    __syncthreads();
+    if (tid < 256) {
+      float v = part[tid];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) v += part[w * 256 + tid];
+      Pb[(int64_t)s * slab + tid] = v;
+    }
+  }
 
   float* Ps = P + (int64_t)s * slab;
 #pragma unroll
@@ -1092,13 +1103,6 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
         const int n = wn * WTN + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         Ps[(int64_t)n * ldp + k] = acc[a][b][r];
       }
-    }
-  }
-  if (do_bias) {
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
-      const float v = bsum[a] + __shfl_xor(bsum[a], 32, 64);
-      if (lh == 0 && bias_tile(a)) Pb[(int64_t)s * slab + wn * WTN + a * 32 + li] = v;
     }
   }
 }

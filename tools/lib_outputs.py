@@ -22,6 +22,10 @@ if a.compare:
     x, y = (torch.load(f, weights_only=True) for f in a.compare)
     bad = [k for k in x if not torch.equal(x[k], y[k])]
     print("bitwise equal" if not bad else f"DIFFER: {bad}", {k: tuple(v.shape) for k, v in x.items()})
+    for k in bad:  # largest difference relative to the array's scale, and the count of differing elements
+        d = (x[k].double() - y[k].double()).abs()
+        print(f"  {k}: {int((d > 0).sum())} differ, max |d| {d.max().item():.3e}, "
+              f"max |d| / max |y| {(d.max() / y[k].double().abs().max()).item():.3e}")
     sys.exit(1 if bad else 0)
 from nerf_amd import kernels as K  # noqa: E402
 from nerf_amd.vanilla import VanillaNeRF  # noqa: E402
