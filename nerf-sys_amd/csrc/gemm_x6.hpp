@@ -967,11 +967,7 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
   float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
   // staging: a 16 x 256 fp32 slab = 1024 float4, thread f = tid + 512 i: row f >> 6, float4 f & 63
-#ifdef NERF_X6W_PF3  // A/B builds: three register sets, the loads of slab it + 3 issued at iteration it
-  constexpr int PF = 3;
-#else
-  constexpr int PF = 2;
-#endif
+  constexpr int PF = 2;  // register sets (three, loads issued three slabs ahead, were slower: call 29)
   float4 rg[PF][2], rx[PF][2];
 #define WX6W_GLOAD(set_, m_)                                                                               \
   _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                          \
@@ -1027,13 +1023,14 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
     if (braw) WX6W_BACC(0, 1.f);
   }
   __syncthreads();
-  for (int64_t it0 = 0; it0 < nit; it0 += PF) {
-#pragma unroll
-    for (int j = 0; j < PF; ++j) {  // slab it = it0 + j: LDS buffer it & 1, register set j
-      const int64_t it = it0 + j;
-      if (it >= nit) break;
+  // slab it: LDS buffer j = it & 1, register set j.  Whole rounds of the two sets run in the loop and a last odd slab
+  // is peeled after it: with a break inside the unrolled round, a path with set 0's loads still in flight reached the
+  // loop header and the compiler's wait counting drained every load (vmcnt(0)) at the top of each round; 0.425 ->
+  // 0.421 ms per fine layer, bitwise the same (profiles/r05/x6_variants_ab.txt, call 34)
+  auto do_slab = [&](auto J, const int64_t it) __attribute__((always_inline)) {
+      constexpr int j = decltype(J)::value;
       WX6W_GLOAD(j, r0 + (it + PF < nit ? it + PF : nit - 1) * MR);
-      const int buf = PF == 2 ? j : (int)(it & 1);
+      const int buf = j;
       const nerf_bf16* Gs = smem + buf * STAGE;
       const nerf_bf16* Xs = Gs + 3 * IMG;
       nerf_bf16x8 af[TM][3];
@@ -1075,8 +1072,13 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __r
         }
       }
       __syncthreads();
-    }
+  };
+  int64_t it0 = 0;
+  for (; it0 + PF <= nit; it0 += PF) {
+    do_slab(std::integral_constant<int, 0>{}, it0);
+    do_slab(std::integral_constant<int, 1>{}, it0 + 1);
   }
+  if (it0 < nit) do_slab(std::integral_constant<int, 0>{}, it0);
 #undef WX6W_GLOAD
 #undef WX6W_SSTORE
 #undef WX6W_BACC
