@@ -23,9 +23,11 @@ Prints ONE JSON line on rank 0 (contract in the task statement), with
                   against the HBM peak, with algorithmic bytes per launch (roofline_bf16).
   bf16 / fp32   — the other MLP precision's engine step timed in the same run (BASELINE configs[2] beside
                   configs[1]), with its own roofline, step MFMA fraction and (N = 1) its drop-in loop body.
-  psnr          — (N = 1) the metric's PSNR half: both precisions' engines, from the same seed-0 weights and
+  psnr          — the metric's PSNR half: both precisions' engines, from the same seed-0 weights and
                   batches, continue to --psnr-steps total steps (outside the timed region), then render every
-                  held-out 800x800 view; mean full-image PSNR per precision and the bf16 - fp32 gap.
+                  held-out 800x800 view; mean full-image PSNR per precision and the bf16 - fp32 gap.  At N > 1 every
+                  rank trains the replica (data parallel, global batch N x 4096) and rank 0 renders it after an
+                  all-gathered parameter checksum (params_equal_across_ranks per precision).
   dp            — (N > 1) per-rank step time (max / min), HIP-event time of each all-reduce bucket, and
                   params_equal_across_ranks: an all-gathered fp64 sum + bit hash of every rank's parameters.
   llff          — BASELINE configs[3] (C4): the Fern-style 1008x756 NDC scene, same fp32 engine, --llff-steps steps.
@@ -34,12 +36,14 @@ Prints ONE JSON line on rank 0 (contract in the task statement), with
   ngp           — (N = 1) the reference's production expert (MetaNGP, 16 x 2^20 hash grid, 96 stratified samples) train
                   step: rays/s, per-kernel times, the table scatter against the float-atomic request rate, CPU oracle
                   beside it (tools/bench_ngp.py).
-  container     — (N = 1) the production MoE container (4 NGP experts + occupancy marching + background MLP,
+  container     — the production MoE container (4 NGP experts + occupancy marching + background MLP,
                   autograd + FlatAdam): rays/s, per-kernel-class times, the hash kernels' HBM roofline, CPU oracle
-                  (tools/bench_container.py).
+                  (tools/bench_container.py).  At N > 1: FlatAdam(world_size=N) with the bucketed gradient
+                  all-reduce, and a `dp` block (params_equal_across_ranks).
   cpu_baseline  — the CPU oracle (a restatement of the reference's PyTorch path, pinned to its golden
                   vectors) running the same train step (4096 rays, 64+128, 2 nets), median of >= 5 steps
-                  on this host's CPU share (rank 0, N=1); `all_cores` beside it at os.cpu_count() threads.
+                  on this host's CPU share (rank 0, after every GPU leg; at N > 1 the other ranks wait in a
+                  gloo barrier); `all_cores` beside it at os.cpu_count() threads.
   dropin        — (N=1) the reference's own loop body (an/pipelines/online_stage/runtime_adapt.py:286-310:
                   render_rays -> compute_mse_loss -> backward -> clip_grad_norm_ -> torch Adam; under
                   autocast + GradScaler for bf16) on this repo's drop-in render_rays + VanillaNeRF autograd
@@ -134,6 +138,9 @@ def parse():
                     help="skip the Instant-NGP expert sub-record (SURVEY §8f row 1, tools/bench_ngp.py)")
     ap.add_argument("--no-container", action="store_true",
                     help="skip the production MoE-container sub-record (SURVEY §8f rows 1-3, tools/bench_container.py)")
+    ap.add_argument("--container-steps", type=int, default=48, help="timed steps of the container sub-record")
+    ap.add_argument("--container-warmup", type=int, default=40,
+                    help="untimed container steps (the occupancy warm-up is half of them)")
     ap.add_argument("--prod-cpu-seconds", type=float, default=12.0,
                     help="CPU-oracle sample of the ngp / container sub-records (seconds)")
     ap.add_argument("--no-native-ref", action="store_true",
@@ -206,19 +213,35 @@ def _oracle_step_rate(S, NI, n, steps, threads, budget_s=None):
     return statistics.median(times), times
 
 
-def cpu_baseline(S, NI, n, steps):
+def _baseline_threads(world):
+    """OMP_NUM_THREADS (the box's CPU share: 16 on a one-GPU box).  Under torchrun at N > 1 an unset OMP_NUM_THREADS
+    becomes 1 per rank; rank 0 then uses the share it may run on (affinity, bounded by the cgroup quota), since
+    the other ranks sit blocked in a barrier while it runs."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and not (world > 1 and env == "1"):
+        return int(env)
+    sh = _cpu_share()
+    n = sh.get("affinity_cpus") or os.cpu_count() or 1
+    q = sh.get("cgroup_cpu_quota")
+    return max(1, min(n, int(q))) if q else n
+
+
+def cpu_baseline(S, NI, n, steps, world=1):
     """The CPU oracle's train step (same op graph: 2 nets, 64+128, MSE coarse+fine, clip, Adam) on an n-ray
     batch through a Blender-style camera: one warm-up step on 128 rays, then the median of `steps` steps.
     Threads = the host CPU share this process is given (OMP_NUM_THREADS on the GPU box: 16 of the machine's CPUs).
     BASELINE.md §3 asks for torch.set_num_threads(os.cpu_count()): that leg runs beside it as `all_cores` on a
     smaller sample (512 rays, median of <= 3 steps, ~30 s budget) — on the GPU box os.cpu_count() reports the whole
     machine, more threads than this process's share (affinity / cgroup quota are reported with it)."""
-    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    threads = _baseline_threads(world)
     med, times = _oracle_step_rate(S, NI, n, steps, threads)
     rec = {"value": round(n / med, 2), "unit": "rays/s", "cores": threads, "kind": "port",
            "sample": f"median of {steps} oracle train steps x {n} rays (64+128, 2 nets, fp32, MSE coarse+fine, "
                      f"clip, Adam): {med:.2f} s/step (steps {', '.join(f'{t:.2f}' for t in times)} s)",
            "cpu_model": _cpu_model(), "torch_threads": torch.get_num_threads(), **_cpu_share()}
+    if world > 1:
+        rec["note"] = (f"rank 0 of {world}, after every GPU leg, with the other ranks blocked in a gloo barrier; the "
+                       "same bounded sample as at N = 1")
     allc = os.cpu_count() or 1
     quota = rec.get("cgroup_cpu_quota")
     if allc != threads and quota is not None and quota < allc:
@@ -476,10 +499,12 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_
         # two buckets only (bucket 0 = coarse gradient on the side stream, bucket 1 = fine gradient + loss); the kernel
         # pass above ran without the side stream, i.e. with ONE all-reduce of the whole buffer (reported beside it)
         single = [x[0] for x in (tm.get("allreduce") or []) if x]
+        saved = _snapshot(tr)   # a timing device: the trainer leaves it in the state it entered it
         tr.enable_exchange_timing(n_ev)
         for s in range(a.warmup + a.steps + n_ev, a.warmup + a.steps + 2 * n_ev):
             one(s)
         torch.cuda.synchronize()
+        _restore(tr, saved)
         ex = tr.collect_exchange_timing()
         ar_mean = [sum(x[b] for x in ex if x[b] is not None) / max(1, sum(x[b] is not None for x in ex)) for b in range(2)]
         single_mean = sum(single) / len(single) if single else 0.0
@@ -522,15 +547,25 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_
     return rec, tr, (coarse, fine)
 
 
+def _snapshot(tr):
+    return [x.detach().clone() for x in (tr.params, tr.m, tr.v)], tr.step_count
+
+
+def _restore(tr, saved):
+    with torch.no_grad():
+        for x, y in zip((tr.params, tr.m, tr.v), saved[0]):
+            x.copy_(y)
+    tr.step_count = saved[1]
+
+
 def exposed_exchange(a, tr, one, dev, world, barrier, step_ms):
     """The exchange's exposed cost, measured rather than inferred from events: after the checksum, the same step runs
     a.steps more times with the all-reduces skipped (tr.exchange_enabled = False: every rank applies its own
     gradient), timed like the main region (barrier + synchronize, max over ranks); exposed = step time with the
     exchange - step time without it.  The trainer's parameters / moments are restored afterwards."""
-    saved = [x.detach().clone() for x in (tr.params, tr.m, tr.v)]
-    count = tr.step_count
+    saved = _snapshot(tr)
     tr.exchange_enabled = False
-    s0 = a.warmup + a.steps + max(1, a.timing_steps)
+    s0 = a.warmup + a.steps + 2 * max(1, a.timing_steps)   # seeds after the kernel- and exchange-timing passes
     try:
         one(s0)
         torch.cuda.synchronize()
@@ -544,10 +579,7 @@ def exposed_exchange(a, tr, one, dev, world, barrier, step_ms):
         el = time.perf_counter() - t0
     finally:
         tr.exchange_enabled = True
-        with torch.no_grad():
-            for x, y in zip((tr.params, tr.m, tr.v), saved):
-                x.copy_(y)
-        tr.step_count = count
+        _restore(tr, saved)
     mine = torch.tensor([el], dtype=torch.float64, device=dev)
     allr = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(allr, mine)
@@ -558,19 +590,8 @@ def exposed_exchange(a, tr, one, dev, world, barrier, step_ms):
 
 
 def params_checksum(params, world):
-    """After the timed region: every rank's flat parameter buffer reduced to (fp64 sum, position-weighted int64 hash of
-    the fp32 bit patterns) and all-gathered — data parallel with one gradient all-reduce keeps the replicas bitwise
-    equal, so an N-GPU run validates itself from its own line (params_equal_across_ranks)."""
-    bits = params.detach().contiguous().view(torch.int32).to(torch.int64)
-    wpos = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 1048573 + 1
-    h = (bits * wpos).sum().view(1)                      # int64, wraps on overflow identically on every rank
-    f = params.detach().double().sum().view(1)
-    hs, fs = [torch.zeros_like(h) for _ in range(world)], [torch.zeros_like(f) for _ in range(world)]
-    dist.all_gather(hs, h)
-    dist.all_gather(fs, f)
-    rows = [(float(x.item()), int(y.item())) for x, y in zip(fs, hs)]
-    return {"params_equal_across_ranks": all(r == rows[0] for r in rows), "world_size_checked": dist.get_world_size(),
-            "params_sum_per_rank": [r[0] for r in rows], "params_bit_hash_per_rank": [r[1] for r in rows]}
+    from nerf_amd.dp import params_checksum as pc
+    return pc(params, world)
 
 
 def llff_run(a, dev, world, rank, barrier, nccl):
@@ -621,7 +642,7 @@ def sweep_run(a, dev, world, rank):
     return summ
 
 
-def production_runs(a, dev):
+def production_runs(a, dev, rank=0, world=1):
     """the reference's production path — its default expert is Instant-NGP (common/args.py:56-58) with
     occupancy marching (models/inr/meta_ngp.py:389-443, nerfs/ray_rendering.py:494-558) inside the MoE container
     (models/inr/meta_container.py:275-343).  The ngp and container sub-records time their train steps (inputs resident
@@ -630,7 +651,7 @@ def production_runs(a, dev):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     out = {}
     cpu = dict(cpu_seconds=a.prod_cpu_seconds, no_cpu_baseline=a.no_cpu_baseline)
-    if not a.no_ngp:
+    if not a.no_ngp and world == 1:   # the single-expert NGP step has no gradient exchange of its own
         import bench_ngp
         progress("ngp (Instant-NGP expert) leg")
         out["ngp"] = bench_ngp.run(SimpleNamespace(steps=20, warmup=5, batch=4096, samples=96, train_views=100, **cpu),
@@ -639,8 +660,9 @@ def production_runs(a, dev):
     if not a.no_container:
         import bench_container
         progress("container (MoE: 4 NGP experts + occupancy + bg MLP) leg")
-        out["container"] = bench_container.run(SimpleNamespace(steps=48, warmup=40, batch=4096, train_views=100,
-                                                               shard=False, no_bucket=False, **cpu), dev)
+        out["container"] = bench_container.run(
+            SimpleNamespace(steps=a.container_steps, warmup=a.container_warmup, batch=4096, train_views=a.train_views,
+                            shard=False, no_bucket=False, **cpu), dev, rank, world)
         torch.cuda.empty_cache()
     return out
 
@@ -653,6 +675,7 @@ def psnr_run(a, rb, scene, runs, rank, world, n_local):
     from nerf_amd.ray_rendering import render_image
     fx, fy, cx, cy = scene.intrinsics
     out = {}
+    replicas = {}
     for prec, (tr, (coarse, fine)) in runs.items():
         done = tr.step_count
         torch.cuda.synchronize()
@@ -666,6 +689,11 @@ def psnr_run(a, rb, scene, runs, rank, world, n_local):
                 progress(f"psnr: {prec} step {s + 1}/{a.psnr_steps}")
         torch.cuda.synchronize()
         train_s = time.perf_counter() - t0
+        if world > 1:   # data parallel: every rank trained this replica; rank 0 renders it (the others are equal)
+            chk = params_checksum(tr.params, world)
+            replicas[prec] = chk["params_equal_across_ranks"]
+            if rank != 0:
+                continue
         tr.sync_to_modules()
         coarse.eval(), fine.eval()
         ps = []
@@ -677,13 +705,20 @@ def psnr_run(a, rb, scene, runs, rank, world, n_local):
         coarse.train(), fine.train()
         out[prec] = {"psnr": round(sum(ps) / len(ps), 3), "per_view": [round(p, 3) for p in ps],
                      "steps": tr.step_count, "train_s_after_timed": round(train_s, 2)}
+    if rank != 0:
+        return None
     rec = {"steps": a.psnr_steps, "views": int(scene.test_poses.shape[0]), "image": f"{scene.W}x{scene.H}",
-           "samples": [a.samples, a.importance], **out,
+           "samples": [a.samples, a.importance], "n_gpus": world, "global_batch": n_local * world, **out,
            "protocol": "engine trainers from the same seed-0 weights and the same 4096-ray batches / jitter seeds, "
                        "trained to `steps` total steps (the timed steps included), then full-image PSNR of each "
                        "held-out view in linear colour space (runtime_adapt.py:150-157), averaged"}
     if "fp32" in out and "bf16" in out:
         rec["bf16_minus_fp32_db"] = round(out["bf16"]["psnr"] - out["fp32"]["psnr"], 3)
+    if world > 1:
+        rec["params_equal_across_ranks"] = replicas
+        rec["dp_note"] = (f"{world} ranks trained each replica data parallel (global batch {n_local * world} rays per "
+                          "step, one gradient all-reduce per step); rank 0 rendered the held-out views after an "
+                          "all-gathered checksum of every rank's parameters")
     return rec
 
 
@@ -704,6 +739,11 @@ def main():
             dist.init_process_group("nccl", device_id=dev)  # RCCL on ROCm
         else:
             dist.init_process_group("gloo")
+
+    cpu_group = None
+    if world > 1:   # a host-side group for the final wait (rank 0's CPU baseline runs for ~1-2 minutes)
+        import datetime
+        cpu_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(minutes=30)) if nccl else None
 
     def barrier():
         if world > 1:
@@ -787,23 +827,30 @@ def main():
         progress("C4 (llff) leg")
         out["llff"] = llff_run(a, dev, world, rank, barrier, nccl)
     progress("timed legs done")
-    if not a.no_psnr and rank == 0 and runs and world == 1:
-        out["psnr"] = psnr_run(a, rb, scene, runs, rank, world, n_local)
+    if not a.no_psnr and runs:
+        ps = psnr_run(a, rb, scene, runs, rank, world, n_local)
+        if rank == 0:
+            out["psnr"] = ps
     if not a.no_sweep and a.scene == "blender" and a.path == "engine":
         progress("C5 (8-scene sweep) leg")
         sw = sweep_run(a, dev, world, rank)
         if rank == 0:
             out["sweep"] = sw
-    if world == 1 and a.path == "engine" and a.scene == "blender":
-        out.update(production_runs(a, dev))
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(a.samples, a.importance, a.cpu_batch, a.cpu_steps)
+    if a.path == "engine" and a.scene == "blender":
+        prod = production_runs(a, dev, rank, world)
+        if rank == 0:
+            out.update(prod)
+    # the CPU baseline on rank 0 after every GPU leg; at N > 1 the other ranks wait in a gloo barrier (blocked in a
+    # socket read, not spinning on a core beside the baseline's threads)
+    if rank == 0 and not a.no_cpu_baseline:
+        progress("cpu baseline leg")
+        out["cpu_baseline"] = cpu_baseline(a.samples, a.importance, a.cpu_batch, a.cpu_steps, world)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
-        barrier()  # the other ranks wait for rank 0's report before tearing down
+        cpu_group.barrier() if cpu_group is not None else barrier()  # everyone waits for rank 0's report
         dist.destroy_process_group()
 
 

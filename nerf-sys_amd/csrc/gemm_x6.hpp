@@ -398,9 +398,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   constexpr int WTM = 32 * TM, BM = WTM * NW, TN = TN_, BN = 32 * TN_, WTN = BN;
   constexpr int KS = BK / 16, CPR = BK / 8;       // MFMA k-steps / 16-B weight chunks per row, per slab
   constexpr int BCH = 3 * BN * CPR / NT;          // weight chunks per thread per slab
-#ifndef NERF_X6W_REGB
-  static_assert((3 * BN * CPR) % NT == 0 || true, "weight staging");  // GLDS: per-wave DMA groups (GPW, below)
-#else
+#ifdef NERF_X6W_REGB  // register staging: whole 16-B chunks per thread (the GLDS DMA groups are checked below)
   static_assert((3 * BN * CPR) % NT == 0 && (BN * CPR) % NT == 0, "weight staging");
 #endif
 #if !defined(NERF_X6W_REGB) || defined(NERF_X6W_SWIZZLE)
@@ -464,7 +462,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void gemm_nt_x6w_kernel(const float*
   // 0.588-0.594 ms per fine launch, 218.5k -> 221k rays/s, the same loss bits; s_memtime stamps of the forward: slab
   // 11.4k -> 9.6k cycles, its "weight store + barrier" tail 3.5k -> 1.9k
   constexpr int GPP = BN * BK * 2 / 1024, GPW = 3 * GPP / NW;  // 1-KiB groups per piece image / per wave
-  static_assert(!GLDS || (BK == 32 && (3 * GPP) % NW == 0), "GLDS staging");
+  // GLDS: the NW waves' GPW groups each must cover the three piece images' 3 GPP 1-KiB groups exactly
+  static_assert(!GLDS || (BK == 32 && GPW * NW == 3 * GPP && GPP * 1024 == BN * BK * 2), "GLDS staging");
   const int wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t gofs = (uint32_t)((((lane >> 2) * ldb) + 8 * ((lane & 3) ^ ((lane >> 4) & 3))) * 2);
   const uint32_t smem_u32 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;  // chunk c = tid + NT i: plane c / (BN CPR), row (c / CPR) % BN, chunk c % CPR
@@ -938,7 +937,7 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_x6_kernel(const float* __re
 // split once; eight waves of 64 (n) x 128 (k) (2 x 4 MFMA tiles) amortise each G fragment over four X fragments.
 // 16-row slabs, six piece images [16][288] bf16 per stage, double-buffered (108 KiB: one workgroup per CU, two waves
 // per SIMD); the loads of slab it + 2 are issued at iteration it (two register sets; three were slower,
-// 0.477 -> 0.512 ms, NERF_X6W_PF3).  The bias columns are summed from the raw staging registers.  Requirements: rows_per_split % 16 == 0, M % 16 == 0, ldg / ldx % 4 == 0, K >= 256 (the first
+// 0.477 -> 0.512 ms in a round-4 A/B build, not kept).  The bias columns are summed from the raw staging registers.  Requirements: rows_per_split % 16 == 0, M % 16 == 0, ldg / ldx % 4 == 0, K >= 256 (the first
 // 256 columns of X).
 __global__ __launch_bounds__(512, 1) void gemm_wgrad_x6w_kernel(const float* __restrict__ G, int ldg,
                                                                const float* __restrict__ X, int ldx,

@@ -363,4 +363,4 @@ extern "C" int nerf_dataset_rays(const float* c2w, const float* intrinsics, cons
   return nerf_launch_status();
 }
 
-extern "C" const char* nerf_version(void) { return "nerf_amd 0.1 gfx950"; }
+// nerf_version() is generated by the Makefile (build/version.cpp): it carries the hash of the sources it was built from

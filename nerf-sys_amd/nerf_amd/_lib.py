@@ -20,6 +20,28 @@ _ERR = {-1: "invalid argument", -2: "pointer not 16-byte aligned", -3: "unknown 
 _lib = None
 
 
+def source_hash() -> str:
+    """The hash the Makefile bakes into nerf_version(): sha256 over csrc/*.hip + csrc/*.hpp (byte order of their
+    paths) followed by include/nerf_amd.h, first 16 hex digits.  Equal to the loaded library's `src=` field iff that
+    library was built from this tree's sources."""
+    import glob
+    import hashlib
+    pkg = os.path.dirname(_HERE)
+    rel = sorted(os.path.relpath(p, pkg) for p in glob.glob(os.path.join(pkg, "csrc", "*.hip")) +
+                 glob.glob(os.path.join(pkg, "csrc", "*.hpp")))
+    h = hashlib.sha256()
+    for r in rel + [os.path.join("..", "include", "nerf_amd.h")]:
+        with open(os.path.join(pkg, r), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def built_hash() -> str:
+    """The `src=` field of the loaded library's nerf_version()."""
+    v = lib().nerf_version().decode()
+    return v.split("src=", 1)[1] if "src=" in v else ""
+
+
 def lib():
     global _lib
     if _lib is None:

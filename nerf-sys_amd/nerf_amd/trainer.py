@@ -27,6 +27,7 @@ from .dp import allreduce_flat, inv_count as _inv_count
 from .vanilla import PackedLayout, VanillaNeRF
 
 _CS = ("linear", "srgb", "identity")
+ENGINE_PRECISIONS = ("fp32", "bf16")
 
 
 class RayBatcher:
@@ -84,9 +85,14 @@ class NeRFTrainer:
             self.seg_off += [k * P + cs, (k + 1) * P]
             self.seg_lr += [lr_sigma, lr_color]
         self.S, self.n_imp = n_samples, n_importance
-        if precision not in K.PRECISIONS:
-            raise ValueError(f"precision must be one of {K.PRECISIONS}")
-        self.precision = precision  # MLP GEMMs: fp32 (configs[1]) or bf16 (configs[2]); compositing stays fp32
+        # fp32 (configs[1]) or bf16 (configs[2]); compositing stays fp32.  The fp16 build of the MLP kernels
+        # (K.PRECISIONS has "fp16") is the reference's autocast(float16) loop on the drop-in surface, where
+        # GradScaler supplies the loss scale and the inf/nan step skip; this engine has neither, so unscaled
+        # ~1/(3 N) gradients would underflow in its fp16 backward: refused here
+        if precision not in ENGINE_PRECISIONS:
+            raise ValueError(f"precision must be one of {ENGINE_PRECISIONS} (fp16 runs only under autocast + "
+                             f"GradScaler on the drop-in render_rays / VanillaNeRF surface)")
+        self.precision = precision
         self.bf16_flags = int(bf16_flags)  # K.BF16_LAYERED_* (A/B runs of the layered bf16 launches)
         # fp32 trunk GEMMs: "split" = every trunk GEMM as bf16 piece products (gemm_x6.hpp; the input gradients with
         # separate small-term accumulators), the default; "native_dgrad" = input gradients on the fp32 MFMA;

@@ -242,3 +242,36 @@ def test_bench_engine_run_world2_gloo():
     for rank_times in dp["allreduce_ms_per_rank"]:
         assert len(rank_times) == 2 and all(t > 0.0 for t in rank_times), dp["allreduce_ms_per_rank"]
     assert "exposed_exchange_ms" in dp and dp["step_ms_no_exchange"] > 0
+
+
+def test_bench_world2_line_complete_gloo():
+    """The N > 1 bench line carries what the N = 1 line does: rank 0's CPU baseline (the other
+    rank waiting in the final barrier), the PSNR leg trained data parallel on both ranks and rendered by rank 0 with
+    the replicas checked equal, and the production container on FlatAdam(world_size=2) with a `dp` block whose
+    all-gathered parameter checksum says the replicas stayed bitwise equal.  Two ranks share cuda:0 over gloo."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_PORT=str(_free_port()), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--steps", "2",
+           "--warmup", "1", "--timing-steps", "1", "--train-views", "4", "--psnr-steps", "8", "--psnr-views", "1",
+           "--cpu-batch", "32", "--cpu-steps", "1", "--no-llff", "--no-sweep", "--no-dropin", "--no-other-precision",
+           "--no-native-ref", "--container-steps", "3", "--container-warmup", "4", "--prod-cpu-seconds", "1"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    print(json.dumps({k: out[k] for k in ("value", "psnr", "cpu_baseline")}))
+    assert out["n_gpus"] == 2 and out["dp"]["params_equal_across_ranks"] is True
+    cb = out["cpu_baseline"]
+    assert cb and cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port"
+    ps = out["psnr"]
+    assert ps["n_gpus"] == 2 and ps["params_equal_across_ranks"] == {"fp32": True}
+    assert ps["fp32"]["steps"] == 8 and ps["fp32"]["psnr"] > 0
+    c = out["container"]
+    assert c["n_gpus"] == 2 and c["value"] > 0
+    assert c["dp"]["world_size"] == 2 and c["dp"]["flat_adam"]["world_size"] == 2
+    assert c["dp"]["params_equal_across_ranks"] is True and len(set(c["dp"]["params_bit_hash_per_rank"])) == 1
+    assert c["exchange"]["bucketed"] is True

@@ -283,6 +283,46 @@ def test_render_rays_golden(net):
     net.eval()
 
 
+def test_c1_crop_render_full_size(net):
+    """BASELINE configs[0] (C1) at its stated size: the 100x100 centre crop of an 800x800 Lego-style camera (10,000
+    rays, the golden `rays_const` crop), 64 coarse samples, coarse-only MLP, through render_rays on the GPU against
+    the pinned oracle (an/nerfs/ray_rendering.py:290-345) at the north-star 1e-4: eval mode (linspace t) and train
+    mode with an injected stratified draw, plus the train-mode MSE gradients of every parameter (1e-4 of scale)."""
+    from nerf_amd.ray_rendering import render_rays
+    from nerf_amd.ray_sampling import rays_for_camera
+    z = load("rays")
+    f = float(z["focal"])
+    rays = rays_for_camera(800, 800, f, f, 400.0, 400.0, z["c2w"].to(DEV), near=2.0, far=6.0).view(800, 800, 8)
+    rays = rays[350:450, 350:450].reshape(-1, 8).contiguous()
+    assert rays.shape == (10000, 8)
+    _close(rays, z["rays_const"], 2e-6, what="C1 crop rays")
+    p = mlp_params("w/")
+    rays_c = rays.cpu()
+    net.eval()
+    with torch.no_grad():
+        rgb, d, w, a = render_rays(net, rays, ray_samples=64)
+    ref = O.render_rays(p, rays_c, 64, training=False)
+    _close(rgb, ref[0], what="C1 eval rgb")
+    _close(d, ref[1], what="C1 eval depth", rel_scale=True)
+    _close(w, ref[2], what="C1 eval weights")
+    _close(a, ref[3], what="C1 eval acc")
+    net.train()
+    u = torch.rand(10000, 64, generator=torch.Generator().manual_seed(100))
+    gt = torch.rand(10000, 3, generator=torch.Generator().manual_seed(101))
+    net.zero_grad()
+    rgb, d, w, a = render_rays(net, rays, ray_samples=64, u_strat=u.to(DEV))
+    torch.nn.functional.mse_loss(rgb, gt.to(DEV)).backward()
+    pr = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    ref = O.render_rays(pr, rays_c, 64, training=True, u_strat=u)
+    torch.nn.functional.mse_loss(ref[0], gt).backward()
+    _close(rgb, ref[0], what="C1 train rgb")
+    _close(d, ref[1], what="C1 train depth", rel_scale=True)
+    _close(w, ref[2], what="C1 train weights")
+    for n, q in net.named_parameters():
+        _close(q.grad, pr[n].grad, rel_scale=True, what=f"C1 train grad {n}")
+    net.eval()
+
+
 def test_sample_pdf_vs_oracle(K):
     g = torch.Generator().manual_seed(11)
     N, S, NI = 300, 64, 128

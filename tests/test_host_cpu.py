@@ -30,6 +30,13 @@ def test_library_exports_header_symbols():
     assert b"gfx950" in L.nerf_version()
 
 
+def test_library_built_from_this_tree():
+    """nerf_version() carries the hash of the sources the .so was linked from (Makefile): a prebuilt library that
+    does not match HEAD's csrc/ + include/ fails here instead of being tested silently."""
+    from nerf_amd._lib import built_hash, source_hash
+    assert built_hash() == source_hash(), "libnerf_amd.so is stale: rebuild with `make -C nerf-sys_amd`"
+
+
 def test_packed_layout_roundtrip():
     from nerf_amd.vanilla import PackedLayout, PARAM_SHAPES, NUM_PARAMS
     L = PackedLayout.get()
@@ -79,3 +86,12 @@ def test_graft_build_entry_imports():
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
     assert callable(m.build) and callable(m.smoke)
+
+
+def test_engine_refuses_fp16():
+    """The fused engine has no loss scaling / inf-skip: fp16 is for the autocast + GradScaler drop-in loop only
+    (ADVICE r05)."""
+    from nerf_amd.trainer import NeRFTrainer
+    from nerf_amd.vanilla import VanillaNeRF
+    with pytest.raises(ValueError, match="fp16"):
+        NeRFTrainer(VanillaNeRF(), VanillaNeRF(), device="cpu", precision="fp16")

@@ -242,6 +242,11 @@ def run(a, dev, rank=0, world=1):
     }
     if exch:
         out["exchange"] = exch
+    if world > 1:   # the replicas after every step above: one gradient exchange per step keeps them bitwise equal
+        from nerf_amd.dp import params_checksum
+        out["dp"] = {"world_size": world, "backend": dist.get_backend(), "flat_adam": {
+            "world_size": one.opt.world_size, "shard": one.opt.shard, "bucket_tables": one.opt.bucket_tables,
+            "grad_bytes": int(one.opt.grad.numel() * 4)}, **params_checksum(one.opt.flat, world)}
     out["cpu_baseline"] = None if (a.no_cpu_baseline or world > 1) else cpu_baseline(a.cpu_seconds)
     return out
 
