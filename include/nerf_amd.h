@@ -318,6 +318,23 @@ int nerf_ngp_bwd_hash(const NerfNgpNet* net, const NerfHashGrid* grid, const flo
                       float enc_eps, float* d_table, float* d_w, int accumulate, void* ws, int64_t ws_bytes,
                       hipStream_t stream);
 
+/* Device-sized forms (the container's sync-free train step, meta_container.py:275-343 with the sizes never read on
+ * the host): every buffer is sized for `cap` rows and the row count is read on the device from rng (int32 pair,
+ * device): rows = min(rng[1] - rng[0], cap).  The grids cover the capacity; workgroups past the count exit.
+ *   _fwd_enc_n / _bwd_hash_n: rows 0 .. rows - 1 of x_d / enc / rgb_sigma / d_rgb_sigma (an expert's gathered samples,
+ *                             rng = that expert's dispatch offsets); ws sized by nerf_ngp_workspace_bytes(net, cap)
+ *   _density_enc_rng:         rows rng[0] .. rng[1] - 1 of x and sigma (one expert's slice of a packed march) */
+int nerf_ngp_fwd_enc_n(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table, const float* w,
+                       const float* x_d, int64_t cap, const int32_t* rng, const float* aabb, float enc_eps, float* enc,
+                       int enc_stride, float* rgb_sigma, hipStream_t stream);
+int nerf_ngp_density_enc_rng(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table, const float* w,
+                             const float* x, int64_t x_stride, int64_t cap, const int32_t* rng, const float* aabb,
+                             float enc_eps, float* sigma, hipStream_t stream);
+int nerf_ngp_bwd_hash_n(const NerfNgpNet* net, const NerfHashGrid* grid, const float* w, const float* enc,
+                        int enc_stride, const float* x_d, int64_t cap, const int32_t* rng, const float* d_rgb_sigma,
+                        const float* aabb, float enc_eps, float* d_table, float* d_w, int accumulate, void* ws,
+                        int64_t ws_bytes, hipStream_t stream);
+
 /* ------------------------------------------------------------------ MoE container */
 
 /* MetaContainer._routing (models/inr/meta_container.py:97-134): distances of x[:, :3] (rows of pitch
@@ -341,6 +358,12 @@ int nerf_moe_dispatch(const float* weights, int64_t M, int K, float eps, int32_t
 /* dst[i][c] = src[idx[i]][c], c < cols (the expert's x.index_select rows). */
 int nerf_gather_rows(const float* src, int64_t src_stride, const int32_t* idx, int64_t n, int cols, float* dst,
                      int64_t dst_stride, hipStream_t stream);
+/* Device-sized forms (see nerf_ngp_fwd_enc_n): dispatch over `cap` rows of which the first *m_dev are real; gather
+ * of idx entries rng[0] .. rng[1] - 1 (rng = an expert's device offsets) into dst rows 0 .. */
+int nerf_moe_dispatch_n(const float* weights, int64_t cap, const int32_t* m_dev, int K, float eps, int32_t* offsets,
+                        int32_t* idx, void* ws, int64_t ws_bytes, hipStream_t stream);
+int nerf_gather_rows_rng(const float* src, int64_t src_stride, const int32_t* idx, const int32_t* rng, int64_t cap,
+                         int cols, float* dst, int64_t dst_stride, hipStream_t stream);
 
 /* The mix of expert k (meta_container.py:304-318): out[idx[i]][c] += y[i][c] * weights[idx[i]][k] for the
  * n rows of the expert (rows unique within a call; call k = 0..K-1 in order for the reference's sum order;
@@ -486,6 +509,15 @@ int nerf_moe_blend_finish(const float* s_acc, const float* c_acc, int64_t M, flo
 int nerf_moe_blend_bwd(const float* y, int64_t n, const int32_t* idx, const float* weights, int K, int k,
                        const float* s_acc, const float* rgb_sigma, const float* d_rgb_sigma, float* d_y,
                        hipStream_t stream);
+/* Device-sized blend (see nerf_ngp_fwd_enc_n): y / d_y rows 0 .. rng[1] - rng[0] - 1 pair with idx entries rng[0] ..;
+ * _finish_n over `cap` rows of which the first *m_dev are real. */
+int nerf_moe_blend_rng(const float* y, int64_t cap, const int32_t* idx, const int32_t* rng, const float* weights, int K,
+                       int k, float* s_acc, float* c_acc, hipStream_t stream);
+int nerf_moe_blend_finish_n(const float* s_acc, const float* c_acc, int64_t cap, const int32_t* m_dev, float* rgb_sigma,
+                            hipStream_t stream);
+int nerf_moe_blend_bwd_rng(const float* y, int64_t cap, const int32_t* idx, const int32_t* rng, const float* weights,
+                           int K, int k, const float* s_acc, const float* rgb_sigma, const float* d_rgb_sigma,
+                           float* d_y, hipStream_t stream);
 
 /* ------------------------------------------------------------------ meta-learning updates (§8f row 4) */
 

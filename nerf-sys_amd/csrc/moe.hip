@@ -66,8 +66,9 @@ __global__ void route_kernel(const float* __restrict__ x, int64_t xs, int64_t M,
 
 // per-block counts of routed rows per expert
 __global__ void dispatch_count_kernel(const float* __restrict__ W, int64_t M, int K, float eps,
-                                      int32_t* __restrict__ bcnt) {
+                                      int32_t* __restrict__ bcnt, const int32_t* __restrict__ m_dev) {
   __shared__ int cnt[MOE_MAX_K];
+  if (m_dev && *m_dev < M) M = *m_dev;  // device-sized (nerf_moe_dispatch_n): rows past the count route nowhere
   if (threadIdx.x < MOE_MAX_K) cnt[threadIdx.x] = 0;
   __syncthreads();
   const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -116,8 +117,9 @@ __global__ void dispatch_offsets_kernel(const int32_t* __restrict__ tot, int K, 
 
 __global__ void dispatch_write_kernel(const float* __restrict__ W, int64_t M, int K, float eps,
                                       const int32_t* __restrict__ bbase, const int32_t* __restrict__ offsets,
-                                      int32_t* __restrict__ idx) {
+                                      int32_t* __restrict__ idx, const int32_t* __restrict__ m_dev) {
   __shared__ int wcnt[MOE_MAX_K][4];
+  if (m_dev && *m_dev < M) M = *m_dev;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (int k = 0; k < K; ++k) {
@@ -139,7 +141,12 @@ __global__ void dispatch_write_kernel(const float* __restrict__ W, int64_t M, in
 }
 
 __global__ void gather_rows_kernel(const float* __restrict__ src, int64_t ss, const int32_t* __restrict__ idx, int64_t n,
-                                   int cols, float* __restrict__ dst, int64_t ds) {
+                                   int cols, float* __restrict__ dst, int64_t ds, const int32_t* __restrict__ rng) {
+  if (rng) {  // device-sized (nerf_gather_rows_rng): idx entries rng[0] .. rng[1] - 1 -> dst rows 0 ..
+    const int64_t c = (int64_t)rng[1] - rng[0];
+    n = c < n ? (c < 0 ? 0 : c) : n;
+    idx += rng[0];
+  }
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n * cols) return;
   const int64_t i = t / cols;
@@ -338,8 +345,8 @@ extern "C" int64_t nerf_moe_dispatch_workspace_bytes(int64_t M, int K) {
   return nerf_cdiv(M < 1 ? 1 : M, 256) * K * 4 + MOE_MAX_K * 4 + 256;
 }
 
-extern "C" int nerf_moe_dispatch(const float* weights, int64_t M, int K, float eps, int32_t* offsets, int32_t* idx,
-                                 void* ws, int64_t ws_bytes, hipStream_t st) {
+static int moe_dispatch_impl(const float* weights, int64_t M, const int32_t* m_dev, int K, float eps, int32_t* offsets,
+                             int32_t* idx, void* ws, int64_t ws_bytes, hipStream_t st) {
   if (M < 0 || K < 1 || K > MOE_MAX_K || !offsets) return NERF_E_ARG;
   if (M == 0) {
     (void)hipMemsetAsync(offsets, 0, (K + 1) * sizeof(int32_t), st);
@@ -349,12 +356,23 @@ extern "C" int nerf_moe_dispatch(const float* weights, int64_t M, int K, float e
   const int64_t nblk = nerf_cdiv(M, 256);
   if (ws_bytes < nblk * K * 4 + MOE_MAX_K * 4) return NERF_E_WORKSPACE;
   int32_t* bcnt = reinterpret_cast<int32_t*>(ws);
-  dispatch_count_kernel<<<(unsigned)nblk, 256, 0, st>>>(weights, M, K, eps, bcnt);
+  dispatch_count_kernel<<<(unsigned)nblk, 256, 0, st>>>(weights, M, K, eps, bcnt, m_dev);
   int32_t* tot = bcnt + nblk * K;
   dispatch_scan_kernel<<<K, 256, 0, st>>>(bcnt, nblk, K, tot);
   dispatch_offsets_kernel<<<1, 64, 0, st>>>(tot, K, offsets);
-  dispatch_write_kernel<<<(unsigned)nblk, 256, 0, st>>>(weights, M, K, eps, bcnt, offsets, idx);
+  dispatch_write_kernel<<<(unsigned)nblk, 256, 0, st>>>(weights, M, K, eps, bcnt, offsets, idx, m_dev);
   return nerf_launch_status();
+}
+
+extern "C" int nerf_moe_dispatch(const float* weights, int64_t M, int K, float eps, int32_t* offsets, int32_t* idx,
+                                 void* ws, int64_t ws_bytes, hipStream_t st) {
+  return moe_dispatch_impl(weights, M, nullptr, K, eps, offsets, idx, ws, ws_bytes, st);
+}
+
+extern "C" int nerf_moe_dispatch_n(const float* weights, int64_t cap, const int32_t* m_dev, int K, float eps,
+                                   int32_t* offsets, int32_t* idx, void* ws, int64_t ws_bytes, hipStream_t st) {
+  if (!m_dev) return NERF_E_ARG;
+  return moe_dispatch_impl(weights, cap, m_dev, K, eps, offsets, idx, ws, ws_bytes, st);
 }
 
 extern "C" int nerf_gather_rows(const float* src, int64_t src_stride, const int32_t* idx, int64_t n, int cols,
@@ -362,7 +380,18 @@ extern "C" int nerf_gather_rows(const float* src, int64_t src_stride, const int3
   if (n < 0 || cols < 1 || src_stride < cols || dst_stride < cols) return NERF_E_ARG;
   if (n == 0) return NERF_OK;
   if (!src || !idx || !dst) return NERF_E_ARG;
-  gather_rows_kernel<<<(unsigned)nerf_cdiv(n * cols, 256), 256, 0, st>>>(src, src_stride, idx, n, cols, dst, dst_stride);
+  gather_rows_kernel<<<(unsigned)nerf_cdiv(n * cols, 256), 256, 0, st>>>(src, src_stride, idx, n, cols, dst, dst_stride,
+                                                                         nullptr);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_gather_rows_rng(const float* src, int64_t src_stride, const int32_t* idx, const int32_t* rng,
+                                    int64_t cap, int cols, float* dst, int64_t dst_stride, hipStream_t st) {
+  if (cap < 0 || cols < 1 || src_stride < cols || dst_stride < cols || !rng) return NERF_E_ARG;
+  if (cap == 0) return NERF_OK;
+  if (!src || !idx || !dst) return NERF_E_ARG;
+  gather_rows_kernel<<<(unsigned)nerf_cdiv(cap * cols, 256), 256, 0, st>>>(src, src_stride, idx, cap, cols, dst,
+                                                                           dst_stride, rng);
   return nerf_launch_status();
 }
 
@@ -566,8 +595,19 @@ __global__ void scatter_counts_kernel(const int32_t* __restrict__ hit_idx, const
 
 // blend of expert k's (rgb, sigma) rows into the mix accumulators (expert order, as the reference's sums):
 // s[m] += W[m,k] * sigma ; c[m] += (W[m,k] * sigma) * rgb
+// device-sized (rng): y rows 0 .. rng[1] - rng[0] - 1 pair with idx entries rng[0] ..
+__device__ __forceinline__ const int32_t* rng_rows(const int32_t* __restrict__ rng, int64_t& n, const int32_t* idx) {
+  if (rng) {
+    const int64_t c = (int64_t)rng[1] - rng[0];
+    n = c < n ? (c < 0 ? 0 : c) : n;
+    idx += rng[0];
+  }
+  return idx;
+}
 __global__ void blend_kernel(const float* __restrict__ y, int64_t n, const int32_t* __restrict__ idx,
-                             const float* __restrict__ W, int K, int k, float* __restrict__ s, float* __restrict__ c) {
+                             const float* __restrict__ W, int K, int k, float* __restrict__ s, float* __restrict__ c,
+                             const int32_t* __restrict__ rng) {
+  idx = rng_rows(rng, n, idx);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t m = idx[i];
@@ -581,7 +621,8 @@ __global__ void blend_kernel(const float* __restrict__ y, int64_t n, const int32
 
 // rs_mix[m] = [c / max(s, 1e-12), max(s, 1e-12)]
 __global__ void blend_finish_kernel(const float* __restrict__ s, const float* __restrict__ c, int64_t M,
-                                    float* __restrict__ rs) {
+                                    float* __restrict__ rs, const int32_t* __restrict__ m_dev) {
+  if (m_dev && *m_dev < M) M = *m_dev;
   const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
   const float sn = fmaxf(s[m], 1e-12f);
@@ -591,7 +632,9 @@ __global__ void blend_finish_kernel(const float* __restrict__ s, const float* __
 // backward of the blend for expert k: given d rs_mix (M,4) and the raw sums, d y_k (n,4)
 __global__ void blend_bwd_kernel(const float* __restrict__ y, int64_t n, const int32_t* __restrict__ idx,
                                  const float* __restrict__ W, int K, int k, const float* __restrict__ s,
-                                 const float* __restrict__ rs, const float* __restrict__ drs, float* __restrict__ dy) {
+                                 const float* __restrict__ rs, const float* __restrict__ drs, float* __restrict__ dy,
+                                 const int32_t* __restrict__ rng) {
+  idx = rng_rows(rng, n, idx);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t m = idx[i];
@@ -655,7 +698,16 @@ extern "C" int nerf_moe_blend(const float* y, int64_t n, const int32_t* idx, con
   if (n < 0 || K < 1 || k < 0 || k >= K) return NERF_E_ARG;
   if (n == 0) return NERF_OK;
   if (!y || !idx || !weights || !s_acc || !c_acc) return NERF_E_ARG;
-  blend_kernel<<<(unsigned)nerf_cdiv(n, 256), 256, 0, st>>>(y, n, idx, weights, K, k, s_acc, c_acc);
+  blend_kernel<<<(unsigned)nerf_cdiv(n, 256), 256, 0, st>>>(y, n, idx, weights, K, k, s_acc, c_acc, nullptr);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_moe_blend_rng(const float* y, int64_t cap, const int32_t* idx, const int32_t* rng,
+                                  const float* weights, int K, int k, float* s_acc, float* c_acc, hipStream_t st) {
+  if (cap < 0 || K < 1 || k < 0 || k >= K || !rng) return NERF_E_ARG;
+  if (cap == 0) return NERF_OK;
+  if (!y || !idx || !weights || !s_acc || !c_acc) return NERF_E_ARG;
+  blend_kernel<<<(unsigned)nerf_cdiv(cap, 256), 256, 0, st>>>(y, cap, idx, weights, K, k, s_acc, c_acc, rng);
   return nerf_launch_status();
 }
 
@@ -664,7 +716,16 @@ extern "C" int nerf_moe_blend_finish(const float* s_acc, const float* c_acc, int
   if (M < 0) return NERF_E_ARG;
   if (M == 0) return NERF_OK;
   if (!s_acc || !c_acc || !rgb_sigma) return NERF_E_ARG;
-  blend_finish_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(s_acc, c_acc, M, rgb_sigma);
+  blend_finish_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(s_acc, c_acc, M, rgb_sigma, nullptr);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_moe_blend_finish_n(const float* s_acc, const float* c_acc, int64_t cap, const int32_t* m_dev,
+                                       float* rgb_sigma, hipStream_t st) {
+  if (cap < 0 || !m_dev) return NERF_E_ARG;
+  if (cap == 0) return NERF_OK;
+  if (!s_acc || !c_acc || !rgb_sigma) return NERF_E_ARG;
+  blend_finish_kernel<<<(unsigned)nerf_cdiv(cap, 256), 256, 0, st>>>(s_acc, c_acc, cap, rgb_sigma, m_dev);
   return nerf_launch_status();
 }
 
@@ -675,6 +736,17 @@ extern "C" int nerf_moe_blend_bwd(const float* y, int64_t n, const int32_t* idx,
   if (n == 0) return NERF_OK;
   if (!y || !idx || !weights || !s_acc || !rgb_sigma || !d_rgb_sigma || !d_y) return NERF_E_ARG;
   blend_bwd_kernel<<<(unsigned)nerf_cdiv(n, 256), 256, 0, st>>>(y, n, idx, weights, K, k, s_acc, rgb_sigma,
-                                                                d_rgb_sigma, d_y);
+                                                                d_rgb_sigma, d_y, nullptr);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_moe_blend_bwd_rng(const float* y, int64_t cap, const int32_t* idx, const int32_t* rng,
+                                      const float* weights, int K, int k, const float* s_acc, const float* rgb_sigma,
+                                      const float* d_rgb_sigma, float* d_y, hipStream_t st) {
+  if (cap < 0 || K < 1 || k < 0 || k >= K || !rng) return NERF_E_ARG;
+  if (cap == 0) return NERF_OK;
+  if (!y || !idx || !weights || !s_acc || !rgb_sigma || !d_rgb_sigma || !d_y) return NERF_E_ARG;
+  blend_bwd_kernel<<<(unsigned)nerf_cdiv(cap, 256), 256, 0, st>>>(y, cap, idx, weights, K, k, s_acc, rgb_sigma,
+                                                                  d_rgb_sigma, d_y, rng);
   return nerf_launch_status();
 }

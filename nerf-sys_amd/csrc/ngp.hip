@@ -1198,10 +1198,16 @@ __global__ __launch_bounds__(256, 2) void ngp_bwd_prod_kernel(const float* __res
                                                               const float* __restrict__ gout,
                                                               float* __restrict__ d_enc, float* __restrict__ partial,
                                                               int64_t ntiles, HashArgs ha = HashArgs{},
-                                                              float* __restrict__ dtab = nullptr) {
+                                                              float* __restrict__ dtab = nullptr,
+                                                              const int32_t* __restrict__ rng = nullptr) {
   using namespace ngp_prod;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (rng) {  // device-sized launch (nerf_ngp_bwd_hash_n): M is the capacity, the rows are rng[1] - rng[0]
+    const int64_t n = (int64_t)rng[1] - rng[0];
+    M = n < 0 ? 0 : (n < M ? n : M);
+    ntiles = (M + NGP_BROWS - 1) / NGP_BROWS;
+  }
   ngp_f32x4 acc[NSLOT];
 #pragma unroll
   for (int j = 0; j < NSLOT; ++j) acc[j] = ngp_f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1211,7 +1217,7 @@ __global__ __launch_bounds__(256, 2) void ngp_bwd_prod_kernel(const float* __res
   NgpFrag fa, fb;
   load_frag<0>(w, wt, wave, tid & 63, fa);
   TileIn nx;
-  load_tile_in(enc, es, in_dim, x_d, M, blockIdx.x, tid >> 3, tid & 7, nx);
+  if (M > 0) load_tile_in(enc, es, in_dim, x_d, M, blockIdx.x, tid >> 3, tid & 7, nx);
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t m0 = tile * NGP_BROWS;
@@ -1405,11 +1411,17 @@ __global__ __launch_bounds__(256) void ngp_fwd_prod_kernel(const float* __restri
                                                            int es, int in_dim, const float* __restrict__ x_d,
                                                            int64_t M, float* __restrict__ out, HashArgs ha = HashArgs{},
                                                            const float* __restrict__ table = nullptr,
-                                                           float* __restrict__ enc_out = nullptr) {
+                                                           float* __restrict__ enc_out = nullptr,
+                                                           const int32_t* __restrict__ rng = nullptr) {
   using namespace ngp_prod;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int pr = tid >> 3, pp = tid & 7;
+  if (rng) {  // device-sized launch (nerf_ngp_fwd_enc_n): the grid covers the capacity M, the rows are rng[1] - rng[0]
+    const int64_t n = (int64_t)rng[1] - rng[0];
+    M = n < 0 ? 0 : (n < M ? n : M);
+  }
+  if ((int64_t)blockIdx.x * NGP_BROWS >= M) return;  // whole workgroup: no barrier is left waiting
   const int64_t m0 = (int64_t)blockIdx.x * NGP_BROWS, m = m0 + pr, mc = m < M ? m : M - 1;
   const bool ok = m < M;
   NgpFrag fa, fb;
@@ -1512,10 +1524,18 @@ __global__ __launch_bounds__(256) void ngp_fwd_prod_kernel(const float* __restri
 __global__ __launch_bounds__(256) void ngp_density_enc_prod_kernel(HashArgs a, const float* __restrict__ table,
                                                                    const float* __restrict__ w,
                                                                    const float* __restrict__ x, int64_t xs,
-                                                                   int64_t M, float* __restrict__ sigma) {
+                                                                   int64_t M, float* __restrict__ sigma,
+                                                                   const int32_t* __restrict__ rng = nullptr) {
   using namespace ngp_prod;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  if (rng) {  // device-sized launch (nerf_ngp_density_enc_rng): rows rng[0] .. rng[1] - 1 of x and sigma
+    const int64_t lo = rng[0], n = (int64_t)rng[1] - lo;
+    M = n < 0 ? 0 : (n < M ? n : M);
+    x += lo * xs;
+    sigma += lo;
+  }
+  if ((int64_t)blockIdx.x * NGP_BROWS >= M) return;
   const int64_t m0 = (int64_t)blockIdx.x * NGP_BROWS;
   NgpFrag fa, fb;
   load_frag<0>(w, nullptr, wave, lane, fa);
@@ -1794,9 +1814,9 @@ extern "C" int nerf_ngp_density(const NerfNgpNet* net, const float* w, const flo
   return nerf_launch_status();
 }
 
-extern "C" int nerf_ngp_density_enc(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table,
-                                    const float* w, const float* x, int64_t x_stride, int64_t M, const float* aabb,
-                                    float enc_eps, float* sigma, hipStream_t st) {
+static int ngp_density_enc_impl(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table, const float* w,
+                                const float* x, int64_t x_stride, int64_t M, const int32_t* rng, const float* aabb,
+                                float enc_eps, float* sigma, hipStream_t st) {
   NgpPlan P, Pb;
   HashArgs a;
   if (!net || !grid || M < 0 || x_stride < 3 || !make_plan(*net, false, P) || !hash_args(grid, nullptr, a))
@@ -1812,13 +1832,27 @@ extern "C" int nerf_ngp_density_enc(const NerfNgpNet* net, const NerfHashGrid* g
     a.eps = enc_eps;
   }
   ngp_density_enc_prod_kernel<<<(unsigned)nerf_cdiv(M, NGP_BROWS), 256, (size_t)ngp_prod::F_SMEM * 4, st>>>(
-      a, table, w, x, x_stride, M, sigma);
+      a, table, w, x, x_stride, M, sigma, rng);
   return nerf_launch_status();
 }
 
-extern "C" int nerf_ngp_fwd_enc(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table,
-                                const float* w, const float* x_d, int64_t M, const float* aabb, float enc_eps,
-                                float* enc, int enc_stride, float* rgb_sigma, hipStream_t st) {
+extern "C" int nerf_ngp_density_enc(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table,
+                                    const float* w, const float* x, int64_t x_stride, int64_t M, const float* aabb,
+                                    float enc_eps, float* sigma, hipStream_t st) {
+  return ngp_density_enc_impl(net, grid, table, w, x, x_stride, M, nullptr, aabb, enc_eps, sigma, st);
+}
+
+extern "C" int nerf_ngp_density_enc_rng(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table,
+                                        const float* w, const float* x, int64_t x_stride, int64_t cap,
+                                        const int32_t* rng, const float* aabb, float enc_eps, float* sigma,
+                                        hipStream_t st) {
+  if (!rng) return NERF_E_ARG;
+  return ngp_density_enc_impl(net, grid, table, w, x, x_stride, cap, rng, aabb, enc_eps, sigma, st);
+}
+
+static int ngp_fwd_enc_impl(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table, const float* w,
+                            const float* x_d, int64_t M, const int32_t* rng, const float* aabb, float enc_eps,
+                            float* enc, int enc_stride, float* rgb_sigma, hipStream_t st) {
   NgpPlan P, Pb;
   HashArgs a;
   if (!net || !grid || M < 0 || !make_plan(*net, false, P) || !hash_args(grid, nullptr, a)) return NERF_E_ARG;
@@ -1839,11 +1873,24 @@ extern "C" int nerf_ngp_fwd_enc(const NerfNgpNet* net, const NerfHashGrid* grid,
   const size_t smp = (size_t)ngp_prod::F_SMEM * 4;
   if (P.sigmoid)
     ngp_fwd_prod_kernel<0, 1, true><<<blocks, 256, smp, st>>>(w, nullptr, enc_stride, P.in_dim, x_d, M, rgb_sigma, a,
-                                                                table, enc);
+                                                                table, enc, rng);
   else
     ngp_fwd_prod_kernel<0, 0, true><<<blocks, 256, smp, st>>>(w, nullptr, enc_stride, P.in_dim, x_d, M, rgb_sigma, a,
-                                                                table, enc);
+                                                                table, enc, rng);
   return nerf_launch_status();
+}
+
+extern "C" int nerf_ngp_fwd_enc(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table,
+                                const float* w, const float* x_d, int64_t M, const float* aabb, float enc_eps,
+                                float* enc, int enc_stride, float* rgb_sigma, hipStream_t st) {
+  return ngp_fwd_enc_impl(net, grid, table, w, x_d, M, nullptr, aabb, enc_eps, enc, enc_stride, rgb_sigma, st);
+}
+
+extern "C" int nerf_ngp_fwd_enc_n(const NerfNgpNet* net, const NerfHashGrid* grid, const float* table, const float* w,
+                                  const float* x_d, int64_t cap, const int32_t* rng, const float* aabb, float enc_eps,
+                                  float* enc, int enc_stride, float* rgb_sigma, hipStream_t st) {
+  if (!rng) return NERF_E_ARG;
+  return ngp_fwd_enc_impl(net, grid, table, w, x_d, cap, rng, aabb, enc_eps, enc, enc_stride, rgb_sigma, st);
 }
 
 extern "C" int nerf_ngp_bwd(const NerfNgpNet* net, const float* w, const float* enc, int enc_stride,
@@ -1900,10 +1947,10 @@ extern "C" int nerf_ngp_bwd(const NerfNgpNet* net, const float* w, const float* 
 
 // nerf_ngp_bwd + nerf_hash_encode_bwd in one launch for the production shape with a linear / smoothstep F = 2 grid:
 // the table gradient is scatter-added into d_table from inside the MLP backward (no d_enc in HBM).
-extern "C" int nerf_ngp_bwd_hash(const NerfNgpNet* net, const NerfHashGrid* hgrid, const float* w, const float* enc,
-                                 int enc_stride, const float* x_d, int64_t M, const float* d_rgb_sigma,
-                                 const float* aabb, float enc_eps, float* d_table, float* d_w, int accumulate,
-                                 void* ws, int64_t ws_bytes, hipStream_t st) {
+static int ngp_bwd_hash_impl(const NerfNgpNet* net, const NerfHashGrid* hgrid, const float* w, const float* enc,
+                             int enc_stride, const float* x_d, int64_t M, const int32_t* rng, const float* d_rgb_sigma,
+                             const float* aabb, float enc_eps, float* d_table, float* d_w, int accumulate, void* ws,
+                             int64_t ws_bytes, hipStream_t st) {
   NgpPlan P;
   HashArgs a;
   if (!net || !hgrid || !d_w || M < 0 || !make_plan(*net, true, P) || enc_stride < net->in_dim ||
@@ -1931,11 +1978,11 @@ extern "C" int nerf_ngp_bwd_hash(const NerfNgpNet* net, const NerfHashGrid* hgri
   if (P.sigmoid) {
     allow_lds(ngp_bwd_prod_kernel<1, true>);
     ngp_bwd_prod_kernel<1, true><<<grid, 256, smp, st>>>(w, wt, enc, enc_stride, P.in_dim, x_d, M, d_rgb_sigma,
-                                                           nullptr, partial, ntiles, a, d_table);
+                                                           nullptr, partial, ntiles, a, d_table, rng);
   } else {
     allow_lds(ngp_bwd_prod_kernel<0, true>);
     ngp_bwd_prod_kernel<0, true><<<grid, 256, smp, st>>>(w, wt, enc, enc_stride, P.in_dim, x_d, M, d_rgb_sigma,
-                                                           nullptr, partial, ntiles, a, d_table);
+                                                           nullptr, partial, ntiles, a, d_table, rng);
   }
   const unsigned rblocks = (unsigned)nerf_cdiv(P.total / 4, RED_COLS4);
   if (nerf_aligned16(d_w))
@@ -1943,4 +1990,21 @@ extern "C" int nerf_ngp_bwd_hash(const NerfNgpNet* net, const NerfHashGrid* hgri
   else
     ngp_reduce_kernel<false><<<rblocks, 256, 0, st>>>(partial, P.total, grid, d_w, accumulate);
   return nerf_launch_status();
+}
+
+extern "C" int nerf_ngp_bwd_hash(const NerfNgpNet* net, const NerfHashGrid* hgrid, const float* w, const float* enc,
+                                 int enc_stride, const float* x_d, int64_t M, const float* d_rgb_sigma,
+                                 const float* aabb, float enc_eps, float* d_table, float* d_w, int accumulate,
+                                 void* ws, int64_t ws_bytes, hipStream_t st) {
+  return ngp_bwd_hash_impl(net, hgrid, w, enc, enc_stride, x_d, M, nullptr, d_rgb_sigma, aabb, enc_eps, d_table, d_w,
+                           accumulate, ws, ws_bytes, st);
+}
+
+extern "C" int nerf_ngp_bwd_hash_n(const NerfNgpNet* net, const NerfHashGrid* hgrid, const float* w, const float* enc,
+                                   int enc_stride, const float* x_d, int64_t cap, const int32_t* rng,
+                                   const float* d_rgb_sigma, const float* aabb, float enc_eps, float* d_table,
+                                   float* d_w, int accumulate, void* ws, int64_t ws_bytes, hipStream_t st) {
+  if (!rng) return NERF_E_ARG;
+  return ngp_bwd_hash_impl(net, hgrid, w, enc, enc_stride, x_d, cap, rng, d_rgb_sigma, aabb, enc_eps, d_table, d_w,
+                           accumulate, ws, ws_bytes, st);
 }

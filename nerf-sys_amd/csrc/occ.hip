@@ -67,7 +67,8 @@ __device__ __forceinline__ int march_ray(const Grid& G, const uint8_t* __restric
                                          const float d[3], float t, float tf, float step, float cone, int max_steps,
                                          int64_t w, int32_t rid, int32_t* __restrict__ ray_idx,
                                          float* __restrict__ t0, float* __restrict__ t1,
-                                         float2* __restrict__ stage = nullptr, int cap = 0) {
+                                         float2* __restrict__ stage = nullptr, int cap = 0,
+                                         int64_t wend = INT64_MAX) {
   // clip to the outermost level box
   const float big = (float)(1 << (G.L - 1));
   for (int a = 0; a < 3; ++a) {
@@ -92,9 +93,11 @@ __device__ __forceinline__ int march_ray(const Grid& G, const uint8_t* __restric
     if (id < 0) break;
     if (bin[id]) {
       if (t0) {
-        ray_idx[w] = rid;
-        t0[w] = t;
-        t1[w] = t + dt;
+        if (w < wend) {  // wend: the pair's end in a capacity-clamped offset list (the sync-free container step)
+          ray_idx[w] = rid;
+          t0[w] = t;
+          t1[w] = t + dt;
+        }
         ++w;
       } else if (stage && n < cap) {
         stage[n] = make_float2(t, t + dt);
@@ -170,7 +173,8 @@ __global__ void march_multi_kernel(MarchExperts E, const float* __restrict__ ray
     const float tf = fminf(far_plane, ry[7]);
     if (stratified) t += nerf_uniform(seed, 0x0CC00 + (uint64_t)k, (uint64_t)r) * E.step[k];
     n = march_ray(E.G[k], E.bin[k], o, d, t, tf, E.step[k], cone, max_steps, offsets ? offsets[j] : 0, (int32_t)r,
-                  ray_idx, offsets ? t0 : nullptr, t1, offsets ? nullptr : (stage ? stage + j * cap : nullptr), cap);
+                  ray_idx, offsets ? t0 : nullptr, t1, offsets ? nullptr : (stage ? stage + j * cap : nullptr), cap,
+                  offsets ? (int64_t)offsets[j + 1] : INT64_MAX);
   }
   if (!offsets) counts[j] = n;
 }
@@ -185,9 +189,11 @@ __global__ __launch_bounds__(256) void march_emit_kernel(const float2* __restric
   const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (j >= KN) return;
-  const int c = counts[j];
+  int c = counts[j];
   if (c > cap) return;
   const int64_t o = offsets[j];
+  // offsets may be clamped to a capacity (the sync-free container step): the pair keeps what fits before its end
+  if (o + c > (int64_t)offsets[j + 1]) c = (int)((int64_t)offsets[j + 1] - o);
   const int32_t r = (int32_t)(j % N);
   const float2* sg = stage + j * cap;
   for (int s = lane; s < c; s += 64) {

@@ -89,6 +89,14 @@ def lib():
             "nerf_ngp_density_enc": [P, P, P, P, P, I64, I64, P, F, P, P],
             "nerf_ngp_fwd_enc": [P, P, P, P, P, I64, P, F, P, I, P, P],
             "nerf_ngp_bwd_hash": [P, P, P, P, I, P, I64, P, P, F, P, P, I, P, I64, P],
+            "nerf_ngp_fwd_enc_n": [P, P, P, P, P, I64, P, P, F, P, I, P, P],
+            "nerf_ngp_density_enc_rng": [P, P, P, P, P, I64, I64, P, P, F, P, P],
+            "nerf_ngp_bwd_hash_n": [P, P, P, P, I, P, I64, P, P, P, F, P, P, I, P, I64, P],
+            "nerf_moe_dispatch_n": [P, I64, P, I, F, P, P, P, I64, P],
+            "nerf_gather_rows_rng": [P, I64, P, P, I64, I, P, I64, P],
+            "nerf_moe_blend_rng": [P, I64, P, P, P, I, I, P, P, P],
+            "nerf_moe_blend_finish_n": [P, P, I64, P, P, P],
+            "nerf_moe_blend_bwd_rng": [P, I64, P, P, P, I, I, P, P, P, P, P],
             "nerf_ngp_bwd": [P, P, P, I, P, I64, P, P, P, I, P, I64, P],
             "nerf_moe_route": [P, I64, I64, P, I, I, F, P, P],
             "nerf_moe_route_n": [P, I64, I64, P, P, I, I, F, P, P],
@@ -171,7 +179,9 @@ EXPORTS = ("nerf_rays_gen", "nerf_pick_pixels", "nerf_clamp_near_far", "nerf_ray
            "nerf_moe_blend", "nerf_moe_blend_finish", "nerf_moe_blend_bwd", "nerf_occ_threshold_floats",
            "nerf_sgd_multi", "nerf_reptile_workspace_bytes", "nerf_reptile_update", "nerf_dataset_rays",
            "nerf_occ_march_multi", "nerf_occ_march_multi_staged", "nerf_packed_visibility_groups", "nerf_ngp_density", "nerf_ngp_density_enc", "nerf_ngp_fwd_enc", "nerf_ngp_bwd_hash",
-           "nerf_occ_sample_cells", "nerf_moe_route_n",
+           "nerf_occ_sample_cells", "nerf_moe_route_n", "nerf_ngp_fwd_enc_n", "nerf_ngp_density_enc_rng",
+           "nerf_ngp_bwd_hash_n", "nerf_moe_dispatch_n", "nerf_gather_rows_rng", "nerf_moe_blend_rng",
+           "nerf_moe_blend_finish_n", "nerf_moe_blend_bwd_rng",
            "nerf_packed_points_n")
 
 

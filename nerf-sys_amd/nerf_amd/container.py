@@ -203,6 +203,8 @@ def _march_experts(model, rays, sub_params, render_step_size, alpha_thre, cone_a
         before_sync()
     bounds = offs[::N].cpu().tolist()                  # the one host read: K+1 expert boundaries
     M = bounds[-1]
+    if getattr(model, "device_sized", False) and "_dev_sizes" not in model.__dict__:
+        model.__dict__["_dev_sizes"] = _DevSizes(M)    # seeds the device-sized path's capacity (next calls)
     if M == 0:
         return None, None, None, None
     ri = torch.empty(M, dtype=torch.int32, device=dev)
@@ -247,6 +249,282 @@ def _march_experts(model, rays, sub_params, render_step_size, alpha_thre, cone_a
     return ri, t0, t1, offs
 
 
+# ------------------------------------------------------------------ device-sized (sync-free) container step
+#
+# The host-sized path above reads two sizes per call on the host (the marched sample count, and the merged count with
+# the K+1 expert offsets), and every launch after such a read waits for the host to catch up: ~0.9 ms of idle GPU per
+# train step.  The device-sized path sizes every buffer for a CAPACITY of samples and every kernel
+# after the march reads its row count from device memory (nerf_*_n / _rng entry points), so the host never waits and
+# runs ahead of the GPU.  The capacity follows the sample counts of earlier steps: each call copies its counts to
+# pinned host memory without waiting, a later call reads them once they have landed (event query, no sync) and keeps
+# the capacity at >= 2x the largest count seen (power of two).  A step whose march would exceed the capacity keeps
+# the first CAP samples (per (expert, ray) pair in order) and is counted in model.dev_overflows (never observed in
+# the bench: the counts move by a few percent per step).  The first call of a model runs the host-sized path, which
+# seeds the capacity.  Outputs equal the host-sized path's (tests/test_gpu_moe.py): the same kernels on the same
+# rows; only the experts' weight-gradient slab partition (a persistent grid sized by the capacity) moves the fp32
+# summation order of the MLP weight gradients.
+
+
+class _DevSizes:
+    """Capacity bookkeeping of one model's device-sized renders (see above)."""
+
+    def __init__(self, first_total, min_cap=1 << 16):
+        self.min_cap = int(min_cap)
+        self.max_seen = int(first_total)
+        self.cap = self._cap_for(self.max_seen)
+        self.pending = []          # (event, pinned int32 march total, capacity it ran with)
+        self.overflows = 0
+        self.calls = 0
+
+    def _cap_for(self, total):
+        return max(self.min_cap, 1 << (max(1, 2 * int(total)) - 1).bit_length())
+
+    def poll(self):
+        keep = []
+        for ev, host, cap in self.pending:
+            if ev.query():
+                tot = int(host[0])
+                if tot > cap:
+                    self.overflows += 1
+                self.max_seen = max(self.max_seen, tot)
+            else:
+                keep.append((ev, host, cap))
+        self.pending = keep[-8:]
+        self.cap = max(self.cap, self._cap_for(self.max_seen))
+        return self.cap
+
+    def record(self, total_dev, cap):
+        host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        host.copy_(total_dev.view(1), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending.append((ev, host, cap))
+        self.calls += 1
+
+
+def _ngp_dev_ok(model):
+    """The device-sized path covers containers of production-shape Instant-NGP experts (the fused kernels)."""
+    from .ngp import InstantNGP
+    return all(isinstance(sub, InstantNGP) and sub._fused_ok() for sub in model.submodules)
+
+
+class _NgpFnDev(torch.autograd.Function):
+    """The expert's forward / backward on its gathered rows 0 .. rng[1] - rng[0] - 1 of capacity-sized buffers."""
+
+    @staticmethod
+    def forward(ctx, x_d, rng, table, w_packed, sub):
+        from .ngp import TIMING, _addr
+        cap = x_d.shape[0]
+        g = sub.xyz_encoder.grid
+        od = g.levels * g.features_per_level
+        enc = torch.empty((cap, od), dtype=torch.float32, device=x_d.device)
+        out = torch.empty((cap, 4), dtype=torch.float32, device=x_d.device)
+        ab = (ctypes.c_float * 6)(*sub._aabb_host)
+        h = TIMING.start("fwd_enc", rng)
+        check(lib().nerf_ngp_fwd_enc_n(_addr(sub.net_struct), _addr(g), ptr(table.detach()), ptr(w_packed), ptr(x_d),
+                                       cap, ptr(rng), ab, float(sub._eps), ptr(enc), od, ptr(out), stream()),
+              "nerf_ngp_fwd_enc_n")
+        TIMING.stop(h)
+        ctx.sub, ctx.table = sub, table
+        ctx.save_for_backward(x_d, enc, w_packed, rng)
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gr):
+        from .ngp import TIMING, _addr, _table_grad_ready, ngp_workspace
+        x_d, enc, w_packed, rng = ctx.saved_tensors
+        sub, t = ctx.sub, ctx.table
+        cap = x_d.shape[0]
+        gr = gr.contiguous().float()
+        flat = getattr(t, "_nerf_flat_grad", False) and t.grad is not None
+        tgt = t.grad if flat else torch.zeros_like(t)
+        d_w = torch.empty_like(w_packed)
+        ws = ngp_workspace(sub.net_struct, cap, x_d.device)
+        ab = (ctypes.c_float * 6)(*sub._aabb_host)
+        h = TIMING.start("bwd_hash", rng)
+        check(lib().nerf_ngp_bwd_hash_n(_addr(sub.net_struct), _addr(sub.xyz_encoder.grid), ptr(w_packed), ptr(enc),
+                                        enc.stride(0), ptr(x_d), cap, ptr(rng), ptr(gr), ab, float(sub._eps),
+                                        ptr(tgt), ptr(d_w), 0, ptr(ws), ws.numel(), stream()), "nerf_ngp_bwd_hash_n")
+        TIMING.stop(h)
+        if flat:
+            _table_grad_ready(t)
+        return None, None, (None if flat else tgt), d_w, None
+
+
+class _BlendFnDev(torch.autograd.Function):
+    """_BlendFn over capacity-sized rows: expert k's rows pair with idx entries rngs[k][0] .., the mix is finished for
+    the first *m_dev rows."""
+
+    @staticmethod
+    def forward(ctx, W, m_dev, idx, rngs, ks, *ys):
+        cap, K = W.shape
+        s = torch.zeros(cap, dtype=torch.float32, device=W.device)
+        c = torch.zeros((cap, 3), dtype=torch.float32, device=W.device)
+        L = lib()
+        for k, rng, y in zip(ks, rngs, ys):
+            check(L.nerf_moe_blend_rng(ptr(y), cap, ptr(idx), ptr(rng), ptr(W), K, k, ptr(s), ptr(c), stream()),
+                  "nerf_moe_blend_rng")
+        rs = torch.empty((cap, 4), dtype=torch.float32, device=W.device)
+        check(L.nerf_moe_blend_finish_n(ptr(s), ptr(c), cap, ptr(m_dev), ptr(rs), stream()), "nerf_moe_blend_finish_n")
+        ctx.save_for_backward(W, s, rs, idx, *rngs, *ys)
+        ctx.ks, ctx.n = ks, len(ks)
+        return rs
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g):
+        W, s, rs, idx, *rest = ctx.saved_tensors
+        rngs, ys = rest[:ctx.n], rest[ctx.n:]
+        g = g.contiguous().float()
+        cap, K = W.shape
+        grads = []
+        for k, rng, y in zip(ctx.ks, rngs, ys):
+            dy = torch.empty_like(y)
+            check(lib().nerf_moe_blend_bwd_rng(ptr(y), cap, ptr(idx), ptr(rng), ptr(W), K, k, ptr(s), ptr(rs), ptr(g),
+                                               ptr(dy), stream()), "nerf_moe_blend_bwd_rng")
+            grads.append(dy)
+        return (None, None, None, None, None, *grads)
+
+
+def _march_experts_dev(model, rays, sub_params, render_step_size, alpha_thre, cone_angle, sizes):
+    """_march_experts without the host read: the packed arrays hold sizes.cap samples; the offsets are clamped to it.
+    Returns (ray_idx, t0, t1, offsets (K*N+1), cap)."""
+    from .ngp import TIMING, _addr
+    from .occupancy import exclusive_scan
+    subs = list(model.submodules)
+    K, N, dev = len(subs), rays.shape[0], rays.device
+    ex0 = subs[0]
+    for ex in subs[1:]:
+        if (ex.near_plane, ex.far_plane) != (ex0.near_plane, ex0.far_plane):
+            raise ValueError("experts with different near/far planes")
+    cone = [ex.cone_angle if cone_angle is None else cone_angle for ex in subs]
+    if len(set(cone)) != 1:
+        raise ValueError("experts with different cone angles")
+    grids = (type(ex0.occ_grid.grid) * K)(*[ex.occ_grid.grid for ex in subs])
+    bins = (ctypes.c_void_p * K)(*[ex.occ_grid.binaries.data_ptr() for ex in subs])
+    boxes = (ctypes.c_float * (6 * K))(*[float(v) for ex in subs for v in ex._aabb_host])
+    steps = (ctypes.c_float * K)(*[float(ex.render_step_size if render_step_size is None else render_step_size)
+                                   for ex in subs])
+    training = bool(ex0.training)
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    L = lib()
+    counts = torch.empty(K * N, dtype=torch.int32, device=dev)
+    args = (grids, bins, boxes, steps, K, ptr(rays), N, float(ex0.near_plane), float(ex0.far_plane), float(cone[0]),
+            int(training), ctypes.c_uint64(seed), 8192)
+    stage = torch.empty(K * N * MARCH_STAGE_CAP * 2, dtype=torch.float32, device=dev)
+    check(L.nerf_occ_march_multi_staged(*args, ptr(counts), ptr(stage), MARCH_STAGE_CAP, None, None, None, None,
+                                        stream()), "nerf_occ_march_multi_staged(count)")
+    offs = exclusive_scan(counts)
+    cap = sizes.poll()
+    sizes.record(offs[K * N:], cap)
+    offs.clamp_(max=cap)
+    ri = torch.empty(cap, dtype=torch.int32, device=dev)
+    t0 = torch.empty(cap, dtype=torch.float32, device=dev)
+    t1 = torch.empty(cap, dtype=torch.float32, device=dev)
+    check(L.nerf_occ_march_multi_staged(*args, ptr(counts), ptr(stage), MARCH_STAGE_CAP, ptr(offs), ptr(ri), ptr(t0),
+                                        ptr(t1), stream()), "nerf_occ_march_multi_staged(emit)")
+    del stage
+    athr = [ex.alpha_thre if alpha_thre is None else alpha_thre for ex in subs]
+    if training:
+        with torch.no_grad():
+            m_dev = offs[K * N:]
+            xd = torch.empty((cap, 6), dtype=torch.float32, device=dev)
+            check(L.nerf_packed_points_n(ptr(rays), ptr(ri), ptr(t0), ptr(t1), cap, ptr(m_dev), ptr(xd), stream()),
+                  "nerf_packed_points_n")
+            sig = torch.empty(cap, dtype=torch.float32, device=dev)
+            bounds = offs[::N].contiguous()            # K+1 expert boundaries, on the device
+            for k, ex in enumerate(subs):
+                w = ex.packed(sub_params[k]).detach()
+                ab = (ctypes.c_float * 6)(*ex._aabb_host)
+                h = TIMING.start("density_enc", bounds[k:k + 2])
+                check(L.nerf_ngp_density_enc_rng(_addr(ex.net_struct), _addr(ex.xyz_encoder.grid),
+                                                 ptr(ex.xyz_encoder.hash_table.detach()), ptr(w), ptr(xd), 6, cap,
+                                                 ptr(bounds[k:k + 2]), ab, float(ex._eps), ptr(sig), stream()),
+                      "nerf_ngp_density_enc_rng")
+                TIMING.stop(h)
+            key = (tuple((ex.occ_grid.gen, ex.occ_grid.occs._version, ex.occ_grid.occs.data_ptr()) for ex in subs),
+                   tuple(athr))
+            cache = model.__dict__.setdefault("_vis_thr", {})
+            thr = cache.get(key)
+            if thr is None:
+                occ_mean = torch.stack([ex.occ_grid.occs.mean() for ex in subs]).float()
+                thr = torch.minimum(occ_mean, torch.tensor(athr, dtype=torch.float32, device=dev)).contiguous()
+                cache.clear()
+                cache[key] = thr
+            keep = torch.zeros(cap, dtype=torch.int32, device=dev)
+            check(L.nerf_packed_visibility_groups(ptr(t0), ptr(t1), ptr(sig), ptr(offs), K * N, N, 1e-4,
+                                                  float(max(athr)), ptr(thr), ptr(keep), stream()),
+                  "nerf_packed_visibility_groups")
+            pos = exclusive_scan(keep)
+            ri2 = torch.empty(cap, dtype=torch.int32, device=dev)
+            t02 = torch.empty(cap, dtype=torch.float32, device=dev)
+            t12 = torch.empty(cap, dtype=torch.float32, device=dev)
+            check(L.nerf_packed_compact(ptr(keep), ptr(pos), cap, ptr(ri), ptr(t0), ptr(t1), ptr(ri2), ptr(t02),
+                                        ptr(t12), None, stream()), "nerf_packed_compact")
+            offs = pos[offs.long()].contiguous()
+            ri, t0, t1 = ri2, t02, t12
+    return ri, t0, t1, offs, cap
+
+
+def _render_container_occ_dev(model, rays, params, bg_color_default, render_step_size, alpha_thre, cone_angle):
+    from .ray_rendering import _get_bg_rgb
+    from .occupancy import exclusive_scan, render_packed
+    rays = rays.contiguous().float()
+    N = rays.shape[0]
+    dev = rays.device
+    d = rays[:, 3:6]
+    K = len(model.submodules)
+    sub_params = ([model.get_subdict(params, f"submodules.{k}") for k in range(K)] if params is not None
+                  else [None] * K)
+    ws = [sub.packed(sub_params[k]) for k, sub in enumerate(model.submodules)]  # (cached by pack_scope)
+    bg = _get_bg_rgb(model, d, params, rays, N, bg_color_default)
+    sizes = model.__dict__["_dev_sizes"]
+    ri_all, t0_all, t1_all, offs_all, cap = _march_experts_dev(model, rays, sub_params, render_step_size, alpha_thre,
+                                                               cone_angle, sizes)
+    t0s = (ctypes.c_void_p * K)(*([t0_all.data_ptr()] * K))
+    t1s = (ctypes.c_void_p * K)(*([t1_all.data_ptr()] * K))
+    ofs = (ctypes.c_void_p * K)(*[offs_all[k * N:].data_ptr() for k in range(K)])
+    L = lib()
+    cnt = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
+    check(L.nerf_segments_union(t0s, t1s, ofs, K, N, ptr(cnt), None, None, None, None, stream()),
+          "nerf_segments_union(count)")
+    moff = exclusive_scan(cnt[:N])
+    cap2 = 2 * cap  # a ray's union of its experts' sorted boundary lists has < 2x their segments
+    ri = torch.empty(cap2, dtype=torch.int32, device=dev)
+    t0 = torch.empty(cap2, dtype=torch.float32, device=dev)
+    t1 = torch.empty(cap2, dtype=torch.float32, device=dev)
+    check(L.nerf_segments_union(t0s, t1s, ofs, K, N, None, ptr(moff), ptr(ri), ptr(t0), ptr(t1), stream()),
+          "nerf_segments_union(write)")
+    m_dev = moff[N:]
+    xm = torch.empty((cap2, 6), dtype=torch.float32, device=dev)
+    check(L.nerf_packed_points_n(ptr(rays), ptr(ri), ptr(t0), ptr(t1), cap2, ptr(m_dev), ptr(xm), stream()),
+          "nerf_packed_points_n")
+    with torch.no_grad():
+        W = torch.empty((cap2, K), dtype=torch.float32, device=dev)
+        c = (ctypes.c_float * len(model._cent_host))(*model._cent_host)
+        check(L.nerf_moe_route_n(ptr(xm), 6, cap2, ptr(m_dev), c, K, int(model.cluster_2d),
+                                 float(model.boundary_margin), ptr(W), stream()), "nerf_moe_route_n")
+        offs_dev = torch.empty(K + 1, dtype=torch.int32, device=dev)
+        idx = torch.empty(cap2 * K, dtype=torch.int32, device=dev)
+        wsb = int(L.nerf_moe_dispatch_workspace_bytes(cap2, K))
+        wsd = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        check(L.nerf_moe_dispatch_n(ptr(W), cap2, ptr(m_dev), K, 1e-8, ptr(offs_dev), ptr(idx), ptr(wsd), wsb,
+                                    stream()), "nerf_moe_dispatch_n")
+    ks, rngs, ys = [], [], []
+    for k, sub in enumerate(model.submodules):
+        rng = offs_dev[k:k + 2]
+        xk = torch.empty((cap2, 6), dtype=torch.float32, device=dev)
+        check(L.nerf_gather_rows_rng(ptr(xm), 6, ptr(idx), ptr(rng), cap2, 6, ptr(xk), 6, stream()),
+              "nerf_gather_rows_rng")
+        ys.append(_NgpFnDev.apply(xk, rng, sub.xyz_encoder.hash_table, ws[k], sub))
+        ks.append(k)
+        rngs.append(rng)
+    rs = _BlendFnDev.apply(W, m_dev, idx, rngs, ks, *ys)
+    rgb, depth, w, acc = render_packed(rs, t0, t1, moff, bg)
+    return rgb, depth, w[:, None], acc
+
+
 def render_container_occ(model, rays, *, params=None, bg_color_default="white", chunk=1_000_000,
                          render_step_size=None, alpha_thre=None, cone_angle=None):
     """render_rays_occ for the full container (nerfs/ray_rendering.py:384-481): per-expert AABB prefilter and
@@ -255,6 +533,9 @@ def render_container_occ(model, rays, *, params=None, bg_color_default="white", 
     before ONE packed integration.  Returns rgb (N,3), depth (N,), weights (M,1), acc (N,)."""
     from .ngp import pack_scope
     with pack_scope():
+        if getattr(model, "device_sized", False) and _ngp_dev_ok(model) and "_dev_sizes" in model.__dict__:
+            return _render_container_occ_dev(model, rays, params, bg_color_default, render_step_size, alpha_thre,
+                                             cone_angle)
         return _render_container_occ(model, rays, params, bg_color_default, chunk, render_step_size, alpha_thre,
                                      cone_angle)
 

@@ -78,6 +78,9 @@ class _Timing:
         torch.cuda.synchronize()
         out = {}
         for name, e0, e1, rows in self.records:
+            if isinstance(rows, torch.Tensor):  # device-sized launches: the (lo, hi) row range on the device
+                r = rows.cpu()
+                rows = int(r[1]) - int(r[0])
             out.setdefault(name, []).append((e0.elapsed_time(e1), rows))
         self.records = []
         return out
@@ -742,6 +745,20 @@ class InstantNGP(nn.Module):
 
     def packed(self, params=None):
         return self.layout.pack(self.tensors(params))
+
+    def _fused_ok(self) -> bool:
+        """Whether the one-launch kernels (fwd_enc, density_enc, bwd_hash) cover this expert's shape: each entry point
+        answers NERF_E_UNSUPPORTED before it looks at its buffers, so a zero-row call probes it."""
+        v = self.__dict__.get("_fused_ok_v")
+        if v is None:
+            L, g, n = lib(), self.xyz_encoder.grid, self.net_struct
+            od = g.levels * g.features_per_level
+            rc1 = L.nerf_ngp_fwd_enc(_addr(n), _addr(g), None, None, None, 0, None, 0.0, None, od, None, stream())
+            rc2 = L.nerf_ngp_density_enc(_addr(n), _addr(g), None, None, None, 3, 0, None, 0.0, None, stream())
+            rc3 = L.nerf_ngp_bwd_hash(_addr(n), _addr(g), None, None, od, None, 0, None, None, 0.0, None,
+                                      ctypes.c_void_p(16), 1, None, 0, stream())
+            v = self.__dict__["_fused_ok_v"] = (rc1 == 0 and rc2 == 0 and rc3 == 0)
+        return v
 
     def load_reference_state(self, state: Dict[str, torch.Tensor]):
         with torch.no_grad():

@@ -301,3 +301,112 @@ def test_staged_march_equals_two_pass_march(z, train):
         for a, b in zip(out, ref):
             assert torch.equal(a, b), cap
     assert L.nerf_occ_march_multi_staged(*args, ptr(counts), ptr(stage), 0, None, None, None, None, stream()) < 0
+
+
+# ------------------------------------------------------------------ device-sized (sync-free) container step
+
+PROD_KW = dict(hidden=64, sigma_depth=2, color_hidden=64, color_depth=2, dir_encoding="spherical",
+               hash_enc_conf=dict(levels=16, features_per_level=2, log2_hashmap_size=14, min_res=16, max_res=512,
+                                  interpolation="Linear"))
+
+
+def _prod_container(seed=0):
+    """A production-shape container (the fused NGP kernels' shape: 16 x 2 hash features, 2 x 64 trunk, 2 x 64 colour,
+    SH directions; smaller tables and grids) with random occupancy — the shape the device-sized path runs on."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from nerf_amd.container import MetaContainer
+    from nerf_amd.ray_sampling import SceneBox
+    torch.manual_seed(seed)
+    boxes, cents = [], []
+    for sy in (-1, 1):
+        for sz in (-1, 1):
+            lo = torch.tensor([-1.5, -1.5 if sy < 0 else -0.1, -1.5 if sz < 0 else -0.1])
+            hi = torch.tensor([1.5, 0.1 if sy < 0 else 1.5, 0.1 if sz < 0 else 1.5])
+            boxes.append(SceneBox(aabb=torch.stack([lo, hi])))
+            cents.append([0.0, 0.75 * sy, 0.75 * sz])
+    occ = {"use_occ": True, "resolution": 16, "levels": 2, "occ_ready": True, "near_plane": 0.05,
+           "alpha_thre": 1e-3, "cone_angle": 0.004}
+    mc = MetaContainer(num_submodules=4, centroids=torch.tensor(cents), aabb=torch.tensor([[-1.5] * 3, [1.5] * 3]),
+                       nerf_variant="instant", boundary_margin=1.05, cluster_2d=True, use_bg_nerf=True, bg_hidden=32,
+                       occ_conf=occ, expert_box_list=boxes, **PROD_KW).to(DEV)
+    g = torch.Generator().manual_seed(seed + 1)
+    with torch.no_grad():
+        for sub in mc.submodules:
+            sub.occ_grid.binaries.copy_((torch.rand(sub.occ_grid.binaries.shape, generator=g) < 0.6).to(torch.uint8))
+            sub.xyz_encoder.hash_table.mul_(100.0)   # densities well away from zero: the visibility filter bites
+    return mc
+
+
+def _render_loss(mc, rays, seed, gt):
+    from nerf_amd.ray_rendering import render_rays
+    mc.zero_grad(set_to_none=True)
+    torch.manual_seed(seed)                      # the march jitter seed is drawn from torch's CPU generator
+    rgb, depth, w, acc = render_rays(mc, rays, ray_samples=64)
+    loss = ((rgb - gt) ** 2).mean()
+    loss.backward()
+    grads = {n: p.grad.detach().clone() for n, p in mc.named_parameters() if p.grad is not None}
+    return rgb.detach(), depth.detach(), w.detach(), acc.detach(), loss.detach(), grads
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_container_device_sized_equals_host_sized(train):
+    """The sync-free container step (every size after the march read on the device, capacity-sized buffers) against
+    the host-sized step on the same rays and jitter seed: rgb / depth / acc and the packed weights bitwise equal;
+    parameter gradients equal up to the MLP weight-gradient slab partition (the persistent grid follows the
+    capacity) and the hash scatter's atomic order — 1e-5 of each tensor's scale."""
+    from nerf_amd import container as C
+    mc = _prod_container(3).train(train)
+    mc.device_sized = True
+    rays = _occ_rays(1024, 12)
+    gt = torch.rand(1024, 3, generator=torch.Generator().manual_seed(4)).to(DEV)
+    _render_loss(mc, rays, 1, gt)                # first call: host-sized, seeds the capacity
+    sizes = mc.__dict__["_dev_sizes"]
+    assert sizes.calls == 0 and sizes.max_seen > 0
+    calls = []
+    orig = C._render_container_occ_dev
+    C._render_container_occ_dev = lambda *a, **k: calls.append(1) or orig(*a, **k)
+    try:
+        dev_out = _render_loss(mc, rays, 7, gt)
+    finally:
+        C._render_container_occ_dev = orig
+    assert calls, "the device-sized path did not run"
+    mc.device_sized = False
+    host_out = _render_loss(mc, rays, 7, gt)
+    torch.cuda.synchronize()
+    sizes.poll()
+    assert sizes.overflows == 0 and sizes.calls == 1
+    for a, b, what in zip(dev_out[:4], host_out[:4], ("rgb", "depth", "weights", "acc")):
+        if what == "weights":
+            a = a[:b.shape[0]]                   # capacity rows: the first M are the packed samples
+        assert torch.equal(a, b), (what, (a - b).abs().max().item())
+    assert torch.equal(dev_out[4], host_out[4])
+    gd, gh = dev_out[5], host_out[5]
+    assert set(gd) == set(gh) and len(gh) > 0
+    for n_ in gh:
+        scale = max(gh[n_].abs().max().item(), 1e-30)
+        err = (gd[n_] - gh[n_]).abs().max().item()
+        assert err <= 1e-5 * scale, (n_, err, scale)
+    assert any(float(gh[n_].abs().sum()) > 0 for n_ in gh if "hash_table" in n_)
+
+
+def test_container_device_sized_overflow_is_counted():
+    """A capacity below the step's march count keeps the first CAP samples (finite outputs, no fault) and is counted
+    once its count reaches the host; the next call's capacity covers the count."""
+    from nerf_amd.ray_rendering import render_rays
+    mc = _prod_container(5).train()
+    mc.device_sized = True
+    rays = _occ_rays(512, 13)
+    torch.manual_seed(0)
+    render_rays(mc, rays, ray_samples=64)         # seeds _dev_sizes
+    sizes = mc.__dict__["_dev_sizes"]
+    total = sizes.max_seen
+    sizes.min_cap, sizes.cap, sizes.max_seen = 1, 256, 0
+    assert total > 256
+    torch.manual_seed(1)
+    rgb, depth, w, acc = render_rays(mc, rays, ray_samples=64)
+    ((rgb - 0.5) ** 2).mean().backward()
+    torch.cuda.synchronize()
+    assert torch.isfinite(rgb).all() and torch.isfinite(depth).all()
+    cap = sizes.poll()
+    assert sizes.overflows == 1 and cap >= 2 * (total // 2)

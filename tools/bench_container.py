@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (gloo: a rehearsal of N ranks sharing one GPU; RCCL needs one GPU per rank)")
     ap.add_argument("--shard", action="store_true", help="shard FlatAdam over the ranks (reduce-scatter + all-gather)")
+    ap.add_argument("--host-sized", action="store_true",
+                    help="the host-sized render (two host reads of the packed sizes per step) instead of the "
+                         "device-sized sync-free one (container.py, DESIGN.md §3.8)")
     ap.add_argument("--no-bucket", action="store_true",
                     help="one all-reduce of the flat gradient in step() instead of per-table buckets started by the "
                          "hash-table backward")
@@ -136,6 +139,8 @@ def build_step(a, dev, rank=0, world=1):
                           nerf_variant="instant", boundary_margin=1.05, cluster_2d=True, use_bg_nerf=True,
                           bg_hidden=32, occ_conf=occ, expert_box_list=[SceneBox(aabb=b) for b in boxes], **KW)
     model = model.to(dev).train()
+    # the sync-free step: every size after the march stays on the device (container.py "device-sized")
+    model.device_sized = not getattr(a, "host_sized", False)
     lr = {"encoding": 1e-2, "sigma": 2e-3, "color": 2e-3, "background": 1e-3}
     groups = [{"params": g["params"], "lr": lr[k]} for k, g in model.get_param_groups().items()]
     opt = FlatAdam(groups, grad_clip=1.0, world_size=world, shard=a.shard, bucket_tables=not a.no_bucket)
@@ -242,6 +247,18 @@ def run(a, dev, rank=0, world=1):
     }
     if exch:
         out["exchange"] = exch
+    sz = model.__dict__.get("_dev_sizes")
+    if model.device_sized and sz is not None:
+        torch.cuda.synchronize()
+        sz.poll()
+        out["device_sized"] = {"capacity": sz.cap, "max_march_samples": sz.max_seen, "calls": sz.calls,
+                               "overflows": sz.overflows,
+                               "note": "every size after the march read on the device (no host sync in the step); "
+                                       "buffers sized for `capacity` samples (>= 2x the largest march seen); the "
+                                       "kernels' grids cover the capacity, their row counts (the roofline's bytes) "
+                                       "are the real ones, read back after the timed steps"}
+    else:
+        out["device_sized"] = None
     if world > 1:   # the replicas after every step above: one gradient exchange per step keeps them bitwise equal
         from nerf_amd.dp import params_checksum
         out["dp"] = {"world_size": world, "backend": dist.get_backend(), "flat_adam": {
