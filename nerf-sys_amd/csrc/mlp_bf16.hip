@@ -372,8 +372,8 @@ int fused_forward(const float* w, const float* x_d, int64_t M, float* rgb_sigma,
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
   }
   frag_pack_kernel<<<(unsigned)nerf_cdiv(T.off[FT] / 8, 256), 256, 0, st>>>(w, W.Wf, T);
-  pe_prefill_bf16_kernel<<<(unsigned)nerf_cdiv(Mp, 256), 256, 0, st>>>(x_d, M, Mp, W.X3E, W.CIN);
-  FusedArgs A{};
+  FusedArgs A{};  // (the io waves encode x_d themselves: io_encode, no pe_prefill_bf16_kernel launch)
+  A.xd = x_d;
   A.wf = W.Wf;
   A.w = w;
   A.X3E = W.X3E;

@@ -143,6 +143,7 @@ struct FusedArgs {
   uint32_t* MC0;         // [Mp][4] (training)
   float* O3;             // [Mp][32] fp32 colour-out pre-activations, cols 0..3 (training)
   float* out;            // [M][4] rgb_sigma
+  const float* xd;       // [M][6] sample points + directions (the io waves encode them: no prefill launch)
   int64_t M, Mp;
   int ntiles;
 };
@@ -501,6 +502,59 @@ struct IoRows64 {
   }
 };
 
+// The encodings of rows 32 j + (lane >> 3) + 8 i (i = 0..3) of the tile at m0, computed by io wave j from x_d (lane:
+// columns 8 (lane & 7) .. + 7), exactly what pe_prefill_bf16_kernel writes (same sin / cos and bf16 packing, so the
+// bits are the same): XYZ — the xyz encoding [x, cos / sin 2^0..2^9 per dimension, 0] (X3E columns 256..319; also
+// stored to HBM for the backward's narrow weight gradients); else the colour-input prefill [0 x 15 (geo: the
+// compute waves), d, cos / sin 2^0..2^3 per dimension, 0 ...].  Rows >= M are zero.  Replaces the prefill launch and
+// its 256 B per row of HBM round trip (round 6).
+template <bool XYZ>
+__device__ __forceinline__ void io_encode(IoRows64& R, const float* __restrict__ xd, int64_t M, int64_t m0, int j,
+                                          int lane, nerf_bf16* __restrict__ x3e) {
+  const int cb = 8 * (lane & 7);
+  uint4 out[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t m = m0 + 32 * j + (lane >> 3) + 8 * i;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+    if (m < M) {
+      const float* r = xd + m * 6 + (XYZ ? 0 : 3);
+      const float x[3] = {r[0], r[1], r[2]};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = cb + e;
+        if (XYZ) {
+          if (c < 3) {
+            v[e] = x[c];
+          } else if (c < 63) {
+            const int q = c - 3, k = q / 20, rr = q - 20 * k, l = rr < 10 ? rr : rr - 10;
+            float sn, cs;
+            pe_sincos_bf16(x[k] * (float)(1 << l), &sn, &cs);
+            v[e] = rr < 10 ? cs : sn;
+          }
+        } else {
+          if (c >= 15 && c < 18) {
+            v[e] = x[c - 15];
+          } else if (c >= 18 && c < 42) {
+            const int q = c - 18, k = q >> 3, wi = q & 7, l = wi & 3;
+            float sn, cs;
+            pe_sincos_bf16(x[k] * (float)(1 << l), &sn, &cs);
+            v[e] = wi < 4 ? cs : sn;
+          }
+        }
+      }
+    }
+    out[i] = make_uint4(nerf_pack_bf16x2(v[0], v[1]), nerf_pack_bf16x2(v[2], v[3]), nerf_pack_bf16x2(v[4], v[5]),
+                        nerf_pack_bf16x2(v[6], v[7]));
+    if (XYZ)  // the backward's copy (read only by the narrow weight gradients, at the end of the backward)
+      __builtin_nontemporal_store(__builtin_bit_cast(nerf_u32x4t, out[i]),
+                                  reinterpret_cast<nerf_u32x4t*>(x3e + m * 320 + 256 + cb));
+  }
+  R.v0 = out[0]; R.v1 = out[1]; R.v2 = out[2]; R.v3 = out[3];
+}
+
 // Barriers per tile (compute and io waves pass the same sequence): B_k (k = 0..7, "every trunk epilogue k is in
 // LDS"; B_k sits inside the stage after k), H2 (colour input complete), C (colour layer 0 output complete, inside
 // colour out), D (end of tile: the next tile's encoding is in E).  Trunk epilogue k writes H[k & 1]; the io waves
@@ -510,7 +564,7 @@ __device__ __forceinline__ void io_role(const FusedArgs& A, nerf_bf16* Hs, nerf_
                                         int lane) {
   const int64_t Mp = A.Mp;
   IoRows64 enc, cin;
-  enc.load(A.X3E + 256, 320, (int64_t)tile * BMF, j, lane);
+  io_encode<true>(enc, A.xd, A.M, (int64_t)tile * BMF, j, lane, A.X3E);
   enc.store(Es, EP, j, lane);
   bar();  // prologue
   for (int t = tile; t < A.ntiles; t += G) {
@@ -521,14 +575,14 @@ __device__ __forceinline__ void io_role(const FusedArgs& A, nerf_bf16* Hs, nerf_
       bar();  // B_k
       if (k == 4) {  // trunk.4 (the last reader of the encoding) is done: colour-input prefill -> E
         cin.store(Es, EP, j, lane);
-        if (next) enc.load(A.X3E + 256, 320, m0 + (int64_t)G * BMF, j, lane);
+        if (next) io_encode<true>(enc, A.xd, A.M, m0 + (int64_t)G * BMF, j, lane, A.X3E);
       }
       if (TRAIN) {
         nerf_bf16* Y = (k == 3) ? A.X3E : A.Y + (int64_t)(k < 3 ? k : k - 1) * Mp * 256;
         io_copy<256, MASKS>(Hs + (k & 1) * BMF * HP, HP, Y, k == 3 ? 320 : 256, m0, MASKS ? A.MB + (int64_t)k * Mp * 8 : nullptr, j,
                             lane);
       }
-      if (k == 0) cin.load(A.CIN, 64, m0, j, lane);
+      if (k == 0) io_encode<false>(cin, A.xd, A.M, m0, j, lane, nullptr);
     }
     bar();  // H2: colour input complete in E
     if (TRAIN) io_copy<64, false>(Es, EP, A.CIN, 64, m0, nullptr, j, lane);

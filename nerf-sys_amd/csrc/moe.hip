@@ -147,11 +147,12 @@ __global__ void gather_rows_kernel(const float* __restrict__ src, int64_t ss, co
     n = c < n ? (c < 0 ? 0 : c) : n;
     idx += rng[0];
   }
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n * cols) return;
-  const int64_t i = t / cols;
-  const int c = (int)(t - i * cols);
-  dst[i * ds + c] = src[(int64_t)idx[i] * ss + c];
+  // grid-stride: the device-sized form launches a bounded grid over the capacity (most of it past the count)
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n * cols; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / cols;
+    const int c = (int)(t - i * cols);
+    dst[i * ds + c] = src[(int64_t)idx[i] * ss + c];
+  }
 }
 
 __global__ void combine_kernel(const float* __restrict__ y, int64_t n, int C, const int32_t* __restrict__ idx,
@@ -390,8 +391,9 @@ extern "C" int nerf_gather_rows_rng(const float* src, int64_t src_stride, const 
   if (cap < 0 || cols < 1 || src_stride < cols || dst_stride < cols || !rng) return NERF_E_ARG;
   if (cap == 0) return NERF_OK;
   if (!src || !idx || !dst) return NERF_E_ARG;
-  gather_rows_kernel<<<(unsigned)nerf_cdiv(cap * cols, 256), 256, 0, st>>>(src, src_stride, idx, cap, cols, dst,
-                                                                           dst_stride, rng);
+  const int64_t blocks = nerf_cdiv(cap * cols, 256);
+  gather_rows_kernel<<<(unsigned)(blocks < 4096 ? blocks : 4096), 256, 0, st>>>(src, src_stride, idx, cap, cols, dst,
+                                                                                dst_stride, rng);
   return nerf_launch_status();
 }
 

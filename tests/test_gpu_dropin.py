@@ -116,8 +116,10 @@ def test_autocast_dispatches_16bit_kernels(K):
 def test_reference_amp_loop_body_with_gradscaler(K):
     """runtime_adapt.py:290-310 with use_amp=True, as written, on the drop-in surface: 40 steps of 1024-ray batches
     from a synthetic 100x100 scene, 64 + 128.  The AMP loop learns, its loss stays within 15 % of the fp32 loop's
-    (same seed, same batches, same jitter draws), and GradScaler never skips a step (no inf / nan gradient: its
-    scale is still the initial 2^16, which it halves on every inf)."""
+    (same seed, same batches, same jitter draws), and GradScaler's skipped steps are counted from its scale history
+    (it halves the scale on every step whose gradient holds an inf / nan and skips that step): at most 4 of 40, each
+    printed with its step (fp16 rounding of a large gradient can overflow once in a while; the 6-step oracle test
+    pins the scale exactly)."""
     from nerf_amd.losses import compute_mse_loss
     from nerf_amd.scene import make_blender_scene
     from nerf_amd.trainer import RayBatcher
@@ -131,7 +133,7 @@ def test_reference_amp_loop_body_with_gradscaler(K):
         base = _model(pc, pf).train()
         optimizer = _adam(base, 2e-3, 2e-3)
         scaler = torch.amp.GradScaler("cuda", enabled=use_amp)
-        ls = []
+        ls, scales = [], []
         for step in range(40):
             rays, rgbs = rb.batch(1024, seed=step)
             optimizer.zero_grad()
@@ -144,9 +146,13 @@ def test_reference_amp_loop_body_with_gradscaler(K):
             scaler.step(optimizer)
             scaler.update()
             ls.append(float(loss.detach()))
+            scales.append(scaler.get_scale() if use_amp else 1.0)
         if use_amp:
-            print(f"GradScaler scale after 40 AMP steps: {scaler.get_scale()}")
-            assert scaler.get_scale() >= 2.0 ** 12, f"GradScaler skipped many steps (scale {scaler.get_scale()})"
+            prev = [65536.0] + scales[:-1]
+            skipped = [i for i, (a0, a1) in enumerate(zip(prev, scales)) if a1 < a0]
+            print(f"GradScaler: scale after 40 AMP steps {scaler.get_scale()}, skipped steps {skipped}")
+            assert len(skipped) <= 4, f"GradScaler skipped {len(skipped)} steps: {skipped}"
+            assert all(a1 in (a0 / 2, a0) for a0, a1 in zip(prev, scales)), scales  # no growth inside 40 steps
         curves[use_amp] = torch.tensor(ls)
     a, b = curves[True], curves[False]
     assert torch.isfinite(a).all()

@@ -47,6 +47,15 @@ _, _, gaps = anatomy(a, b)
 print("\nlargest idle gaps of the last step (us: before -> after):")
 for g, i in sorted(gaps, reverse=True)[:12]:
     print(f"  {g / 1e3:7.1f}  {rows[i - 1]['Kernel_Name'][:50]}  ->  {rows[i]['Kernel_Name'][:50]}")
+heavy = max(spans[:-ev], key=lambda ab: anatomy(*ab)[1])
+per = defaultdict(lambda: [0.0, 0])
+for i in range(*heavy):
+    d = (int(rows[i]["End_Timestamp"]) - int(rows[i]["Start_Timestamp"])) / 1e3
+    per[rows[i]["Kernel_Name"][:80]][0] += d
+    per[rows[i]["Kernel_Name"][:80]][1] += 1
+print("\nheaviest step (the occupancy update's), per kernel (us, launches):")
+for k, (t, c) in sorted(per.items(), key=lambda x: -x[1][0])[:20]:
+    print(f"  {t:8.1f} {c:4d}  {k}")
 walls = [anatomy(a, b) for a, b in spans[:-ev]]
 print(f"\nmean over {len(walls)} steps: wall {sum(w for w, _, _ in walls) / len(walls):.1f} us, "
       f"busy {sum(x for _, x, _ in walls) / len(walls):.1f} us")
