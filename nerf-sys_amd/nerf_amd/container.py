@@ -680,6 +680,8 @@ class MetaContainer(nn.Module):
                       else [None] * K)
         if active_module is not None:
             return self.submodules[active_module](x, params=sub_params[active_module])
+        from . import second_order as so
+        so.refuse("a container's expert mix (pass active_module)")
         x = x.contiguous().float()
         N = x.shape[0]
         with torch.no_grad():

@@ -88,22 +88,30 @@ def snapshot_params(model):
 def task_adapt(P, model, support, inner_lr, iterations, active_module: Optional[int] = None):
     """meta_core.py:14-68. Returns (fast OrderedDict, [detached loss per iteration]).
 
-    First order only (P.algo in {"fomaml", "reptile"}).  Like the reference (:30-38) each inner forward runs under
-    autocast(fp16) when P.use_amp (default True) and a GPU is present: vanilla experts then take the fp16 build of
-    their MLP kernels (vanilla.amp_precision); the Instant-NGP kernels stay fp32."""
+    P.algo "fomaml" / "reptile" (first order) run on the HIP kernels.  Like the reference (:30-38) each inner forward
+    then runs under autocast(fp16) when P.use_amp (default True) and a GPU is present: vanilla experts take the fp16
+    build of their MLP kernels (vanilla.amp_precision); the Instant-NGP kernels stay fp32.  Any other algo ("maml")
+    is second order (create_graph=True, no autocast, :28-29): the inner losses run the torch composite of
+    second_order.py and the update is the reference's tensor expression, so the graph reaches the outer backward."""
+    from .second_order import second_order
     algo = str(getattr(P, "algo", "")).lower()
-    if algo not in ("fomaml", "reptile"):
-        raise NotImplementedError(f"task_adapt: algo {algo!r} needs second-order gradients (create_graph=True), "
-                                  "which the HIP kernels do not provide; use 'fomaml' or 'reptile'")
+    first_order = algo in ("fomaml", "reptile")
     base = model.submodules[active_module] if active_module is not None else model
     fast = extract_module_params(base, copy=(algo == "reptile"))
     losses = []
-    amp_enabled = bool(getattr(P, "use_amp", True)) and torch.cuda.is_available()
+    amp_enabled = bool(getattr(P, "use_amp", True)) and torch.cuda.is_available() and first_order
     for _ in range(int(iterations)):
-        with torch.autocast("cuda", dtype=torch.float16, enabled=amp_enabled):
-            loss = compute_loss(P, model, support, params=fast, active_module=active_module)
-        grads = torch.autograd.grad(loss, tuple(fast.values()), create_graph=False, allow_unused=True)
-        fast = sgd_update(fast, grads, inner_lr)
+        if first_order:
+            with torch.autocast("cuda", dtype=torch.float16, enabled=amp_enabled):
+                loss = compute_loss(P, model, support, params=fast, active_module=active_module)
+            grads = torch.autograd.grad(loss, tuple(fast.values()), create_graph=False, allow_unused=True)
+            fast = sgd_update(fast, grads, inner_lr)
+        else:
+            with second_order():
+                loss = compute_loss(P, model, support, params=fast, active_module=active_module)
+                grads = torch.autograd.grad(loss, tuple(fast.values()), create_graph=True, allow_unused=True)
+            fast = OrderedDict((n, w if g is None else (w - inner_lr * g.to(w.dtype)))
+                               for (n, w), g in zip(fast.items(), grads))
         losses.append(loss.detach())
     return fast, losses
 

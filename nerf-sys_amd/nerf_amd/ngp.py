@@ -769,6 +769,8 @@ class InstantNGP(nn.Module):
     def forward(self, x_d: torch.Tensor, params=None) -> torch.Tensor:
         assert x_d.shape[-1] == 6, f"Expected (...,6) [xyz,dir], got {x_d.shape}"
         shp = x_d.shape[:-1]
+        from . import second_order as so
+        so.refuse("the Instant-NGP expert")
         out = _NgpFn.apply(x_d.reshape(-1, 6), self.xyz_encoder.hash_table, self.packed(params), self)
         return out.view(*shp, 4)
 

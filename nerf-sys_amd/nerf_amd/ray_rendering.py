@@ -98,6 +98,9 @@ def volume_render(rgb_sigma: Tensor, t_vals: Tensor, bg_rgb: Optional[Tensor] = 
         rgb_sigma = torch.cat([rgb, sig], -1)
     if bg_rgb is not None:
         bg_rgb = bg_rgb.to(rgb_sigma.device, dtype=torch.float32)
+    from . import second_order as so
+    if so.active():  # create_graph=True inner loop (second_order.py)
+        return so.volume_render(rgb_sigma.float(), t_vals.detach().float(), bg_rgb, float(sigma_scale))
     return VolumeRenderFn.apply(rgb_sigma, t_vals.detach(), bg_rgb, float(sigma_scale))
 
 

@@ -9,7 +9,7 @@ fast-weights surface (models/metamodule/metamodule.py:20-69): parameter names, `
 Gradients flow by PyTorch autograd to whatever tensors were used (module parameters or explicit
 fast-weight tensors), through ``VanillaMLPFn`` whose weights are explicit inputs (packed once per call
 into the kernel layout by differentiable torch indexing).  Double backward (MAML second order,
-pipelines/offline_stage/meta_core.py:57) is not supported and raises.
+pipelines/offline_stage/meta_core.py:57) runs the torch composite of second_order.py inside ``second_order()``.
 """
 from __future__ import annotations
 
@@ -236,6 +236,9 @@ class VanillaNeRF(nn.Module):
     def forward(self, x_d: torch.Tensor, params=None) -> torch.Tensor:
         assert x_d.shape[-1] == 6, f"Expected (...,6) [xyz,dir], got {tuple(x_d.shape)}"
         shp = x_d.shape[:-1]
+        from . import second_order as so
+        if so.active():  # create_graph=True inner loop: the differentiable torch composite (second_order.py)
+            return so.vanilla_forward(self, x_d.reshape(-1, 6), params).view(*shp, 4)
         out = mlp_forward(x_d.reshape(-1, 6), self.packed(params))
         return out.view(*shp, 4)
 

@@ -204,6 +204,58 @@ def test_task_adapt_golden(algo):
         assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in net.parameters())
 
 
+@pytest.mark.parametrize("algo", ["maml", "fomaml"])
+def test_maml_second_order_golden(algo):
+    """meta_core.py:14-68 with algo="maml" (create_graph=True: the inner losses run second_order.py's torch composite
+    on the GPU) and "fomaml", 2 inner steps on 32 support rays, then the query loss with the adapted fast weights
+    (HIP path) and its backward to the module parameters — against the imported reference's fixture (maml.npz).
+    The second-order terms move the outer gradient by up to 1.3e-3 (fixture: maml vs fomaml); the tolerance is
+    2e-5 of each tensor's gradient scale, and the maml gradient must sit closer to the maml fixture than to the
+    fomaml one."""
+    from nerf_amd.losses import compute_mse_loss
+    from nerf_amd.meta import task_adapt
+    z = load("maml")
+    model, net = _meta_model()
+    P = types.SimpleNamespace(algo=algo, fim=False, use_amp=False, ray_samples=32, chunk_points=1 << 20,
+                              color_space="linear")
+    fast, losses = task_adapt(P, model, {"rays": z["rays_s"].to(DEV), "rgbs": z["gt_s"].to(DEV)}, 0.05, 2,
+                              active_module=0)
+    torch.testing.assert_close(torch.stack(losses).cpu(), z[f"{algo}/losses"], rtol=1e-4, atol=1e-7)
+    q = compute_mse_loss(P, model, {"rays": z["rays_q"].to(DEV), "rgbs": z["gt_q"].to(DEV)}, params=fast,
+                         active_module=0)
+    torch.testing.assert_close(q.detach().cpu(), z[f"{algo}/query"], rtol=1e-4, atol=1e-7)
+    q.backward()
+    grads = dict(net.named_parameters())
+    other = "fomaml" if algo == "maml" else "maml"
+    for key in [k for k in z if k.startswith(f"{algo}/grad/")]:
+        n = key.split("/", 2)[2]
+        gv, ref, alt = grads[n].grad.detach().cpu(), z[key], z[f"{other}/grad/{n}"]
+        scale = max(ref.abs().max().item(), 1e-12)
+        err = (gv - ref).abs().max().item()
+        assert err <= 2e-5 * scale, (n, err, scale)
+        sep = (alt - ref).abs().max().item()
+        if sep > 1e-3 * scale:   # the two algorithms' outer gradients differ here: ours must match its own
+            assert err < 0.1 * sep, (n, err, sep)
+    if algo == "maml":
+        for key in [k for k in z if k.startswith("maml/fast/")]:
+            n = key.split("/", 2)[2]
+            ref = z[key]
+            err = (fast[n].detach().cpu() - ref).abs().max().item()
+            assert err <= 1e-5 * max(1.0, ref.abs().max().item()), (n, err)
+
+
+def test_second_order_refuses_uncovered_paths():
+    """Inside second_order() the expert kernels whose backward lies on the loss -> fast-weight path and that have no
+    torch composite raise instead of returning a silently first-order inner gradient."""
+    from nerf_amd.second_order import second_order
+    from nerf_amd.ngp import InstantNGP
+    ngp = InstantNGP().to(DEV)
+    x = torch.rand(16, 6, device=DEV)
+    with second_order():
+        with pytest.raises(NotImplementedError):
+            ngp(x)
+
+
 def test_reptile_update_golden():
     """meta_core.py:145-176 incl. the NaN-delta and zero-delta guards — bit-exact."""
     from nerf_amd.meta import reptile_meta_update

@@ -122,8 +122,40 @@ def test_drz_layout_discovery(tmp_path):
     assert isinstance(va[0], ImageMetadata)
 
 
-def test_task_adapt_refuses_second_order():
-    from types import SimpleNamespace
-    from nerf_amd.meta import task_adapt
-    with pytest.raises(NotImplementedError):
-        task_adapt(SimpleNamespace(algo="maml"), None, None, 0.1, 1)
+def test_second_order_context():
+    """second_order() (MAML create_graph=True, nerf_amd/second_order.py): active only inside the context with grad
+    mode on; refuse() raises there and is a no-op outside."""
+    from nerf_amd import second_order as so
+    assert not so.active()
+    so.refuse("x")
+    with so.second_order():
+        assert so.active()
+        with torch.no_grad():
+            assert not so.active()
+            so.refuse("x")
+        with pytest.raises(NotImplementedError):
+            so.refuse("the Instant-NGP expert")
+        with so.second_order():
+            assert so.active()
+        assert so.active()
+    assert not so.active()
+
+
+def test_second_order_volume_render_matches_oracle():
+    """The torch composite of volume_render (second_order.py) equals the oracle's restatement on CPU tensors, and its
+    gradient is itself differentiable (create_graph=True) — the property second-order MAML needs."""
+    from nerf_amd import second_order as so
+    from oracle import nerf_oracle as O
+    g = torch.Generator().manual_seed(3)
+    rs = torch.rand(5, 16, 4, generator=g, dtype=torch.float64)
+    rs[..., 3] = torch.exp(torch.randn(5, 16, generator=g, dtype=torch.float64))
+    t = torch.sort(torch.rand(5, 16, generator=g, dtype=torch.float64) * 4 + 2, dim=1).values
+    bg = torch.rand(5, 3, generator=g, dtype=torch.float64)
+    ours = so.volume_render(rs, t, bg)
+    ref = O.volume_render(rs, t, bg)
+    for a, b in zip(ours, ref):
+        torch.testing.assert_close(a, b, rtol=1e-12, atol=1e-12)
+    x = rs.clone().requires_grad_(True)
+    gx, = torch.autograd.grad(so.volume_render(x, t, bg)[0].square().sum(), x, create_graph=True)
+    hx, = torch.autograd.grad(gx.square().sum(), x)
+    assert torch.isfinite(hx).all() and hx.abs().sum() > 0

@@ -13,7 +13,7 @@ MetaNeRF's (x,d,params)->dict forward is wrapped in a 6-line adapter to the cont
 contract expert(x_d (M,6), params) -> (M,4) (SURVEY.md §0 defect 2).
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--only-ngp | --only-moe | --only-data | --only-meta |
-        --only-amp]
+        --only-amp | --only-maml]
 """
 import math
 import os
@@ -443,6 +443,69 @@ def gen_meta():
     np.savez_compressed(os.path.join(OUT, "meta.npz"), **arr)
 
 
+def gen_maml():
+    """Second-order MAML (pipelines/offline_stage/meta_core.py:14-68 with algo="maml": create_graph=True, no
+    autocast) of MetaNeRF(frequency) with the mlp.npz weights: 2 inner steps on 32 support rays, then the query loss
+    on 32 other rays with the adapted fast weights and its backward to the MODULE parameters (meta_core.py:119-142
+    fp32 branch, without the clip / step) — those gradients carry the second-order terms.  Also the same outer
+    gradient with the inner gradient detached (first order), so a test can tell the two apart."""
+    from models.inr.meta_vanilla import MetaNeRF                      # noqa: E402
+    from nerfs.losses import compute_loss                              # noqa: E402
+    from pipelines.offline_stage.meta_core import task_adapt          # noqa: E402
+    z = np.load(os.path.join(OUT, "mlp.npz"))
+    zr = np.load(os.path.join(OUT, "rays.npz"))
+    torch.set_num_threads(8)
+
+    class Expert(torch.nn.Module):  # as gen_meta
+        def __init__(self, n):
+            super().__init__(); self.net = n
+
+        def forward(self, x_d, params=None):
+            o = self.net(x_d[:, :3], x_d[:, 3:6], params=params)
+            return torch.cat([o["rgb"], o["sigma"]], -1)
+
+        def meta_named_parameters(self):
+            return self.net.meta_named_parameters()
+
+    class Model(torch.nn.Module):
+        def __init__(self, e):
+            super().__init__(); self.submodules = torch.nn.ModuleList([e]); self.use_occ = False
+
+        def meta_named_parameters(self):
+            return self.submodules[0].meta_named_parameters()
+
+    g = torch.Generator().manual_seed(777)
+    perm = torch.randperm(10000, generator=g)
+    rays_s = torch.from_numpy(zr["rays_const"])[perm[:32]].contiguous()
+    rays_q = torch.from_numpy(zr["rays_const"])[perm[32:64]].contiguous()
+    gt_s, gt_q = torch.rand(32, 3, generator=g), torch.rand(32, 3, generator=g)
+    arr = {"rays_s": rays_s.numpy(), "rays_q": rays_q.numpy(), "gt_s": gt_s.numpy(), "gt_q": gt_q.numpy()}
+    keep = ("trunk.0.linear.weight", "trunk.4.linear.weight", "trunk.7.linear.bias", "sigma_head.weight",
+            "geo_head.weight", "color_mlp.layer0.linear.weight", "color_mlp.color_out.bias")
+    for algo in ("maml", "fomaml"):
+        net = MetaNeRF(encoding_dir="frequency")
+        with torch.no_grad():
+            for n, p in net.meta_named_parameters():
+                p.copy_(torch.from_numpy(z[f"w/{n}"]))
+        model = Model(Expert(net)).eval()
+        P = SimpleNamespace(algo=algo, fim=False, use_amp=False, ray_samples=32, chunk_points=1 << 20,
+                            color_space="linear")
+        fast, losses = task_adapt(P, model, {"rays": rays_s, "rgbs": gt_s}, inner_lr=0.05, iterations=2,
+                                  active_module=0)
+        q = compute_loss(P, model, {"rays": rays_q, "rgbs": gt_q}, params=fast, active_module=0)
+        q.backward()
+        grads = dict(net.meta_named_parameters())
+        arr[f"{algo}/losses"] = torch.stack(losses).numpy()
+        arr[f"{algo}/query"] = np.float32(q.item())
+        for n in keep:
+            arr[f"{algo}/grad/{n}"] = grads[n].grad.numpy()
+            if algo == "maml":
+                arr[f"{algo}/fast/{n}"] = fast[n].detach().numpy()
+    np.savez_compressed(os.path.join(OUT, "maml.npz"), **arr)
+    d = max(float(np.abs(arr[f"maml/grad/{n}"] - arr[f"fomaml/grad/{n}"]).max()) for n in keep)
+    print("maml: query", arr["maml/query"], "max |grad maml - fomaml|", d)
+
+
 def gen_amp():
     """The reference's AMP numerics (configs/train.json "use_amp": true; pipelines/online_stage/runtime_adapt.py:290-310:
     autocast(float16) around compute_mse_loss, scaler.scale(loss).backward() outside it).  Run on the CPU autocast,
@@ -530,6 +593,11 @@ if __name__ == "__main__":
         sys.path.insert(0, REF)
         torch.set_num_threads(8)
         gen_amp()
+    elif "--only-maml" in sys.argv:
+        sys.dont_write_bytecode = True
+        _install_stubs()
+        sys.path.insert(0, REF)
+        gen_maml()
     elif "--only-meta" in sys.argv:
         sys.dont_write_bytecode = True
         _install_stubs()
