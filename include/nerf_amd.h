@@ -48,6 +48,12 @@ int nerf_rays_gen(const float* c2w, int n_poses, const int32_t* pix, int64_t n, 
 int nerf_pick_pixels(int64_t n, int n_images, int H, int W, uint64_t seed, int32_t* pix_out,
                      hipStream_t stream);
 
+/* nerf_pick_pixels with the seed seed_base + (*step_dev) * seed_mul read on the device (*step_dev: int64 step
+ * counter in HBM), so a captured hipGraph draws a new batch per replay (tools/bench_container.py --graph; the
+ * reference draws each batch from its host RNG, runtime_adapt.py:286-296). */
+int nerf_pick_pixels_dseed(int64_t n, int n_images, int H, int W, uint64_t seed_base, uint64_t seed_mul,
+                           const int64_t* step_dev, int32_t* pix_out, hipStream_t stream);
+
 /* clamp_rays_near_far (nerfs/ray_sampling.py:139-176), in place; valid_out (n) bytes or NULL.
  * has_near/has_far select the overrides. */
 int nerf_clamp_near_far(float* rays, int64_t n, int has_near, float near_v, int has_far, float far_v,
@@ -219,6 +225,12 @@ int nerf_grad_sqnorm(const float* g, int64_t n, float* partials, hipStream_t str
 int nerf_adam(float* p, const float* g, float* m, float* v, int64_t n, const int64_t* seg_off_host,
               const double* seg_lr_host, int n_seg, double beta1, double beta2, float eps, float weight_decay,
               int step, const float* partials, float max_norm, hipStream_t stream);
+
+/* nerf_adam with the step count read from device memory (*step_dev >= 1; the bias corrections are formed in the
+ * kernel in double, as nerf_adam forms them on the host): the optimiser node of a captured train-step hipGraph. */
+int nerf_adam_dstep(float* p, const float* g, float* m, float* v, int64_t n, const int64_t* seg_off_host,
+                    const double* seg_lr_host, int n_seg, double beta1, double beta2, float eps, float weight_decay,
+                    const int64_t* step_dev, const float* partials, float max_norm, hipStream_t stream);
 
 /* ------------------------------------------------------------------ Instant-NGP expert */
 
@@ -423,6 +435,15 @@ int nerf_occ_march_multi_staged(const NerfOccGrid* grids, const uint8_t* const* 
                                 float far_plane, float cone_angle, int stratified, uint64_t seed, int max_steps,
                                 int32_t* counts, float* stage, int cap, const int32_t* offsets, int32_t* ray_idx,
                                 float* t0, float* t1, hipStream_t stream);
+
+/* nerf_occ_march_multi_staged with the jitter seed seed + (*step_dev) * seed_mul read on the device (captured
+ * train-step graphs: one marching jitter stream per replay). */
+int nerf_occ_march_multi_staged_dseed(const NerfOccGrid* grids, const uint8_t* const* binaries, const float* boxes,
+                                      const float* steps, int K, const float* rays, int64_t N, float near_plane,
+                                      float far_plane, float cone_angle, int stratified, uint64_t seed, int max_steps,
+                                      int32_t* counts, float* stage, int cap, const int32_t* offsets,
+                                      int32_t* ray_idx, float* t0, float* t1, const int64_t* step_dev,
+                                      uint64_t seed_mul, hipStream_t stream);
 
 /* Exclusive scan of n int32 into out[n+1] (out[n] = total); in / out 16-byte aligned. Reduce-then-scan over
  * 2048-element tiles: 3 launches, 12 B of HBM traffic per element. */

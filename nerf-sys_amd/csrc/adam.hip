@@ -15,7 +15,8 @@ constexpr int NPART = 256;
 
 struct Segs {
   int64_t off[9];
-  float lr[8];
+  float lr[8];      // lr / bc1 of the step (host-counted steps)
+  double lr0[8];    // the groups' base learning rates (device-counted steps: lr / bc1 formed in the kernel)
   int n;
 };
 
@@ -102,12 +103,20 @@ __device__ __forceinline__ void adam4(int64_t e0, const Segs& segs, const AdamHy
 }
 
 // VEC: p, g, m, v 16-byte aligned -> float4 streams (28 B/element of HBM traffic; the scalar form ran at 4.7 TB/s
-// over 134 M elements), the n % 4 tail element-wise.
+// over 134 M elements), the n % 4 tail element-wise.  step_dev (graph-captured steps): the step count is read from
+// device memory and the bias corrections are formed here, in double as nerf_adam does on the host.
 template <bool VEC>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n, Segs segs,
-                                                   AdamHyper h, const float* __restrict__ part, float max_norm) {
+                                                   AdamHyper h, const float* __restrict__ part, float max_norm,
+                                                   const int64_t* __restrict__ step_dev, double beta1, double beta2) {
   __shared__ float red[17];
+  if (step_dev) {
+    const double st = (double)step_dev[0];
+    const double bc1 = 1.0 - pow(beta1, st), bc2 = 1.0 - pow(beta2, st);
+    for (int i = 0; i < segs.n; ++i) segs.lr[i] = (float)(segs.lr0[i] / bc1);
+    h.bc2s = (float)sqrt(bc2);
+  }
   const float scale = clip_scale(part, max_norm, red);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i0 = 0;
@@ -152,16 +161,18 @@ extern "C" int nerf_grad_sqnorm(const float* g, int64_t n, float* partials, hipS
   return nerf_launch_status();
 }
 
-extern "C" int nerf_adam(float* p, const float* g, float* m, float* v, int64_t n, const int64_t* seg_off_host,
-                         const double* seg_lr_host, int n_seg, double beta1, double beta2, float eps, float weight_decay,
-                         int step, const float* partials, float max_norm, hipStream_t stream) {
-  NERF_CHECK_ARG(p && g && m && v && n >= 0 && seg_off_host && seg_lr_host && n_seg >= 1 && n_seg <= 8 && step >= 1);
+static int adam_launch(float* p, const float* g, float* m, float* v, int64_t n, const int64_t* seg_off_host,
+                       const double* seg_lr_host, int n_seg, double beta1, double beta2, float eps, float weight_decay,
+                       int step, const int64_t* step_dev, const float* partials, float max_norm, hipStream_t stream) {
+  NERF_CHECK_ARG(p && g && m && v && n >= 0 && seg_off_host && seg_lr_host && n_seg >= 1 && n_seg <= 8 &&
+                 (step >= 1 || step_dev));
   Segs s{};
   s.n = n_seg;
   for (int i = 0; i <= n_seg; ++i) s.off[i] = seg_off_host[i];
-  const double bc1 = 1.0 - std::pow(beta1, (double)step);
-  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  const double bc1 = step_dev ? 1.0 : 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = step_dev ? 1.0 : 1.0 - std::pow(beta2, (double)step);
   for (int i = 0; i < n_seg; ++i) s.lr[i] = (float)(seg_lr_host[i] / bc1);
+  for (int i = 0; i < n_seg; ++i) s.lr0[i] = seg_lr_host[i];
   for (int i = 0; i < n_seg; ++i) NERF_CHECK_ARG(s.off[i] <= s.off[i + 1]);
   NERF_CHECK_ARG(s.off[0] >= 0 && s.off[n_seg] <= n);
   const AdamHyper h{(float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), eps, weight_decay,
@@ -171,9 +182,29 @@ extern "C" int nerf_adam(float* p, const float* g, float* m, float* v, int64_t n
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   if (vec)
-    adam_kernel<true><<<(unsigned)blocks, 256, 0, stream>>>(p, g, m, v, n, s, h, partials, max_norm);
+    adam_kernel<true><<<(unsigned)blocks, 256, 0, stream>>>(p, g, m, v, n, s, h, partials, max_norm, step_dev, beta1,
+                                                             beta2);
   else
-    adam_kernel<false><<<(unsigned)blocks, 256, 0, stream>>>(p, g, m, v, n, s, h, partials, max_norm);
+    adam_kernel<false><<<(unsigned)blocks, 256, 0, stream>>>(p, g, m, v, n, s, h, partials, max_norm, step_dev, beta1,
+                                                              beta2);
   return nerf_launch_status();
+}
+
+extern "C" int nerf_adam(float* p, const float* g, float* m, float* v, int64_t n, const int64_t* seg_off_host,
+                         const double* seg_lr_host, int n_seg, double beta1, double beta2, float eps, float weight_decay,
+                         int step, const float* partials, float max_norm, hipStream_t stream) {
+  return adam_launch(p, g, m, v, n, seg_off_host, seg_lr_host, n_seg, beta1, beta2, eps, weight_decay, step, nullptr,
+                     partials, max_norm, stream);
+}
+
+// nerf_adam with the step count in device memory (*step_dev >= 1, read by the kernel): a captured hipGraph replays
+// it with the count its own increment node advanced (the step closure of nerf_amd/graph_step.py)
+extern "C" int nerf_adam_dstep(float* p, const float* g, float* m, float* v, int64_t n, const int64_t* seg_off_host,
+                               const double* seg_lr_host, int n_seg, double beta1, double beta2, float eps,
+                               float weight_decay, const int64_t* step_dev, const float* partials, float max_norm,
+                               hipStream_t stream) {
+  NERF_CHECK_ARG(step_dev);
+  return adam_launch(p, g, m, v, n, seg_off_host, seg_lr_host, n_seg, beta1, beta2, eps, weight_decay, 0, step_dev,
+                     partials, max_norm, stream);
 }
 

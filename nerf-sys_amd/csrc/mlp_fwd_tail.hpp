@@ -29,7 +29,12 @@
 namespace nerf_mlp {
 
 constexpr int FT_ROWS = 64;
-constexpr int FT_WH = 260, FT_WC0 = 52, FT_WC1 = 132, FT_CIN = 68;  // LDS pitches (floats): conflict-free b128 reads
+// LDS pitches (floats).  A ds_read_b128 of lane (lr = l & 15, g = l >> 4) reads 16-B slot (lr * P / 4 + g) mod 16 of the
+// 64-bank array; its lane groups {0-3,12-15,20-27}, ... mix (lr, g) with (lr - 4 .. lr + 7, g + 1), which are all
+// distinct for P / 4 = 2 (mod 16) (slots 2 lr + g): 264 / 72 / 136.  The round-4 pitches 260 / 52 / 132 (P / 4 odd)
+// put two lanes of every group on one slot: 1.4e7 conflict cycles per fine launch (profiles/r05/pmc_mfma.txt).
+// The CIN staging pitch 68 keeps its scalar writes at most 2-way (free for ds_write_b32).
+constexpr int FT_WH = 264, FT_WC0 = 72, FT_WC1 = 136, FT_CIN = 68;
 
 struct FwdTailArgs {
   const float* Y7;   // [Mp][ldy] trunk.7 output (ldy 256 in training, 320 in the inference ping-pong)

@@ -151,10 +151,12 @@ __global__ void march_multi_kernel(MarchExperts E, const float* __restrict__ ray
                                    float far_plane, float cone, int stratified, uint64_t seed, int max_steps,
                                    int32_t* __restrict__ counts, const int32_t* __restrict__ offsets,
                                    int32_t* __restrict__ ray_idx, float* __restrict__ t0, float* __restrict__ t1,
-                                   float2* __restrict__ stage, int cap, int overflow_only) {
+                                   float2* __restrict__ stage, int cap, int overflow_only,
+                                   const int64_t* __restrict__ step_dev, uint64_t seed_mul) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
   if (r >= N) return;
+  if (step_dev) seed += (uint64_t)step_dev[0] * seed_mul;  // graph-captured steps: the seed stream advances on device
   const int64_t j = (int64_t)k * N + r;
   if (overflow_only && counts[j] <= cap) return;
   const float* ry = rays + r * 8;
@@ -641,16 +643,15 @@ extern "C" int nerf_occ_march_multi(const NerfOccGrid* grids, const uint8_t* con
   }
   march_multi_kernel<<<dim3((unsigned)nerf_cdiv(N, 64), K), 64, 0, st>>>(E, rays, N, near_plane, far_plane, cone_angle,
                                                                          stratified, seed, max_steps, counts, offsets,
-                                                                         ray_idx, t0, t1, nullptr, 0, 0);
+                                                                         ray_idx, t0, t1, nullptr, 0, 0, nullptr, 0);
   return nerf_launch_status();
 }
 
-extern "C" int nerf_occ_march_multi_staged(const NerfOccGrid* grids, const uint8_t* const* binaries,
-                                           const float* boxes, const float* steps, int K, const float* rays, int64_t N,
-                                           float near_plane, float far_plane, float cone_angle, int stratified,
-                                           uint64_t seed, int max_steps, int32_t* counts, float* stage, int cap,
-                                           const int32_t* offsets, int32_t* ray_idx, float* t0, float* t1,
-                                           hipStream_t st) {
+static int march_multi_staged(const NerfOccGrid* grids, const uint8_t* const* binaries, const float* boxes,
+                              const float* steps, int K, const float* rays, int64_t N, float near_plane,
+                              float far_plane, float cone_angle, int stratified, uint64_t seed, int max_steps,
+                              int32_t* counts, float* stage, int cap, const int32_t* offsets, int32_t* ray_idx,
+                              float* t0, float* t1, const int64_t* step_dev, uint64_t seed_mul, hipStream_t st) {
   if (K < 1 || K > MARCH_MAX_EXPERTS || N < 0 || max_steps < 1 || cap < 1 || !grids || !binaries || !boxes || !steps)
     return NERF_E_ARG;
   if (N == 0) return NERF_OK;
@@ -669,14 +670,37 @@ extern "C" int nerf_occ_march_multi_staged(const NerfOccGrid* grids, const uint8
   const dim3 grid((unsigned)nerf_cdiv(N, 64), K);
   if (!offsets) {
     march_multi_kernel<<<grid, 64, 0, st>>>(E, rays, N, near_plane, far_plane, cone_angle, stratified, seed, max_steps,
-                                            counts, nullptr, nullptr, nullptr, nullptr, sg, cap, 0);
+                                            counts, nullptr, nullptr, nullptr, nullptr, sg, cap, 0, step_dev, seed_mul);
   } else {
     const int64_t KN = (int64_t)K * N;
     march_emit_kernel<<<(unsigned)nerf_cdiv(KN, 4), 256, 0, st>>>(sg, cap, counts, offsets, N, KN, ray_idx, t0, t1);
     march_multi_kernel<<<grid, 64, 0, st>>>(E, rays, N, near_plane, far_plane, cone_angle, stratified, seed, max_steps,
-                                            counts, offsets, ray_idx, t0, t1, nullptr, cap, 1);
+                                            counts, offsets, ray_idx, t0, t1, nullptr, cap, 1, step_dev, seed_mul);
   }
   return nerf_launch_status();
+}
+
+extern "C" int nerf_occ_march_multi_staged(const NerfOccGrid* grids, const uint8_t* const* binaries,
+                                           const float* boxes, const float* steps, int K, const float* rays, int64_t N,
+                                           float near_plane, float far_plane, float cone_angle, int stratified,
+                                           uint64_t seed, int max_steps, int32_t* counts, float* stage, int cap,
+                                           const int32_t* offsets, int32_t* ray_idx, float* t0, float* t1,
+                                           hipStream_t st) {
+  return march_multi_staged(grids, binaries, boxes, steps, K, rays, N, near_plane, far_plane, cone_angle, stratified,
+                            seed, max_steps, counts, stage, cap, offsets, ray_idx, t0, t1, nullptr, 0, st);
+}
+
+// the staged march with the jitter seed seed + *step_dev * seed_mul read on the device (graph-captured steps)
+extern "C" int nerf_occ_march_multi_staged_dseed(const NerfOccGrid* grids, const uint8_t* const* binaries,
+                                                 const float* boxes, const float* steps, int K, const float* rays,
+                                                 int64_t N, float near_plane, float far_plane, float cone_angle,
+                                                 int stratified, uint64_t seed, int max_steps, int32_t* counts,
+                                                 float* stage, int cap, const int32_t* offsets, int32_t* ray_idx,
+                                                 float* t0, float* t1, const int64_t* step_dev, uint64_t seed_mul,
+                                                 hipStream_t st) {
+  if (!step_dev) return NERF_E_ARG;
+  return march_multi_staged(grids, binaries, boxes, steps, K, rays, N, near_plane, far_plane, cone_angle, stratified,
+                            seed, max_steps, counts, stage, cap, offsets, ray_idx, t0, t1, step_dev, seed_mul, st);
 }
 
 extern "C" int64_t nerf_scan_workspace_bytes(int64_t n) {

@@ -155,9 +155,12 @@ __global__ void dataset_write_kernel(DatasetArgs A, int64_t n, const int32_t* __
   out_idx[r] = A.image_index[im];
 }
 
-__global__ void pick_pixels_kernel(int64_t n, int n_images, int H, int W, uint64_t seed, int32_t* __restrict__ pix) {
+// step_dev (graph-captured steps): the stream's seed is seed + *step_dev * seed_mul, read from device memory
+__global__ void pick_pixels_kernel(int64_t n, int n_images, int H, int W, uint64_t seed,
+                                   const int64_t* __restrict__ step_dev, uint64_t seed_mul, int32_t* __restrict__ pix) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
+  if (step_dev) seed += (uint64_t)step_dev[0] * seed_mul;
   const uint64_t z = nerf_mix64(seed * 0x9e3779b97f4a7c15ULL + nerf_mix64((uint64_t)p + 0x632be59bd9b4e019ULL));
   const uint64_t tot = (uint64_t)n_images * (uint64_t)H * (uint64_t)W;
   const uint64_t k = (uint64_t)(((unsigned __int128)z * tot) >> 64);  // unbiased-enough multiply-shift
@@ -294,7 +297,15 @@ extern "C" int nerf_pick_pixels(int64_t n, int n_images, int H, int W, uint64_t 
                                 hipStream_t stream) {
   NERF_CHECK_ARG(pix_out && n >= 0 && n_images > 0 && H > 0 && W > 0);
   if (n == 0) return NERF_OK;
-  pick_pixels_kernel<<<blocks_for(n, 256), 256, 0, stream>>>(n, n_images, H, W, seed, pix_out);
+  pick_pixels_kernel<<<blocks_for(n, 256), 256, 0, stream>>>(n, n_images, H, W, seed, nullptr, 0, pix_out);
+  return nerf_launch_status();
+}
+
+extern "C" int nerf_pick_pixels_dseed(int64_t n, int n_images, int H, int W, uint64_t seed_base, uint64_t seed_mul,
+                                      const int64_t* step_dev, int32_t* pix_out, hipStream_t stream) {
+  NERF_CHECK_ARG(pix_out && step_dev && n >= 0 && n_images > 0 && H > 0 && W > 0);
+  if (n == 0) return NERF_OK;
+  pick_pixels_kernel<<<blocks_for(n, 256), 256, 0, stream>>>(n, n_images, H, W, seed_base, step_dev, seed_mul, pix_out);
   return nerf_launch_status();
 }
 

@@ -53,6 +53,10 @@ def lib():
         sig = {
             "nerf_rays_gen": [P, I, P, I64, I, I, F, F, F, F, I, F, F, P, F, F, P, P, P, P],
             "nerf_pick_pixels": [I64, I, I, I, U64, P, P],
+            "nerf_pick_pixels_dseed": [I64, I, I, I, U64, U64, P, P, P],
+            "nerf_adam_dstep": [P, P, P, P, I64, P, P, I, D, D, F, F, P, P, F, P],
+            "nerf_occ_march_multi_staged_dseed": [P, P, P, P, I, P, I64, F, F, F, I, U64, I, P, P, I, P, P, P, P, P,
+                                                  U64, P],
             "nerf_clamp_near_far": [P, I64, I, F, I, F, F, F, P, P],
             "nerf_rays_ndc": [P, I64, I, I, F, F, P, P],
             "nerf_sample_stratified": [P, I64, I, I, P, U64, P, P],
@@ -182,7 +186,7 @@ EXPORTS = ("nerf_rays_gen", "nerf_pick_pixels", "nerf_clamp_near_far", "nerf_ray
            "nerf_occ_sample_cells", "nerf_moe_route_n", "nerf_ngp_fwd_enc_n", "nerf_ngp_density_enc_rng",
            "nerf_ngp_bwd_hash_n", "nerf_moe_dispatch_n", "nerf_gather_rows_rng", "nerf_moe_blend_rng",
            "nerf_moe_blend_finish_n", "nerf_moe_blend_bwd_rng",
-           "nerf_packed_points_n")
+           "nerf_packed_points_n", "nerf_pick_pixels_dseed", "nerf_adam_dstep", "nerf_occ_march_multi_staged_dseed")
 
 
 def check(status: int, what: str) -> None:

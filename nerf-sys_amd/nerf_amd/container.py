@@ -164,6 +164,28 @@ class _BlendFn(torch.autograd.Function):
 MARCH_STAGE_CAP = 512  # staged segments per (expert, ray) pair: K*N*512*8 B (67 MB at 4 x 4096 pairs)
 
 
+def vis_thresholds(model, alpha_thre=None):
+    """Per-expert visibility thresholds min(alpha_thre, mean occupancy) (nerfacc sampling's alpha_thre clamp,
+    ray_rendering.py:397-422) in ONE persistent device tensor, recomputed in place only when a grid or alpha_thre
+    changed (the grids update every 16 steps) — not with 4 reductions and a host->device copy every step.  In place,
+    so a captured train-step graph (graph_step.py) reads the current values after an eager occupancy update."""
+    subs = list(model.submodules)
+    athr = [ex.alpha_thre for ex in subs] if alpha_thre is None else list(alpha_thre)
+    key = (tuple((ex.occ_grid.gen, ex.occ_grid.occs._version, ex.occ_grid.occs.data_ptr()) for ex in subs),
+           tuple(athr))
+    st = model.__dict__.setdefault("_vis_thr_state", {"key": None, "buf": None})
+    if st["key"] != key:
+        dev = subs[0].occ_grid.occs.device
+        occ_mean = torch.stack([ex.occ_grid.occs.mean() for ex in subs]).float()
+        val = torch.minimum(occ_mean, torch.tensor(athr, dtype=torch.float32, device=dev))
+        if st["buf"] is None or st["buf"].shape != val.shape:
+            st["buf"] = val.contiguous()
+        else:
+            st["buf"].copy_(val)
+        st["key"] = key
+    return st["buf"]
+
+
 def _march_experts(model, rays, sub_params, render_step_size, alpha_thre, cone_angle, before_sync=None):
     """Every expert's occupancy marching (MetaNGP.occupancy_marching, meta_ngp.py:384-443, on the rays that hit its
     box, ray_rendering.py:397-422) in ONE launch pair: count -> scan -> ONE host read of the K+1 expert boundaries
@@ -225,15 +247,7 @@ def _march_experts(model, rays, sub_params, render_step_size, alpha_thre, cone_a
                     sig[a:b] = ex.density(xd[a:b, :3], params=sub_params[k]).view(-1)
             # per-expert thresholds min(alpha_thre, mean occupancy): recomputed only when a grid or alpha_thre
             # changed (the grids update every 16 steps), not with 4 reductions and a host->device copy every step
-            key = (tuple((ex.occ_grid.gen, ex.occ_grid.occs._version, ex.occ_grid.occs.data_ptr()) for ex in subs),
-                   tuple(athr))
-            cache = model.__dict__.setdefault("_vis_thr", {})
-            thr = cache.get(key)
-            if thr is None:
-                occ_mean = torch.stack([ex.occ_grid.occs.mean() for ex in subs]).float()
-                thr = torch.minimum(occ_mean, torch.tensor(athr, dtype=torch.float32, device=dev)).contiguous()
-                cache.clear()
-                cache[key] = thr
+            thr = vis_thresholds(model, athr)
             keep = torch.empty(M, dtype=torch.int32, device=dev)
             check(L.nerf_packed_visibility_groups(ptr(t0), ptr(t1), ptr(sig), ptr(offs), K * N, N, 1e-4,
                                                   float(max(athr)), ptr(thr), ptr(keep), stream()),
@@ -275,11 +289,30 @@ class _DevSizes:
         self.pending = []          # (event, pinned int32 march total, capacity it ran with)
         self.overflows = 0
         self.calls = 0
+        # frozen (a captured train-step graph, graph_step.py): the capacity no longer moves and no host copy / event
+        # is issued; the largest march total is kept on the device (max_dev) and read after the replays
+        self.frozen = False
+        self.max_dev = None
+
+    def freeze(self, cap=None, device=None):
+        """Fix the capacity (default: the current one) for graph capture."""
+        self.poll()
+        if cap is not None:
+            self.cap = max(int(cap), self.cap)
+        self.frozen = True
+        self.max_dev = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def frozen_report(self):
+        """(largest march total seen by the frozen steps, whether it exceeded the capacity) — one host read."""
+        mx = int(self.max_dev.item()) if self.max_dev is not None else 0
+        return mx, mx > self.cap
 
     def _cap_for(self, total):
         return max(self.min_cap, 1 << (max(1, 2 * int(total)) - 1).bit_length())
 
     def poll(self):
+        if self.frozen:
+            return self.cap
         keep = []
         for ev, host, cap in self.pending:
             if ev.query():
@@ -294,6 +327,10 @@ class _DevSizes:
         return self.cap
 
     def record(self, total_dev, cap):
+        if self.frozen:
+            torch.maximum(self.max_dev, total_dev.view(1), out=self.max_dev)
+            self.calls += 1
+            return
         host = torch.empty(1, dtype=torch.int32, pin_memory=True)
         host.copy_(total_dev.view(1), non_blocking=True)
         ev = torch.cuda.Event()
@@ -407,14 +444,22 @@ def _march_experts_dev(model, rays, sub_params, render_step_size, alpha_thre, co
     steps = (ctypes.c_float * K)(*[float(ex.render_step_size if render_step_size is None else render_step_size)
                                    for ex in subs])
     training = bool(ex0.training)
-    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
     L = lib()
+    # model.step_seed = (int64 device step counter, base, mul): the jitter seed base + step * mul is read on the
+    # device (a captured train-step graph replays with the counter it advances); else one host draw per call
+    ss = getattr(model, "step_seed", None)
+    seed = int(ss[1]) if ss is not None else int(torch.randint(0, 2 ** 62, (1,)).item())
     counts = torch.empty(K * N, dtype=torch.int32, device=dev)
     args = (grids, bins, boxes, steps, K, ptr(rays), N, float(ex0.near_plane), float(ex0.far_plane), float(cone[0]),
             int(training), ctypes.c_uint64(seed), 8192)
     stage = torch.empty(K * N * MARCH_STAGE_CAP * 2, dtype=torch.float32, device=dev)
-    check(L.nerf_occ_march_multi_staged(*args, ptr(counts), ptr(stage), MARCH_STAGE_CAP, None, None, None, None,
-                                        stream()), "nerf_occ_march_multi_staged(count)")
+
+    def march(*rest):
+        if ss is None:
+            return L.nerf_occ_march_multi_staged(*args, *rest, stream())
+        return L.nerf_occ_march_multi_staged_dseed(*args, *rest, ptr(ss[0]), ctypes.c_uint64(int(ss[2])), stream())
+
+    check(march(ptr(counts), ptr(stage), MARCH_STAGE_CAP, None, None, None, None), "nerf_occ_march_multi_staged(count)")
     offs = exclusive_scan(counts)
     cap = sizes.poll()
     sizes.record(offs[K * N:], cap)
@@ -422,8 +467,8 @@ def _march_experts_dev(model, rays, sub_params, render_step_size, alpha_thre, co
     ri = torch.empty(cap, dtype=torch.int32, device=dev)
     t0 = torch.empty(cap, dtype=torch.float32, device=dev)
     t1 = torch.empty(cap, dtype=torch.float32, device=dev)
-    check(L.nerf_occ_march_multi_staged(*args, ptr(counts), ptr(stage), MARCH_STAGE_CAP, ptr(offs), ptr(ri), ptr(t0),
-                                        ptr(t1), stream()), "nerf_occ_march_multi_staged(emit)")
+    check(march(ptr(counts), ptr(stage), MARCH_STAGE_CAP, ptr(offs), ptr(ri), ptr(t0), ptr(t1)),
+          "nerf_occ_march_multi_staged(emit)")
     del stage
     athr = [ex.alpha_thre if alpha_thre is None else alpha_thre for ex in subs]
     if training:
@@ -443,15 +488,7 @@ def _march_experts_dev(model, rays, sub_params, render_step_size, alpha_thre, co
                                                  ptr(bounds[k:k + 2]), ab, float(ex._eps), ptr(sig), stream()),
                       "nerf_ngp_density_enc_rng")
                 TIMING.stop(h)
-            key = (tuple((ex.occ_grid.gen, ex.occ_grid.occs._version, ex.occ_grid.occs.data_ptr()) for ex in subs),
-                   tuple(athr))
-            cache = model.__dict__.setdefault("_vis_thr", {})
-            thr = cache.get(key)
-            if thr is None:
-                occ_mean = torch.stack([ex.occ_grid.occs.mean() for ex in subs]).float()
-                thr = torch.minimum(occ_mean, torch.tensor(athr, dtype=torch.float32, device=dev)).contiguous()
-                cache.clear()
-                cache[key] = thr
+            thr = vis_thresholds(model, athr)
             keep = torch.zeros(cap, dtype=torch.int32, device=dev)
             check(L.nerf_packed_visibility_groups(ptr(t0), ptr(t1), ptr(sig), ptr(offs), K * N, N, 1e-4,
                                                   float(max(athr)), ptr(thr), ptr(keep), stream()),

@@ -45,8 +45,16 @@ def rays_gen(c2w, H, W, fx, fy, cx, cy, *, pix=None, near=None, far=None, aabb=N
     return (rays, rgb) if images_u8 is not None else rays
 
 
-def pick_pixels(n, n_images, H, W, seed, device):
+def pick_pixels(n, n_images, H, W, seed, device, step_dev=None, seed_mul=0):
+    """n random (image, row, col) triples of the counter RNG stream ``seed``; with ``step_dev`` (int64 device
+    counter) the stream is seed + step_dev * seed_mul, read by the kernel (captured train-step graphs)."""
     pix = torch.empty((n, 3), dtype=torch.int32, device=device)
+    if step_dev is not None:
+        need(step_dev, "step_dev", torch.int64)
+        check(lib().nerf_pick_pixels_dseed(n, n_images, H, W, ctypes.c_uint64(seed & (2**64 - 1)),
+                                           ctypes.c_uint64(seed_mul & (2**64 - 1)), ptr(step_dev), ptr(pix),
+                                           stream()), "nerf_pick_pixels_dseed")
+        return pix
     check(lib().nerf_pick_pixels(n, n_images, H, W, ctypes.c_uint64(seed & (2**64 - 1)), ptr(pix), stream()),
           "nerf_pick_pixels")
     return pix
@@ -269,8 +277,15 @@ def grad_sqnorm(g, partials=None):
 
 def adam(p, g, m, v, seg_off: Sequence[int], seg_lr: Sequence[float], step, betas=(0.9, 0.999), eps=1e-8,
          weight_decay=0.0, partials=None, max_norm=0.0):
+    """nerf_adam; ``step`` an int, or an int64 device tensor holding the step count (nerf_adam_dstep)."""
     off = (ctypes.c_int64 * len(seg_off))(*seg_off)
     lr = (ctypes.c_double * len(seg_lr))(*seg_lr)
+    if isinstance(step, torch.Tensor):
+        need(step, "step", torch.int64)
+        check(lib().nerf_adam_dstep(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), off, lr, len(seg_lr), betas[0],
+                                    betas[1], eps, weight_decay, ptr(step), ptr(partials), max_norm, stream()),
+              "nerf_adam_dstep")
+        return
     check(lib().nerf_adam(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), off, lr, len(seg_lr), betas[0], betas[1], eps,
                           weight_decay, step, ptr(partials), max_norm, stream()), "nerf_adam")
 

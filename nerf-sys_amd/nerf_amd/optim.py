@@ -81,6 +81,9 @@ class FlatAdam:
         self.params = params
         self.betas, self.eps, self.wd, self.grad_clip = betas, eps, weight_decay, grad_clip
         self.step_count = 0
+        # device_step(): the step count also lives in HBM and the step reads it there (nerf_adam_dstep), so a captured
+        # hipGraph of the train step advances it per replay (graph_step.py)
+        self.step_dev = None
         # Bucketed exchange (replicated update, world_size > 1): a parameter whose gradient a HIP backward writes in
         # place (the Instant-NGP hash tables, 0.54 GB for four experts) is its own bucket.  The backward calls
         # _bucket_ready when it has enqueued its write; the all-reduces are ISSUED in one fixed bucket order on every
@@ -193,8 +196,18 @@ class FlatAdam:
         else:
             dist.all_gather_into_tensor(self.flat, pshard)  # in place: pshard is this rank's slice of flat
 
+    def device_step(self):
+        """Keep the step count in device memory from now on (graph capture of the train step; world_size 1)."""
+        if self.world_size > 1:
+            raise ValueError("device-counted steps are for single-rank graph capture")
+        if self.step_dev is None:
+            self.step_dev = torch.full((1,), self.step_count, dtype=torch.int64, device=self.flat.device)
+        return self.step_dev
+
     def step(self):
         self.step_count += 1
+        if self.step_dev is not None:
+            self.step_dev.add_(1)
         if self.shard:
             self._step_sharded()
             return
@@ -204,5 +217,5 @@ class FlatAdam:
             parts, mx = self.partials, float(self.grad_clip)
         else:
             parts, mx = None, 0.0
-        K.adam(self.flat, self.grad, self.m, self.v, self.seg_off, self.seg_lr, self.step_count, self.betas, self.eps,
-               self.wd, parts, mx)
+        K.adam(self.flat, self.grad, self.m, self.v, self.seg_off, self.seg_lr,
+               self.step_count if self.step_dev is None else self.step_dev, self.betas, self.eps, self.wd, parts, mx)

@@ -39,12 +39,14 @@ class RayBatcher:
         self.images = scene.images.to(device).contiguous()
         self.device = device
 
-    def batch(self, n, seed, shard=None):
+    def batch(self, n, seed, shard=None, step_dev=None, seed_mul=0):
         """n random pixels from the counter RNG stream ``seed``.  ``shard=(rank, world)`` keeps the rank-strided
         slice pix[rank::world] of that draw (an/scripts/create_clusters.py:799), so every world size sees
-        the same global batch (strong scaling)."""
+        the same global batch (strong scaling).  ``step_dev`` (int64 device counter): the stream is
+        seed + step_dev * seed_mul, read on the device (captured train-step graphs, graph_step.py)."""
         s = self.scene
-        pix = K.pick_pixels(n, self.poses.shape[0], s.H, s.W, seed, self.device)
+        pix = K.pick_pixels(n, self.poses.shape[0], s.H, s.W, seed, self.device, step_dev=step_dev,
+                            seed_mul=seed_mul)
         if shard is not None and shard[1] > 1:
             pix = pix[shard[0]::shard[1]].contiguous()
         fx, fy, cx, cy = s.intrinsics

@@ -59,6 +59,11 @@ def parse():
     ap.add_argument("--host-sized", action="store_true",
                     help="the host-sized render (two host reads of the packed sizes per step) instead of the "
                          "device-sized sync-free one (container.py, DESIGN.md §3.8)")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=None,
+                    help="replay the train step as ONE captured hipGraph (nerf_amd/graph_step.py; world size 1, "
+                         "device-sized render); the default at world size 1")
+    ap.add_argument("--no-graph", dest="graph", action="store_false",
+                    help="launch every kernel of the step from Python (eager)")
     ap.add_argument("--no-bucket", action="store_true",
                     help="one all-reduce of the flat gradient in step() instead of per-table buckets started by the "
                          "hash-table backward")
@@ -146,6 +151,7 @@ def build_step(a, dev, rank=0, world=1):
     opt = FlatAdam(groups, grad_clip=1.0, world_size=world, shard=a.shard, bucket_tables=not a.no_bucket)
     rb = RayBatcher(scene, dev)
     P = SimpleNamespace(ray_samples=96, chunk_points=262_144 * 17, color_space="linear")
+    graph = use_graph(a, world)
 
     def one(step):
         model.maybe_update_expert_occupancies(step)
@@ -156,8 +162,53 @@ def build_step(a, dev, rank=0, world=1):
         opt.step()
         return loss
 
-    one.opt = opt
-    return one, model
+    one.opt, one.graphed, one.eager = opt, None, one
+    if not graph:
+        return one, model
+    # graph mode (world 1): every step reads its seeds and its Adam step count from HBM, so eager steps and graph
+    # replays run the same kernels; from capture_at on, the step is GraphedStep (warm-up, capture, replays)
+    from nerf_amd.container import vis_thresholds
+    from nerf_amd.graph_step import GraphedStep
+    ctr = torch.zeros(1, dtype=torch.int64, device=dev)      # = the step index (batch seed = step * world + rank)
+    model.step_seed = (ctr, 0x5EED0CC, 0x9E3779B97F4A7C15)     # marching jitter: its own counter stream
+    opt.device_step()
+
+    def body():
+        rays, gt = rb.batch(a.batch, seed=rank, step_dev=ctr, seed_mul=world)
+        opt.zero_grad()
+        loss = compute_mse_loss(P, model, {"rays": rays, "rgbs": gt})
+        loss.backward()
+        opt.step()
+        return loss
+
+    def pre(step):
+        ctr.fill_(step)
+        model.maybe_update_expert_occupancies(step)
+        if "_dev_sizes" in model.__dict__:
+            vis_thresholds(model)   # in place: the captured visibility kernel reads the refreshed values
+
+    def eager(step):
+        pre(step)
+        return body()
+
+    gs = GraphedStep(body, pre, warmup=2,
+                     before_capture=lambda: model.__dict__["_dev_sizes"].freeze(device=dev))
+    capture_at = max(a.warmup - 3, model.submodules[0].occ_warmup_steps + 2)
+
+    def one_g(step):
+        return gs(step) if step >= capture_at else eager(step)
+
+    one_g.opt, one_g.graphed, one_g.eager, one_g.body, one_g.ctr = opt, gs, eager, body, ctr
+    return one_g, model
+
+
+def use_graph(a, world):
+    g = getattr(a, "graph", None)
+    if g is None:
+        g = False
+    if g and (world > 1 or getattr(a, "host_sized", False)):
+        raise ValueError("--graph: single rank, device-sized render only")
+    return bool(g)
 
 
 def run(a, dev, rank=0, world=1):
@@ -206,8 +257,8 @@ def run(a, dev, rank=0, world=1):
                 "note": "events on the compute stream around FlatAdam's wait for the table buckets (started by each "
                         "expert's hash backward) plus the all-reduce of the remaining ranges; mean over the steps"}
     G.TIMING.enabled = True
-    for s in range(a.steps):
-        one(a.warmup + a.steps + s)
+    for s in range(a.steps):   # (graph mode: the same step launched eagerly — a replay records no events)
+        one.eager(a.warmup + a.steps + s)
     per = G.TIMING.collect()
     G.TIMING.enabled = False
     ms = {k: sum(t for t, _ in v) / a.steps for k, v in per.items()}          # per step (all experts)
@@ -252,6 +303,15 @@ def run(a, dev, rank=0, world=1):
     if exch:
         out["exchange"] = exch
     sz = model.__dict__.get("_dev_sizes")
+    if one.graphed is not None:
+        mx, over = sz.frozen_report()
+        out["graph"] = {"captured": one.graphed.graph is not None, "replays": one.graphed.calls - one.graphed.warmup,
+                        "capacity": sz.cap, "max_march_samples_frozen": mx, "overflow": over,
+                        "note": "timed steps are replays of ONE hipGraph of the whole train step (nerf_amd/"
+                                "graph_step.py): seeds and the Adam step count read from HBM, occupancy updates "
+                                "eager between replays; kernels_ms_per_step from eager launches of the same step"}
+    else:
+        out["graph"] = None
     if model.device_sized and sz is not None:
         torch.cuda.synchronize()
         sz.poll()
