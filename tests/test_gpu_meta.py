@@ -209,9 +209,10 @@ def test_maml_second_order_golden(algo):
     """meta_core.py:14-68 with algo="maml" (create_graph=True: the inner losses run second_order.py's torch composite
     on the GPU) and "fomaml", 2 inner steps on 32 support rays, then the query loss with the adapted fast weights
     (HIP path) and its backward to the module parameters — against the imported reference's fixture (maml.npz).
-    The second-order terms move the outer gradient by up to 1.3e-3 (fixture: maml vs fomaml); the tolerance is
-    2e-5 of each tensor's gradient scale, and the maml gradient must sit closer to the maml fixture than to the
-    fomaml one."""
+    The second-order terms move each outer gradient tensor by 3.5-7 % of its norm (fixture: maml vs fomaml); the
+    tolerance is a relative error norm of 2e-3 per tensor (the trunk.0 gradient is ~5e-7 in scale: the GPU's and the
+    CPU's fp32 GEMM orders differ there at ~1e-3 of it), and the error must stay under 5 % of the maml - fomaml
+    separation, so the two algorithms are told apart."""
     from nerf_amd.losses import compute_mse_loss
     from nerf_amd.meta import task_adapt
     z = load("maml")
@@ -230,12 +231,9 @@ def test_maml_second_order_golden(algo):
     for key in [k for k in z if k.startswith(f"{algo}/grad/")]:
         n = key.split("/", 2)[2]
         gv, ref, alt = grads[n].grad.detach().cpu(), z[key], z[f"{other}/grad/{n}"]
-        scale = max(ref.abs().max().item(), 1e-12)
-        err = (gv - ref).abs().max().item()
-        assert err <= 2e-5 * scale, (n, err, scale)
-        sep = (alt - ref).abs().max().item()
-        if sep > 1e-3 * scale:   # the two algorithms' outer gradients differ here: ours must match its own
-            assert err < 0.1 * sep, (n, err, sep)
+        err = (gv - ref).norm().item()
+        assert err <= 2e-3 * ref.norm().item(), (n, err, ref.norm().item())
+        assert err <= 0.05 * (alt - ref).norm().item(), (n, err, (alt - ref).norm().item())
     if algo == "maml":
         for key in [k for k in z if k.startswith("maml/fast/")]:
             n = key.split("/", 2)[2]
