@@ -247,7 +247,7 @@ def test_second_order_refuses_uncovered_paths():
     torch composite raise instead of returning a silently first-order inner gradient."""
     from nerf_amd.second_order import second_order
     from nerf_amd.ngp import InstantNGP
-    ngp = InstantNGP().to(DEV)
+    ngp = InstantNGP(scene_box=torch.tensor([[-1.5] * 3, [1.5] * 3])).to(DEV)
     x = torch.rand(16, 6, device=DEV)
     with second_order():
         with pytest.raises(NotImplementedError):
