@@ -219,7 +219,10 @@ def run(a, dev, rank=0, world=1):
     from nerf_amd import ngp as G
 
     one, model = build_step(a, dev, rank, world)
+    verbose = bool(os.environ.get("NERF_BENCH_VERBOSE"))
     for s in range(a.warmup):
+        if verbose:
+            print(f"[bench_container] warmup step {s}", file=sys.stderr, flush=True)
         loss = one(s)
     assert model.occ_ready, "occupancy warm-up did not finish"
 
@@ -235,7 +238,11 @@ def run(a, dev, rank=0, world=1):
         th = time.perf_counter()
         loss = one(s)
         host += time.perf_counter() - th
+    if verbose:
+        print("[bench_container] timed steps issued", file=sys.stderr, flush=True)
     fence()
+    if verbose:
+        print("[bench_container] timed steps done", file=sys.stderr, flush=True)
     el = time.perf_counter() - t0
     if world > 1:  # the job's time is the slowest rank's
         t = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -261,6 +268,8 @@ def run(a, dev, rank=0, world=1):
         one.eager(a.warmup + a.steps + s)
     per = G.TIMING.collect()
     G.TIMING.enabled = False
+    if verbose:
+        print("[bench_container] timing pass done", file=sys.stderr, flush=True)
     ms = {k: sum(t for t, _ in v) / a.steps for k, v in per.items()}          # per step (all experts)
     launch = {k: sum(t for t, _ in v) / len(v) for k, v in per.items()}      # per launch
     n_launch = {k: len(v) / a.steps for k, v in per.items()}
@@ -333,6 +342,8 @@ def run(a, dev, rank=0, world=1):
 
 
 def main():
+    import faulthandler
+    faulthandler.enable()
     a = parse()
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
