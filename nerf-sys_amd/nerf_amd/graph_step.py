@@ -28,8 +28,14 @@ import torch
 
 
 class GraphedStep:
-    """``step_fn()`` -> loss, run eagerly ``warmup`` times on a side stream (allocator and cache warm-up, torch's
-    capture recipe), then captured; every later call replays.  ``pre_fn(step)`` runs eagerly before each call."""
+    """``step_fn()`` -> loss, run eagerly ``warmup`` times (allocator and cache warm-up), then captured; every later call
+    replays.  ``pre_fn(step)`` runs eagerly before each call.
+
+    Everything runs on the caller's current stream, which must not be the default stream, and the capture is taken on
+    that same stream: the autograd graph's AccumulateGrad nodes (one per leaf, created by the eager steps before the
+    capture and kept alive across steps) then sit on the capturing stream.  (With torch's side-stream recipe they sat on
+    the default stream, so the backward forked the default stream into the capture; the graph instantiation at the
+    end of that capture segfaulted in the HIP runtime on the full-size container step.)"""
 
     def __init__(self, step_fn: Callable[[], torch.Tensor], pre_fn: Optional[Callable[[int], None]] = None,
                  warmup: int = 2, before_capture: Optional[Callable[[], None]] = None):
@@ -41,14 +47,13 @@ class GraphedStep:
         self.pool = None
 
     def __call__(self, step: int) -> torch.Tensor:
+        st = torch.cuda.current_stream()
+        if st == torch.cuda.default_stream():
+            raise RuntimeError("GraphedStep: run the train step on a non-default stream (torch.cuda.stream(...))")
         if self.pre_fn is not None:
             self.pre_fn(step)
         if self.graph is None and self.calls < self.warmup:
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                out = self.step_fn()
-            torch.cuda.current_stream().wait_stream(s)
+            out = self.step_fn()
             self.calls += 1
             return out
         if self.graph is None:
@@ -56,7 +61,7 @@ class GraphedStep:
                 self.before_capture()
             torch.cuda.synchronize()
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, stream=st):
                 self.out = self.step_fn()
         self.graph.replay()
         self.calls += 1

@@ -31,6 +31,7 @@ def built():
 
 
 def _state(one, model):
+    torch.cuda.synchronize()                     # the steps run on the graph's own stream
     opt = one.opt
     return [t.detach().clone() for t in (opt.flat, opt.m, opt.v, opt.grad, opt.step_dev)]
 
@@ -40,6 +41,7 @@ def _restore(one, saved):
     with torch.no_grad():
         for t, s in zip((opt.flat, opt.m, opt.v, opt.grad, opt.step_dev), saved):
             t.copy_(s)
+    torch.cuda.synchronize()
 
 
 def test_graph_replay_equals_eager_step(built):
@@ -53,11 +55,14 @@ def test_graph_replay_equals_eager_step(built):
     assert losses[-1] != losses[-2]              # every replay draws its own batch (the seed counter advanced)
     step = 17                                    # no occupancy update at this step (every 16)
     saved = _state(one, model)
-    lg = float(gs(step).item())
+    with torch.cuda.stream(one.stream):
+        lg = float(gs(step).item())
+    torch.cuda.synchronize()
     pg = one.opt.flat.detach().clone()
     sg = int(one.opt.step_dev.item())
     _restore(one, saved)
     le = float(one.eager(step).item())
+    torch.cuda.synchronize()
     pe = one.opt.flat.detach().clone()
     assert sg == int(one.opt.step_dev.item()) == int(saved[4].item()) + 1
     assert abs(lg - le) <= 1e-5 * abs(le), (lg, le)
@@ -80,14 +85,18 @@ def test_graph_replay_after_occupancy_update(built):
     saved = _state(one, model)
     occ = [sub.occ_grid.occs.clone() for sub in model.submodules]
     thr_buf = model.__dict__["_vis_thr_state"]["buf"]
-    lg = float(gs(step).item())                  # pre_fn: the update + in-place threshold refresh, then the replay
+    with torch.cuda.stream(one.stream):
+        lg = float(gs(step).item())              # pre_fn: the update + in-place threshold refresh, then the replay
+    torch.cuda.synchronize()
     pg = one.opt.flat.detach().clone()
     assert any(not torch.equal(a, sub.occ_grid.occs) for a, sub in zip(occ, model.submodules)), "no update ran"
     assert model.__dict__["_vis_thr_state"]["buf"] is thr_buf          # the captured address is still the one used
     _restore(one, saved)                         # parameters back; the grids stay as the update left them
-    vis_thresholds(model)
-    one.ctr.fill_(step)
-    le = float(one.body().item())
+    with torch.cuda.stream(one.stream):
+        vis_thresholds(model)
+        one.ctr.fill_(step)
+        le = float(one.body().item())
+    torch.cuda.synchronize()
     pe = one.opt.flat.detach().clone()
     assert abs(lg - le) <= 1e-5 * abs(le), (lg, le)
     err = (pg - pe).abs().max().item()

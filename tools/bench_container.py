@@ -165,6 +165,9 @@ def build_step(a, dev, rank=0, world=1):
     one.opt, one.graphed, one.eager = opt, None, one
     if not graph:
         return one, model
+    # every step of a graph-mode run (eager or replayed) on one non-default stream, the one the graph is captured on
+    # (graph_step.GraphedStep: the autograd AccumulateGrad nodes live on the stream of the eager steps)
+    S = torch.cuda.Stream(device=dev)
     # graph mode (world 1): every step reads its seeds and its Adam step count from HBM, so eager steps and graph
     # replays run the same kernels; from capture_at on, the step is GraphedStep (warm-up, capture, replays)
     from nerf_amd.container import vis_thresholds
@@ -188,17 +191,21 @@ def build_step(a, dev, rank=0, world=1):
             vis_thresholds(model)   # in place: the captured visibility kernel reads the refreshed values
 
     def eager(step):
-        pre(step)
-        return body()
+        with torch.cuda.stream(S):
+            pre(step)
+            return body()
 
     gs = GraphedStep(body, pre, warmup=2,
                      before_capture=lambda: model.__dict__["_dev_sizes"].freeze(device=dev))
     capture_at = max(a.warmup - 3, model.submodules[0].occ_warmup_steps + 2)
 
     def one_g(step):
-        return gs(step) if step >= capture_at else eager(step)
+        if step < capture_at:
+            return eager(step)
+        with torch.cuda.stream(S):
+            return gs(step)
 
-    one_g.opt, one_g.graphed, one_g.eager, one_g.body, one_g.ctr = opt, gs, eager, body, ctr
+    one_g.opt, one_g.graphed, one_g.eager, one_g.body, one_g.ctr, one_g.stream = opt, gs, eager, body, ctr, S
     return one_g, model
 
 
