@@ -55,8 +55,7 @@ def test_graph_replay_equals_eager_step(built):
     assert losses[-1] != losses[-2]              # every replay draws its own batch (the seed counter advanced)
     step = 17                                    # no occupancy update at this step (every 16)
     saved = _state(one, model)
-    with torch.cuda.stream(one.stream):
-        lg = float(gs(step).item())
+    lg = float(one.on_S(lambda: gs(step)).item())
     torch.cuda.synchronize()
     pg = one.opt.flat.detach().clone()
     sg = int(one.opt.step_dev.item())
@@ -85,17 +84,18 @@ def test_graph_replay_after_occupancy_update(built):
     saved = _state(one, model)
     occ = [sub.occ_grid.occs.clone() for sub in model.submodules]
     thr_buf = model.__dict__["_vis_thr_state"]["buf"]
-    with torch.cuda.stream(one.stream):
-        lg = float(gs(step).item())              # pre_fn: the update + in-place threshold refresh, then the replay
+    lg = float(one.on_S(lambda: gs(step)).item())   # pre_fn: the update + in-place threshold refresh, then the replay
     torch.cuda.synchronize()
     pg = one.opt.flat.detach().clone()
     assert any(not torch.equal(a, sub.occ_grid.occs) for a, sub in zip(occ, model.submodules)), "no update ran"
     assert model.__dict__["_vis_thr_state"]["buf"] is thr_buf          # the captured address is still the one used
     _restore(one, saved)                         # parameters back; the grids stay as the update left them
-    with torch.cuda.stream(one.stream):
+    def eager_body():
         vis_thresholds(model)
         one.ctr.fill_(step)
-        le = float(one.body().item())
+        return one.body()
+
+    le = float(one.on_S(eager_body).item())
     torch.cuda.synchronize()
     pe = one.opt.flat.detach().clone()
     assert abs(lg - le) <= 1e-5 * abs(le), (lg, le)

@@ -190,10 +190,20 @@ def build_step(a, dev, rank=0, world=1):
         if "_dev_sizes" in model.__dict__:
             vis_thresholds(model)   # in place: the captured visibility kernel reads the refreshed values
 
-    def eager(step):
+    def on_S(fn):
+        # the step on S, ordered after the caller's stream work and before it (both ways: the caller reads the loss)
+        cur = torch.cuda.current_stream()
+        S.wait_stream(cur)
         with torch.cuda.stream(S):
+            out = fn()
+        cur.wait_stream(S)
+        return out
+
+    def eager(step):
+        def run():
             pre(step)
             return body()
+        return on_S(run)
 
     gs = GraphedStep(body, pre, warmup=2,
                      before_capture=lambda: model.__dict__["_dev_sizes"].freeze(device=dev))
@@ -202,10 +212,9 @@ def build_step(a, dev, rank=0, world=1):
     def one_g(step):
         if step < capture_at:
             return eager(step)
-        with torch.cuda.stream(S):
-            return gs(step)
+        return on_S(lambda: gs(step))
 
-    one_g.opt, one_g.graphed, one_g.eager, one_g.body, one_g.ctr, one_g.stream = opt, gs, eager, body, ctr, S
+    one_g.opt, one_g.graphed, one_g.eager, one_g.body, one_g.ctr, one_g.stream, one_g.on_S = opt, gs, eager, body, ctr, S, on_S
     return one_g, model
 
 
