@@ -484,8 +484,13 @@ int fused_backward(const float* w, int64_t M, const float* d_rgb_sigma, float* d
   const int64_t Mp = W.Mp;
   if (W.rps % nerf_bwd::TR) return NERF_E_ARG;
   const int S8 = (W.S + 7) / 8 * 8;
+  // the fused tail recomputes C0 with the forward's colour layer-0 fragments: packed here too (a few us), so they are
+  // this call's weights whichever forward (fused or layered) filled the workspace
+  const nerf_fused::FragTab FT_ = nerf_fused::frag_tab();
+  nerf_fused::frag_pack_kernel<<<(unsigned)nerf_cdiv(FT_.off[nerf_fused::FT] / 8, 256), 256, 0, st>>>(w, W.Wf, FT_);
   nerf_tail::TailArgs T{};
-  T.w = w; T.g = d_rgb_sigma; T.O3 = W.O3; T.O16 = W.O16; T.Y7 = W.Y[7]; T.C0 = W.C0; T.CIN = W.CIN;
+  T.w = w; T.g = d_rgb_sigma; T.O3 = W.O3; T.O16 = W.O16; T.Y7 = W.Y[7]; T.CIN = W.CIN;
+  T.wfc0 = W.Wf + FT_.off[9];
   T.dZ7 = W.dA; T.partial = W.partial; T.partial2 = W.partial2;
   T.slab = L.total; T.off16 = L.off[16]; T.cslab = L.total - L.off[16];
   T.off17 = L.off[17]; T.off18 = L.off[18]; T.off19 = L.off[19]; T.off20 = L.off[20]; T.off21 = L.off[21];

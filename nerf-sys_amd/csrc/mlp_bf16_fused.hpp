@@ -588,7 +588,8 @@ __device__ __forceinline__ void io_role(const FusedArgs& A, nerf_bf16* Hs, nerf_
     if (TRAIN) io_copy<64, false>(Es, EP, A.CIN, 64, m0, nullptr, j, lane);
     bar();  // C: colour layer 0 output in H[1]; colour 0 done reading E
     if (next) enc.store(Es, EP, j, lane);
-    if (TRAIN) io_copy<128, MASKS>(Hs + BMF * HP, CP, A.C0, 128, m0, A.MC0, j, lane);
+    // C0 (+ its mask words) only for the LAYERED backward: the fused tail recomputes it from CIN (mlp_bf16_tail.hpp)
+    if (TRAIN && MASKS) io_copy<128, MASKS>(Hs + BMF * HP, CP, A.C0, 128, m0, A.MC0, j, lane);
     bar();  // D
   }
 }

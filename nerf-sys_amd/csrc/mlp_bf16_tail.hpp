@@ -13,11 +13,15 @@
 // with the layered path's bf16 rounding points and MFMA k order, so dZ7 — and with it every trunk gradient — is
 // bitwise the layered path's; the head / colour weight sums run over the two halves of each split (two workgroups,
 // the second half's sums in partial2, added by reduce_splits2 after the slab terms): a fixed order, not the layered one.
-// HBM per row: Y7 512 + C0 256 + CIN 128 + g / O3 / sigma_raw 36 B read, dZ7 512 B written (~1.45 KB; the chain
-// moved ~3.6 KB).  Workgroup = 12 waves: 8 compute + 4 io waves that stage tiles through two register sets into two
-// LDS stages (mlp_bf16_bwd.hpp's scheme).
+// HBM per row: Y7 512 + CIN 128 + g / O3 / sigma_raw 36 B read, dZ7 512 B written (~1.2 KB; the chain moved
+// ~3.6 KB).  Round 6: C0 (the colour layer-0 output, 256 B per row) is no longer written by the fused forward and read
+// back here — each compute wave recomputes its 32 x 32 block of the tile's C0 from the CIN tile with the forward's
+// fragments, bias-initialised accumulators, k order and ReLU / rounding (mlp_bf16_fused.hpp colour layer 0): bitwise
+// the forward's C0, for 4 MFMAs per wave and tile.  Workgroup = 12 waves: 8 compute + 4 io waves that stage tiles
+// through two register sets into two LDS stages (mlp_bf16_bwd.hpp's scheme).
 #pragma once
 #include "mlp_bf16_bwd.hpp"
+#include "mlp_bf16_fused.hpp"
 
 namespace NERF_H16NS {
 namespace nerf_tail {
@@ -27,7 +31,8 @@ using nerf_bwd::swz;
 typedef nerf_bwd::io_u32x4 u32x4;
 
 constexpr int TR = 64;
-// stage (bytes): Y7 [64][256] bf16 | C0 [64][128] | CIN [64][64] | g [64] float4 | O3 cols 0..3 [64] float4 | sraw [64]
+// stage (bytes): Y7 [64][256] bf16 | C0 [64][128] (written by the compute waves) | CIN [64][64] | g [64] float4 |
+// O3 cols 0..3 [64] float4 | sraw [64]
 constexpr int Y_OFF = 0, C_OFF = 64 * 512, I_OFF = C_OFF + 64 * 256, G_OFF = I_OFF + 64 * 128;
 constexpr int O_OFF = G_OFF + 1024, S_OFF = O_OFF + 1024, STB = S_OFF + 256;
 constexpr int NSTG = 2;
@@ -52,8 +57,8 @@ struct TailArgs {
   const float* O3;     // [Mp][32] colour-out pre-activations (cols 0..2)
   const float* O16;    // [Mp][32] col 0 = sigma_raw
   const nerf_bf16* Y7; // trunk.7 output [Mp][256]
-  const nerf_bf16* C0; // colour layer-0 output [Mp][128]
   const nerf_bf16* CIN;// colour input [Mp][64]
+  const nerf_bf16* wfc0;// colour layer 0's fragment image (frag_pack_kernel, tensor 9: 128 x 64, 2 x 4 fragments)
   nerf_bf16* dZ7;      // [Mp][256]
   float* partial;      // slab s of the packed gradient (split s, first half)
   float* partial2;     // [S][cslab] second halves: packed offsets off16 .. total
@@ -116,6 +121,7 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
     wc1[ks] = wfrag(W + A.off20, 128, 1, 32 * (w & 3), ks, lane);  // A[i = C0 col][kk = dO3 col] = Wc1[kk][i]
     wh[ks] = wfrag(W + A.off16, 256, 1, 32 * w, ks, lane);        // A[i = Y7 col][kk = dO16 col] = Wh[kk][i]
   }
+
   if constexpr (NERF_F16)  // geo only: the sigma row (kk = 0: k-step 0, lane half 0, element 0) is added apart
     if (lh == 0) H16_SET(wh[0], 0, 0.f);
   nerf_f32x16 ac1, ac0, ahd;  // dWc1 (waves 0-3: k-block w), dWc0 (n-block w >> 1, k-block w & 1), dWh (k-block w)
@@ -139,6 +145,44 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
     raw_barrier();  // T_t
     const char* L = lds + (t % NSTG) * STB;
     const uint32_t Lo = (uint32_t)((t % NSTG) * STB);
+    // ---- C0 of the tile (rows 32 (w >> 2).., cols 32 (w & 3)..) from its CIN rows: the fused forward's colour layer 0
+    // (acc_bias, 4 k-steps in order, relu_pk_out, the lane-half pairing of relu_to_lds) -> the stage's C0 slot
+    {
+      const int cb = w & 3, row = 32 * (w >> 2) + li;
+      // the weights: A[i = C0 col 32 cb + i][kk = CIN col] = Wc0[col][kk], fragment (nb = cb, ks) of the fused forward's
+      // image of colour layer 0 (frag_pack_kernel: ((nb * 4 + ks) * 64 + lane) * 8), loaded per tile from uniform bases
+      // laundered per tile (hoisted out of the tile loop, the fragments and the bias held 32 VGPRs across it: the
+      // compute waves sit at 166 of 168 without them)
+      uint64_t wp_ = (uint64_t)(uintptr_t)A.wfc0, bp_ = (uint64_t)(uintptr_t)(W + A.off19);
+      asm volatile("" : "+s"(wp_), "+s"(bp_));
+      const nerf_bf16* wcp = reinterpret_cast<const nerf_bf16*>(wp_) + ((int64_t)cb * 256 + lane) * 8;
+      const float* bc0 = reinterpret_cast<const float*>(bp_);
+      nerf_f32x16 c;
+      nerf_fused::acc_bias(c, bc0, 32 * cb, lh);
+#pragma unroll
+      for (int k2 = 0; k2 < 4; k2 += 2) {  // two fragments in flight at a time (register pressure: 168 VGPRs)
+        const nerf_bf16x8 wa = *reinterpret_cast<const nerf_bf16x8*>(wcp + k2 * 64 * 8);
+        const nerf_bf16x8 wb = *reinterpret_cast<const nerf_bf16x8*>(wcp + (k2 + 1) * 64 * 8);
+        c = h16_mfma(wa, ld16(L + ai(row, 2 * k2 + lh)), c);
+        c = h16_mfma(wb, ld16(L + ai(row, 2 * k2 + 2 + lh)), c);
+      }
+      uint2 pk[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (H16_BIAS_AFTER) b4 = *reinterpret_cast<const float4*>(bc0 + 32 * cb + 8 * q + 4 * lh);
+        pk[q] = make_uint2(nerf_fused::relu_pk_out(c[4 * q], c[4 * q + 1], b4.x, b4.y),
+                           nerf_fused::relu_pk_out(c[4 * q + 2], c[4 * q + 3], b4.z, b4.w));
+      }
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        uint2 x = pk[2 * pr], y = pk[2 * pr + 1];
+        const auto r0_ = __builtin_amdgcn_permlane32_swap(x.x, y.x, false, false);
+        const auto r1_ = __builtin_amdgcn_permlane32_swap(x.y, y.y, false, false);
+        *reinterpret_cast<uint4*>(lds + (t % NSTG) * STB + ac(row, 4 * cb + 2 * pr + lh)) =
+            make_uint4(r0_[0], r1_[0], r0_[1], r1_[1]);
+      }
+    }
     // ---- P0: head-output derivatives of the tile's rows (wave 0, lane = row)
     if (w == 0) {
       const int64_t m = r0 + (int64_t)t * TR + lane;
@@ -320,9 +364,9 @@ __device__ __forceinline__ void tail_compute(const TailArgs& A, char* lds, float
   }
 }
 
-// ---- io waves: two named register sets of one tile each (15 x 16 B per lane)
+// ---- io waves: two named register sets of one tile each (11 x 16 B per lane)
 struct TailSet {
-  u32x4 v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14;
+  u32x4 v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10;
   template <int I>
   __device__ __forceinline__ u32x4& at() {
     if constexpr (I == 0) return v0;
@@ -335,45 +379,35 @@ struct TailSet {
     else if constexpr (I == 7) return v7;
     else if constexpr (I == 8) return v8;
     else if constexpr (I == 9) return v9;
-    else if constexpr (I == 10) return v10;
-    else if constexpr (I == 11) return v11;
-    else if constexpr (I == 12) return v12;
-    else if constexpr (I == 13) return v13;
-    else return v14;
+    else return v10;
   }
 };
-// io wave j, rows 16 j .. 16 j + 15 of the tile: Y7 (8 pieces of 2 rows), C0 (4 pieces of 4 rows), CIN (2 pieces of 8
-// rows); plus one per-row vector of all 64 rows: j = 0 g, j = 1 O3 cols 0..3, j = 2 sigma_raw
+// io wave j, rows 16 j .. 16 j + 15 of the tile: Y7 (8 pieces of 2 rows), CIN (2 pieces of 8 rows); plus one per-row
+// vector of all 64 rows: j = 0 g, j = 1 O3 cols 0..3, j = 2 sigma_raw
 __device__ __forceinline__ void tail_load(TailSet& S, const TailArgs& A, int64_t m0, int j, int lane) {
   const nerf_bf16* y = A.Y7 + (m0 + 16 * j + (lane >> 5)) * 256 + 8 * (lane & 31);
-  const nerf_bf16* c = A.C0 + (m0 + 16 * j + (lane >> 4)) * 128 + 8 * (lane & 15);
   const nerf_bf16* x = A.CIN + (m0 + 16 * j + (lane >> 3)) * 64 + 8 * (lane & 7);
   static_for<0, 8>([&](auto I) { S.template at<decltype(I)::value>() = *reinterpret_cast<const u32x4*>(y + 512 * decltype(I)::value); });
-  static_for<0, 4>([&](auto I) { S.template at<8 + decltype(I)::value>() = *reinterpret_cast<const u32x4*>(c + 512 * decltype(I)::value); });
-  static_for<0, 2>([&](auto I) { S.template at<12 + decltype(I)::value>() = *reinterpret_cast<const u32x4*>(x + 512 * decltype(I)::value); });
+  static_for<0, 2>([&](auto I) { S.template at<8 + decltype(I)::value>() = *reinterpret_cast<const u32x4*>(x + 512 * decltype(I)::value); });
   // one unconditional 16-B load per lane for every io wave (a conditional load left the compiler unable to count the
   // set's loads: it drained vmcnt(0) before the stores); g is [M][4]: rows past M read row M - 1 and are zeroed
   const int64_t m = m0 + lane;
   const float* pv = j == 0 ? A.g + (m < A.M ? m : A.M - 1) * 4 : (j == 1 ? A.O3 : A.O16) + m * 32;
-  S.v14 = *reinterpret_cast<const u32x4*>(pv);
-  if (j == 0 && m >= A.M) S.v14 = u32x4{0u, 0u, 0u, 0u};
+  S.v10 = *reinterpret_cast<const u32x4*>(pv);
+  if (j == 0 && m >= A.M) S.v10 = u32x4{0u, 0u, 0u, 0u};
 }
 __device__ __forceinline__ void tail_store(TailSet& S, char* st, int j, int lane) {
   static_for<0, 8>([&](auto I) {
     constexpr int i = decltype(I)::value;
     *reinterpret_cast<u32x4*>(st + ay(16 * j + 2 * i + (lane >> 5), lane & 31)) = S.template at<i>();
   });
-  static_for<0, 4>([&](auto I) {
-    constexpr int i = decltype(I)::value;
-    *reinterpret_cast<u32x4*>(st + ac(16 * j + 4 * i + (lane >> 4), lane & 15)) = S.template at<8 + i>();
-  });
   static_for<0, 2>([&](auto I) {
     constexpr int i = decltype(I)::value;
-    *reinterpret_cast<u32x4*>(st + ai(16 * j + 8 * i + (lane >> 3), lane & 7)) = S.template at<12 + i>();
+    *reinterpret_cast<u32x4*>(st + ai(16 * j + 8 * i + (lane >> 3), lane & 7)) = S.template at<8 + i>();
   });
-  if (j == 0) *reinterpret_cast<u32x4*>(st + G_OFF + 16 * lane) = S.v14;
-  if (j == 1) *reinterpret_cast<u32x4*>(st + O_OFF + 16 * lane) = S.v14;
-  if (j == 2) *reinterpret_cast<uint32_t*>(st + S_OFF + 4 * lane) = S.v14.x;
+  if (j == 0) *reinterpret_cast<u32x4*>(st + G_OFF + 16 * lane) = S.v10;
+  if (j == 1) *reinterpret_cast<u32x4*>(st + O_OFF + 16 * lane) = S.v10;
+  if (j == 2) *reinterpret_cast<uint32_t*>(st + S_OFF + 4 * lane) = S.v10.x;
 }
 __device__ __forceinline__ void tail_step(TailSet& R, const TailArgs& A, char* lds, int j, int t, int nT, int64_t r0,
                                           int lane) {
