@@ -37,7 +37,7 @@ constexpr int64_t WTB_ELEMS = 7 * 65536 + 256 * 32 + 128 * 32 + 32 * 128;
 struct WSB {
   int64_t Mp;
   nerf_bf16 *Wb, *Wf, *X3E, *Y[8], *CIN, *C0;
-  float *O16, *O3;
+  float *O16, *O3, *HO;
   uint32_t *MB[8], *MC0;
   nerf_bf16 *dA, *dB, *dO16, *dO3, *dC0, *WTb, *WTf;
   float *dCIN, *partial, *partial2, *np;
@@ -86,6 +86,7 @@ WSB carve_b(void* base, int64_t M, int training) {
   w.CIN = (nerf_bf16*)take(Mp * 64 * 2);
   w.C0 = (nerf_bf16*)take(Mp * 128 * 2);
   w.O3 = (float*)take(Mp * 32 * 4);
+  w.HO = (float*)take(Mp * 4 * 4);
   if (training) {
     for (int i = 0; i < 8; ++i) w.MB[i] = (uint32_t*)take(Mp * 8 * 4);
     w.MC0 = (uint32_t*)take(Mp * 4 * 4);
@@ -218,12 +219,14 @@ __global__ void build_cin_bf16_kernel(const float* __restrict__ xd, const float*
                       nerf_pack_bf16x2(v[8 * c + 4], v[8 * c + 5]), nerf_pack_bf16x2(v[8 * c + 6], v[8 * c + 7]));
 }
 
+// (HO, training: the dense (o3, sigma_raw) row the fused tail reads, so a layered forward feeds the fused backward)
 __global__ void head_out_b_kernel(const float* __restrict__ O3, const float* __restrict__ O16, int64_t M,
-                                  float* __restrict__ out) {
+                                  float* __restrict__ out, float* __restrict__ HO) {
   const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
   const float* c = O3 + m * 32;
   const float sr = O16[m * 32];
+  if (HO) reinterpret_cast<float4*>(HO)[m] = make_float4(c[0], c[1], c[2], sr);
   const float sg = expf(fminf(fmaxf(sr, -EXP_MAX), EXP_MAX));
   reinterpret_cast<float4*>(out)[m] = make_float4(sigmoidf_(c[0]), sigmoidf_(c[1]), sigmoidf_(c[2]), sg);
 }
@@ -379,7 +382,7 @@ int fused_forward(const float* w, const float* x_d, int64_t M, float* rgb_sigma,
   A.X3E = W.X3E;
   A.Y = training ? W.Y[0] : nullptr;
   A.MB = training ? W.MB[0] : nullptr;
-  A.O16 = W.O16; A.CIN = W.CIN; A.C0 = W.C0; A.MC0 = training ? W.MC0 : nullptr; A.O3 = W.O3;
+  A.O16 = W.O16; A.CIN = W.CIN; A.C0 = W.C0; A.MC0 = training ? W.MC0 : nullptr; A.O3 = W.O3; A.HO = W.HO;
   A.out = rgb_sigma;
   A.M = M;
   A.Mp = Mp;
@@ -489,7 +492,7 @@ int fused_backward(const float* w, int64_t M, const float* d_rgb_sigma, float* d
   const nerf_fused::FragTab FT_ = nerf_fused::frag_tab();
   nerf_fused::frag_pack_kernel<<<(unsigned)nerf_cdiv(FT_.off[nerf_fused::FT] / 8, 256), 256, 0, st>>>(w, W.Wf, FT_);
   nerf_tail::TailArgs T{};
-  T.w = w; T.g = d_rgb_sigma; T.O3 = W.O3; T.O16 = W.O16; T.Y7 = W.Y[7]; T.CIN = W.CIN;
+  T.w = w; T.g = d_rgb_sigma; T.HO = W.HO; T.Y7 = W.Y[7]; T.CIN = W.CIN;
   T.wfc0 = W.Wf + FT_.off[9];
   T.dZ7 = W.dA; T.partial = W.partial; T.partial2 = W.partial2;
   T.slab = L.total; T.off16 = L.off[16]; T.cslab = L.total - L.off[16];
@@ -585,7 +588,7 @@ extern "C" int NERF_H16_FN(nerf_mlp_fwd)(const float* w, const float* x_d, int64
   TRY((ntb<EPI_BIAS_RELU, 1>(W.CIN, 64, Wb(18), 64, Bias(19), W.C0, 128, nullptr, training ? W.MC0 : nullptr, Mp,
                              128, 64, st)));
   TRY((ntb<EPI_BIAS, 0>(W.C0, 128, Wb(20), 128, Bias(21), W.O3, 32, nullptr, nullptr, Mp, 32, 128, st)));
-  head_out_b_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(W.O3, W.O16, M, rgb_sigma);
+  head_out_b_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(W.O3, W.O16, M, rgb_sigma, training ? W.HO : nullptr);
   return nerf_launch_status();
 }
 

@@ -137,11 +137,12 @@ struct FusedArgs {
   nerf_bf16* X3E;        // [Mp][320]: cols 256..319 = enc (read); training: cols 0..255 = trunk.3 output
   nerf_bf16* Y;          // training: Y0, Y1, Y2, Y4, ..., Y7 back to back ([Mp][256] each; Y3 lives in X3E)
   uint32_t* MB;          // training: MB0..MB7 back to back ([Mp][8] ReLU bitmask words each)
-  float* O16;            // [Mp][32] fp32: col 0 = sigma pre-activation (training)
+  float* O16;            // [Mp][32] fp32: col 0 = sigma pre-activation (training, layered backward only)
   nerf_bf16* CIN;        // [Mp][64] colour input (prefill read; training: written back complete)
   nerf_bf16* C0;         // [Mp][128] (training)
   uint32_t* MC0;         // [Mp][4] (training)
-  float* O3;             // [Mp][32] fp32 colour-out pre-activations, cols 0..3 (training)
+  float* O3;             // [Mp][32] fp32 colour-out pre-activations, cols 0..3 (training, layered backward only)
+  float* HO;             // [Mp][4] fp32 (o3_0, o3_1, o3_2, sigma_raw): what the fused tail reads (training)
   float* out;            // [M][4] rgb_sigma
   const float* xd;       // [M][6] sample points + directions (the io waves encode them: no prefill launch)
   int64_t M, Mp;
@@ -594,7 +595,7 @@ __device__ __forceinline__ void io_role(const FusedArgs& A, nerf_bf16* Hs, nerf_
   }
 }
 
-template <bool TRAIN>
+template <bool TRAIN, bool MASKS>
 __device__ __forceinline__ void compute_role(const FusedArgs& A, nerf_bf16* Hs, nerf_bf16* Es, float* Ssig,
                                              const float* Bs, int tile, int G, int w, int li, int lh, int lane) {
   const __amdgpu_buffer_rsrc_t rs =
@@ -677,9 +678,13 @@ __device__ __forceinline__ void compute_role(const FusedArgs& A, nerf_bf16* Hs, 
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[0][0][e] = acc_out(acc[0][0], e, BI(10), 0, 0);
       if (TRAIN) {
-        // the backward reads sigma_raw (O16 col 0) and the colour-out pre-activations (O3 cols 0..2)
-        A.O16[m * 32] = sraw;
-        *reinterpret_cast<float4*>(A.O3 + m * 32) = make_float4(acc[0][0][0], acc[0][0][1], acc[0][0][2], acc[0][0][3]);
+        // the fused tail reads the colour-out pre-activations and sigma_raw as ONE dense 16-B row (round 6; the two
+        // [Mp][32] rows below, 20 B used of two 128-B lines, stay for the layered backward)
+        *reinterpret_cast<float4*>(A.HO + m * 4) = make_float4(acc[0][0][0], acc[0][0][1], acc[0][0][2], sraw);
+        if (MASKS) {
+          A.O16[m * 32] = sraw;
+          *reinterpret_cast<float4*>(A.O3 + m * 32) = make_float4(acc[0][0][0], acc[0][0][1], acc[0][0][2], acc[0][0][3]);
+        }
       }
       if (m < A.M) {
         const float sg = expf(fminf(fmaxf(sraw, -EXP_MAX), EXP_MAX));
@@ -716,7 +721,7 @@ __global__ __launch_bounds__(512, 1) void mlp_fwd_fused_bf16_kernel(FusedArgs A)
   if (w >= NCW)
     io_role<TRAIN, MASKS>(A, Hs, Es, tile, gridDim.x, w - NCW, lane);
   else
-    compute_role<TRAIN>(A, Hs, Es, Ssig, Bs, tile, gridDim.x, w, lane & 31, lane >> 5, lane);
+    compute_role<TRAIN, MASKS>(A, Hs, Es, Ssig, Bs, tile, gridDim.x, w, lane & 31, lane >> 5, lane);
 }
 
 }  // namespace nerf_fused

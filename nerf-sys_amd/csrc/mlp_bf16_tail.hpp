@@ -13,7 +13,7 @@
 // with the layered path's bf16 rounding points and MFMA k order, so dZ7 — and with it every trunk gradient — is
 // bitwise the layered path's; the head / colour weight sums run over the two halves of each split (two workgroups,
 // the second half's sums in partial2, added by reduce_splits2 after the slab terms): a fixed order, not the layered one.
-// HBM per row: Y7 512 + CIN 128 + g / O3 / sigma_raw 36 B read, dZ7 512 B written (~1.2 KB; the chain moved
+// HBM per row: Y7 512 + CIN 128 + g / HO 32 B read, dZ7 512 B written (~1.2 KB; the chain moved
 // ~3.6 KB).  Round 6: C0 (the colour layer-0 output, 256 B per row) is no longer written by the fused forward and read
 // back here — each compute wave recomputes its 32 x 32 block of the tile's C0 from the CIN tile with the forward's
 // fragments, bias-initialised accumulators, k order and ReLU / rounding (mlp_bf16_fused.hpp colour layer 0): bitwise
@@ -54,8 +54,7 @@ __device__ __forceinline__ int adc(int r, int c) { return DC_OFF + r * 256 + 16 
 struct TailArgs {
   const float* w;      // fp32 packed parameters
   const float* g;      // d_rgb_sigma [M][4]
-  const float* O3;     // [Mp][32] colour-out pre-activations (cols 0..2)
-  const float* O16;    // [Mp][32] col 0 = sigma_raw
+  const float* HO;     // [Mp][4] colour-out pre-activations 0..2, sigma_raw (the fused forward's dense row)
   const nerf_bf16* Y7; // trunk.7 output [Mp][256]
   const nerf_bf16* CIN;// colour input [Mp][64]
   const nerf_bf16* wfc0;// colour layer 0's fragment image (frag_pack_kernel, tensor 9: 128 x 64, 2 x 4 fragments)
@@ -383,7 +382,7 @@ struct TailSet {
   }
 };
 // io wave j, rows 16 j .. 16 j + 15 of the tile: Y7 (8 pieces of 2 rows), CIN (2 pieces of 8 rows); plus one per-row
-// vector of all 64 rows: j = 0 g, j = 1 O3 cols 0..3, j = 2 sigma_raw
+// vector of all 64 rows: j = 0 g, j = 1 HO (O3 cols 0..2 + sigma_raw), j = 2 sigma_raw (HO col 3)
 __device__ __forceinline__ void tail_load(TailSet& S, const TailArgs& A, int64_t m0, int j, int lane) {
   const nerf_bf16* y = A.Y7 + (m0 + 16 * j + (lane >> 5)) * 256 + 8 * (lane & 31);
   const nerf_bf16* x = A.CIN + (m0 + 16 * j + (lane >> 3)) * 64 + 8 * (lane & 7);
@@ -392,7 +391,7 @@ __device__ __forceinline__ void tail_load(TailSet& S, const TailArgs& A, int64_t
   // one unconditional 16-B load per lane for every io wave (a conditional load left the compiler unable to count the
   // set's loads: it drained vmcnt(0) before the stores); g is [M][4]: rows past M read row M - 1 and are zeroed
   const int64_t m = m0 + lane;
-  const float* pv = j == 0 ? A.g + (m < A.M ? m : A.M - 1) * 4 : (j == 1 ? A.O3 : A.O16) + m * 32;
+  const float* pv = j == 0 ? A.g + (m < A.M ? m : A.M - 1) * 4 : A.HO + m * 4;
   S.v10 = *reinterpret_cast<const u32x4*>(pv);
   if (j == 0 && m >= A.M) S.v10 = u32x4{0u, 0u, 0u, 0u};
 }
@@ -407,7 +406,7 @@ __device__ __forceinline__ void tail_store(TailSet& S, char* st, int j, int lane
   });
   if (j == 0) *reinterpret_cast<u32x4*>(st + G_OFF + 16 * lane) = S.v10;
   if (j == 1) *reinterpret_cast<u32x4*>(st + O_OFF + 16 * lane) = S.v10;
-  if (j == 2) *reinterpret_cast<uint32_t*>(st + S_OFF + 4 * lane) = S.v10.x;
+  if (j == 2) *reinterpret_cast<uint32_t*>(st + S_OFF + 4 * lane) = S.v10.w;
 }
 __device__ __forceinline__ void tail_step(TailSet& R, const TailArgs& A, char* lds, int j, int t, int nT, int64_t r0,
                                           int lane) {
