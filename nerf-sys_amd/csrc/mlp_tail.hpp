@@ -139,33 +139,42 @@ static __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* _
   if (r0 < r1) fetch(r0);
   for (int64_t t0 = r0; t0 < r1; t0 += CB_ROWS) {
     __syncthreads();  // previous tile's LDS readers are done
-    {  // ---- the CIN row in the head's alignment (rows >= M all zero, as the forward's colour input)
+    {  // ---- the CIN row in the head's alignment (rows >= M all zero, as the forward's colour input).  Thread (row cr,
+      // quarter cq): ONE sincosf per (dimension, band) pair p = 3 cq .. 3 cq + 2 of its row (the same libm call on the
+      // same argument as the forward tail's cin_dir_value, so the same bits; cos -> canonical col 18 + 8 k + l, sin ->
+      // 22 + 8 k + l), geo / d cols 5 cq .. 5 cq + 4 (< 18), and the zero cols 43 + 8 cq .. of the head-aligned
+      // tile; no lane runs another quarter's branch
       const bool real = t0 + cr < M;
       const float d[3] = {pdir.x, pdir.y, pdir.z};
-      float v[16];
-      if (cq == 0) {
-        const float o[16] = {ph[0].x, ph[0].y, ph[0].z, ph[0].w, ph[1].x, ph[1].y, ph[1].z, ph[1].w,
-                             ph[2].x, ph[2].y, ph[2].z, ph[2].w, ph[3].x, ph[3].y, ph[3].z, ph[3].w};
+      float* sr = s_cin + cr * CB_CIN;      // head-aligned: canonical col c at c + 1
 #pragma unroll
-        for (int c = 0; c < 16; ++c) v[c] = (real && c > 0) ? o[c] : 0.f;
-      } else if (cq < 3) {
+      for (int i = 0; i < 3; ++i) {
+        const int p = 3 * cq + i, k = p >> 2, l = p & 3;
+        float sn, cs;
+        sincosf(d[k] * (float)(1 << l), &sn, &cs);
+        sr[1 + 18 + 8 * k + l] = real ? cs : 0.f;
+        sr[1 + 22 + 8 * k + l] = real ? sn : 0.f;
+      }
+      const float o[16] = {ph[0].x, ph[0].y, ph[0].z, ph[0].w, ph[1].x, ph[1].y, ph[1].z, ph[1].w,
+                           ph[2].x, ph[2].y, ph[2].z, ph[2].w, ph[3].x, ph[3].y, ph[3].z, ph[3].w};
 #pragma unroll
-        for (int c = 0; c < 16; ++c) {  // one sincosf at a time (as the forward tail)
-          v[c] = real ? cin_dir_value(16 * cq + c - 1, d) : 0.f;
-          __builtin_amdgcn_sched_barrier(0);
+      for (int i = 0; i < 5; ++i) {
+        const int c = 5 * cq + i;           // canonical geo 0..14 (O16 col c + 1), d 15..17
+        if (c < 18) {
+          float v = 0.f;
+#pragma unroll
+          for (int e = 0; e < 15; ++e)
+            if (c == e) v = o[e + 1];
+          if (c >= 15) v = d[c - 15];
+          sr[1 + c] = real ? v : 0.f;
         }
-      } else {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) v[c] = 0.f;
       }
-      float* sr = s_cin + cr * CB_CIN + 16 * cq;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        *reinterpret_cast<float4*>(sr + 4 * u) = make_float4(v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]);
-      if (cq == 3) {
-        *reinterpret_cast<float4*>(sr + 16) = make_float4(0.f, 0.f, 0.f, 0.f);
-        *reinterpret_cast<float4*>(sr + 20) = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int i = 0; i < 8; ++i) {         // head-aligned cols 0 and 43..71 (canonical 42..62 and the padding)
+        const int c = 43 + 8 * cq + i;
+        if (c < CB_CIN) sr[c] = 0.f;
       }
+      if (cq == 0) sr[0] = 0.f;
     }
     if (tid < CB_ROWS) {
       const int64_t m = t0 + tid;
