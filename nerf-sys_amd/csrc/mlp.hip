@@ -11,8 +11,8 @@
 // Activation layout in the caller's workspace (Mp = M rounded up to 256, row-major, fp32):
 //   X3E [Mp][320] : cols 0..255 = trunk.3 output, cols 256..318 = xyz encoding, col 319 = 0
 //                   (so trunk.4 reads cat([h, enc]) with K = 320 and no copy; trunk.0 reads cols 256..319)
-//   Y0..Y2, Y4..Y7 [Mp][256], HO [Mp][24] (colour pre-activations 0..2, sigma_raw, the 16 head outputs, the
-//   direction: the colour backward rebuilds the colour input and recomputes C0 from it).  Backward adds dA/dB [Mp][256], dO16 [Mp][16] (from the fused colour-branch backward),
+//   Y0..Y2, Y4..Y7 [Mp][256], HO [Mp][4] (colour pre-activations 0..2, sigma_raw), CIN [Mp][64] (geo | dir-enc |
+//   0), C0 [Mp][128].  Backward adds dA/dB [Mp][256], dO16 [Mp][16] (from the fused colour-branch backward),
 //   transposed trunk weights, and S split-M partial slabs of the packed gradient.
 #include "gemm.hpp"
 #include "gemm_x6.hpp"
@@ -26,7 +26,7 @@ using namespace nerf_mlp;
 
 struct WS {
   int64_t Mp;
-  float *X3E, *Y[8], *HO;
+  float *X3E, *Y[8], *HO, *CIN, *C0;
   uint32_t* MB[8];  // ReLU bitmasks of the trunk outputs [Mp][8] (colour layer 0 re-derives its mask from C0 > 0)
   // backward
   float *dA, *dB, *dO16, *WT, *partial, *partial2;
@@ -68,7 +68,9 @@ WS carve(void* base, int64_t M, int training) {
     float* q = take(Mp * 256);
     for (int i = 0; i < 8; ++i) w.Y[i] = (i % 2 == 0) ? q : w.X3E;  // ping-pong
   }
-  w.HO = take(Mp * FT_HO);
+  w.HO = take(Mp * 4);
+  w.CIN = take(Mp * 64);
+  w.C0 = take(Mp * 128);
   if (training) {
     for (int i = 0; i < 8; ++i) w.MB[i] = reinterpret_cast<uint32_t*>(take(Mp * 8));
     if (training == 2) {  // the weight-gradient stream reads dZ_i while the input-gradient chain runs ahead
@@ -458,7 +460,7 @@ extern "C" int nerf_mlp_fwd_ex(const float* w, const float* x_d, int64_t M, floa
     T.Y7 = in; T.ldy = ld_in; T.xd = x_d; T.w = w;
     T.off_wh = L.off[16]; T.off_bh = L.off[17]; T.off_wc0 = L.off[18]; T.off_bc0 = L.off[19];
     T.off_wc1 = L.off[20]; T.off_bc1 = L.off[21];
-    T.HO = W.HO; T.out = rgb_sigma;
+    T.HO = W.HO; T.CIN = W.CIN; T.C0 = W.C0; T.out = rgb_sigma;
     T.M = M; T.Mp = Mp; T.ntiles = (int)(Mp / FT_ROWS);
     const int n_cu = nerf_cu_count();
     const int grid = T.ntiles < 2 * n_cu ? T.ntiles : 2 * n_cu;
@@ -551,7 +553,7 @@ int mlp_bwd_impl(const float* w, int64_t M, const float* d_rgb_sigma, float* d_w
   // events 2/3 (layer 0 has no input gradient) bracket the backward tail (colour branch + heads -> dZ7)
   if (ev) (void)hipEventRecord(ev[2], st);
   // colour branch -> dO16 [Mp][16]; then ONE pass over Y7 for dZ7 and the head weight / bias sums (mlp_tail.hpp)
-  color_bwd_kernel<<<TAIL_NQ * W.S, 256, 0, st>>>(d_rgb_sigma, W.HO, Wt(18), Wt(19), Wt(20), W.dO16,
+  color_bwd_kernel<float, float><<<TAIL_NQ * W.S, 256, 0, st>>>(d_rgb_sigma, W.HO, W.C0, W.CIN, Wt(18), Wt(20), W.dO16,
                                                           W.partial, L.total, L.off[18], L.off[19], L.off[20], L.off[21],
                                                           W.rps, M, Mp, W.partial2, L.total - P2BASE, P2BASE, 16);
   head_bwd_kernel<<<TAIL_NQ * W.S, 256, 0, st>>>(W.dO16, W.Y[7], Wt(16), dcur, W.partial, L.total, W.partial2,

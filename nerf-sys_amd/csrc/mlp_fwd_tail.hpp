@@ -7,11 +7,7 @@
 //   rgb_sigma = [sigmoid(O3), trunc_exp(sigma_raw)]                              (models/trunc_exp.py:30-61)
 // The unfused chain ran five launches per net (two N = 32 GEMMs, the colour-input build, the colour layer-0 GEMM and
 // the head activation) and moved ~2.9 KB per sample row through HBM; this kernel reads the trunk.7 row (1 KB) and
-// the direction, and writes rgb_sigma and, in training, ONE 80-B row per sample for the backward (HO: the colour
-// pre-activations, sigma_raw and the 16 head outputs).  Round 6: the colour input (256 B) and the colour layer-0
-// output (512 B) are no longer written — the colour backward (mlp_tail.hpp) rebuilds CIN from the head outputs and
-// the direction and recomputes C0 with this kernel's MFMA sequence (bitwise the same values), 1.4 KB per row less
-// HBM traffic between the two launches.
+// the direction, and writes what the backward reads (HO 16 B, CIN 256 B, C0 512 B) and rgb_sigma.
 //
 // Geometry: a 256-thread workgroup (4 waves) walks 64-row tiles (persistent, two workgroups per CU); wave w owns rows
 // 16 w .. 16 w + 15 of the tile through all three layers.  Every product is v_mfma_f32_16x16x4_f32 (exact fp32 fmaf
@@ -37,17 +33,15 @@ constexpr int FT_ROWS = 64;
 // 64-bank array; its lane groups {0-3,12-15,20-27}, ... mix (lr, g) with (lr - 4 .. lr + 7, g + 1), which are all
 // distinct for P / 4 = 2 (mod 16) (slots 2 lr + g): 264 / 72 / 136.  The round-4 pitches 260 / 52 / 132 (P / 4 odd)
 // put two lanes of every group on one slot: 1.4e7 conflict cycles per fine launch (profiles/r05/pmc_mfma.txt).
-constexpr int FT_WH = 264, FT_WC0 = 72, FT_WC1 = 136;
-// HO row (training, [Mp][FT_HO] fp32, 96 B): [o3_0, o3_1, o3_2, sigma_raw | O16 cols 0..15 = sigma_raw, geo 0..14 |
-// d_x, d_y, d_z, 0] — the direction too, since the backward entry point receives no sample rows
-constexpr int FT_HO = 24;
+// The CIN staging pitch 68 keeps its scalar writes at most 2-way (free for ds_write_b32).
+constexpr int FT_WH = 264, FT_WC0 = 72, FT_WC1 = 136, FT_CIN = 68;
 
 struct FwdTailArgs {
   const float* Y7;   // [Mp][ldy] trunk.7 output (ldy 256 in training, 320 in the inference ping-pong)
   const float* xd;   // [M][6] (directions in cols 3..5)
   const float* w;    // packed fp32 parameters
   int64_t off_wh, off_bh, off_wc0, off_bc0, off_wc1, off_bc1;
-  float* HO;                   // [Mp][FT_HO] (training: what the colour backward reads)
+  float *HO, *CIN, *C0;        // [Mp][4] (o3_0..2, sigma_raw), [Mp][64], [Mp][128] (training: what the backward reads)
   float* out;                  // [M][4] rgb_sigma
   int64_t M, Mp;
   int ntiles, ldy;
@@ -70,6 +64,7 @@ __global__ __launch_bounds__(256, 2) void fwd_tail_kernel(FwdTailArgs A) {
   __shared__ __attribute__((aligned(16))) float sWc0[128 * FT_WC0];
   __shared__ __attribute__((aligned(16))) float sWc1[16 * FT_WC1];
   __shared__ __attribute__((aligned(16))) float sB[16 + 128 + 16];
+  __shared__ __attribute__((aligned(16))) float sCIN[FT_ROWS * FT_CIN];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane & 15, g = lane >> 4;
 
@@ -130,8 +125,28 @@ __global__ __launch_bounds__(256, 2) void fwd_tail_kernel(FwdTailArgs A) {
       }
       cin[ch] = make_float4(v[0], v[1], v[2], v[3]);
     }
-    // the head outputs the colour backward rebuilds its input from (O16 cols 4 g .. 4 g + 3 of the lane's row)
-    if (TRAIN) *reinterpret_cast<float4*>(A.HO + m * FT_HO + 4 + 4 * g) = make_float4(o16[0], o16[1], o16[2], o16[3]);
+    if (TRAIN) {  // the canonical CIN row (geo | d | PE | 0) for the backward, staged per wave through LDS
+      float* sr = sCIN + (16 * w + lr) * FT_CIN;
+      const float c0v[4] = {cin[0].x, cin[0].y, cin[0].z, cin[0].w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * g + r >= 1) sr[4 * g + r - 1] = c0v[r];
+      const float c1v[4] = {cin[1].x, cin[1].y, cin[1].z, cin[1].w}, c2v[4] = {cin[2].x, cin[2].y, cin[2].z, cin[2].w};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sr[15 + 4 * g + s] = c1v[s];
+        sr[31 + 4 * g + s] = c2v[s];
+        sr[47 + 4 * g + s] = 0.f;
+      }
+      if (g == 3) sr[63] = 0.f;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads back only its own 16 rows
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = (lane >> 4) + 4 * i, c4 = lane & 15;
+        *reinterpret_cast<float4*>(A.CIN + ((int64_t)t * FT_ROWS + 16 * w + row) * 64 + 4 * c4) =
+            *reinterpret_cast<const float4*>(sCIN + (16 * w + row) * FT_CIN + 4 * c4);
+      }
+    }
     // ---- colour layer 0: C0 = relu(CIN Wc0^T + b), 8 column blocks of 16, K = 48 (3 chunks)
     nerf_f32x4 ac[8];
 #pragma unroll
@@ -153,6 +168,7 @@ __global__ __launch_bounds__(256, 2) void fwd_tail_kernel(FwdTailArgs A) {
       const float* b = sB + 16 + 16 * cb + 4 * g;
       c0[cb] = make_float4(fmaxf(ac[cb][0] + b[0], 0.f), fmaxf(ac[cb][1] + b[1], 0.f), fmaxf(ac[cb][2] + b[2], 0.f),
                            fmaxf(ac[cb][3] + b[3], 0.f));
+      if (TRAIN) *reinterpret_cast<float4*>(A.C0 + m * 128 + 16 * cb + 4 * g) = c0[cb];
     }
     // the next tile's trunk.7 rows, under colour out (issued right after the head MFMAs instead, pinned there: 214 -> 218
     // us per launch, round 4 — not kept)
@@ -170,11 +186,9 @@ __global__ __launch_bounds__(256, 2) void fwd_tail_kernel(FwdTailArgs A) {
     float o3[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) o3[r] = ao[r] + sB[144 + 4 * g + r];
-    // the backward's head-output inputs: the colour pre-activations and sigma_raw lead the HO row
-    if (TRAIN && g == 0) {
-      *reinterpret_cast<float4*>(A.HO + m * FT_HO) = make_float4(o3[0], o3[1], o3[2], sigma_raw);
-      *reinterpret_cast<float4*>(A.HO + m * FT_HO + 20) = make_float4(d[0], d[1], d[2], 0.f);
-    }
+    // the backward's head-output inputs, one 16-B row (round 4; the [Mp][32] O16 / O3 rows, 256 B written and read
+    // back at line granularity for 16 used bytes, are gone): the colour pre-activations and sigma_raw
+    if (TRAIN && g == 0) reinterpret_cast<float4*>(A.HO)[m] = make_float4(o3[0], o3[1], o3[2], sigma_raw);
     if (g == 0 && real) {
       const float sg = expf(fminf(fmaxf(sigma_raw, -EXP_MAX), EXP_MAX));
       reinterpret_cast<float4*>(A.out)[m] = make_float4(sigmoidf_(o3[0]), sigmoidf_(o3[1]), sigmoidf_(o3[2]), sg);

@@ -1,5 +1,5 @@
-// Fused colour-branch backward and head backward of the vanilla MLP (fp32 path, mlp.hip); all arithmetic and the
-// weight-gradient sums are fp32.
+// Fused colour-branch backward of the vanilla MLP (fp32 path, mlp.hip).  The activations C0 / CIN may be read as
+// fp32 or bf16 (TA) and dO16 written as fp32 or bf16 (TD); all arithmetic and the weight-gradient sums are fp32.
 // Measured: fp32 path 28.2 -> 28.0 ms/step (six launches and ~1.7 GB of HBM traffic per step removed); the bf16
 // path keeps its bf16-MFMA chain, which is faster there (8.36 vs 8.74 ms/step with this kernel: one 256-thread
 // workgroup per CU walking 48 tiles is latency-bound at ~11 us per tile; the two-workgroups-per-split version
@@ -8,18 +8,15 @@
 #pragma once
 #include "gemm.hpp"
 #include "mlp_common.hpp"
-#include "mlp_fwd_tail.hpp"
 
 // ------------------------------------------------------------------ fused colour-branch backward
 // One kernel for everything between d_rgb_sigma and dO16 (the gradient of the [sigma | geo] head output):
 // sigmoid' and trunc_exp' (head_out), the colour_out and colour layer-0 weight / bias gradients and the
 // geo-feature input gradient.  Grid = the S row splits of the packed weight-gradient slabs; each
-// workgroup walks its split in 64-row tiles (the next tile's head-output rows are prefetched into registers
+// workgroup walks its split in 64-row tiles (the next tile's C0 / CIN rows are prefetched into registers
 // while the current one is computed), keeps its weight-gradient sums in registers across the tiles and
-// writes them into its slab once.  Per row it reads the forward tail's 96-B HO row and d_rgb_sigma (16 B) and writes
-// one dO16 row.
-//   CIN   = [geo, d, dir PE]                  rebuilt from the HO row (geo, d; PE by the forward's sincosf)
-//   C0    = relu(CIN Wc0^T + b)               recomputed with the forward tail's MFMA sequence: bitwise its values
+// writes them into its slab once.  Per row it reads C0 / CIN / O3 / O16[0] / d_rgb_sigma (~1 KB) and writes
+// one 128-B dO16 row; the unfused chain moved ~2.7 KB per row through six launches.
 //   dO3   = g.rgb * s(1-s)                   (3 columns; VALU)
 //   dWc1 += dO3^T C0, dbc1 += sum dO3        (3 x 128: VALU, thread = output column x row half, in the same pass
 //   dC0   = (dO3 Wc1[:3]) * (C0 > 0)          as dC0; the forward ReLU mask is C0 > 0)
@@ -27,9 +24,8 @@
 //   dgeo  = dC0 Wc0[:, :15]                  (MFMA 16x16x4, wave w -> rows 16w.., Wc0 in registers)
 //   dO16  = [g.sigma * exp(clamp(sigma_raw)), dgeo, 0...]   (stored from the dgeo accumulators)
 // Round 4: the dC0 pass was 4-way LDS bank-conflicted (row-per-lane-group mapping), the dWc0 k-steps 2-way, and dgeo
-// ran on 32x32x2 tiles with 17 of 32 columns unused plus an LDS sum of two contraction halves.  Round 6: CIN (256 B)
-// and C0 (512 B) per row are no longer written by the forward and read back here — the C0 recompute is 96 16x16x4
-// MFMAs per wave and tile, against 1.4 KB per row of HBM traffic between the two launches (mlp_fwd_tail.hpp).
+// ran on 32x32x2 tiles with 17 of 32 columns unused plus an LDS sum of two contraction halves (5 barriers per tile,
+// now 3).
 namespace nerf_mlp {
 // row parts per split of color_bwd / head_bwd: part 0 writes its sums into the split's slab, parts 1 .. TAIL_NQ - 1
 // into rows (q - 1) S + s of partial2, added by reduce_splits2 after the slab terms.  Measured (C2, one box,
@@ -51,23 +47,33 @@ __device__ __forceinline__ void tail_part_rows(int64_t sp, int q, int64_t rps, i
   if (r0 > r1) r0 = r1;
 }
 constexpr int CB_ROWS = 64;
-// LDS pitches (floats).  The CIN tile is stored in the head's column alignment (col 0 = 0 — the forward's sigma_raw
-// slot, whose weight is 0 —, cols 1..63 = canonical CIN cols 0..62, cols 64..71 = 0): the C0 recompute reads it as
-// the forward's B operand (ds_read_b128, pitch / 4 = 2 mod 16: conflict-free, mlp_fwd_tail.hpp), the dWc0 k-steps
-// read canonical col c at c + 1.
-constexpr int CB_C0 = 132, CB_CIN = 72;
+constexpr int CB_C0 = 132, CB_CIN = 68;
 
-static __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restrict__ g, const float* __restrict__ HO,
+// 4 consecutive activations as fp32 (fp32 or bf16 storage) and 4 fp32 values stored as T
+__device__ __forceinline__ float4 tail_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 tail_ld4(const __bf16* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+__device__ __forceinline__ void tail_st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ void tail_st4(__bf16* p, float4 v) {
+  p[0] = (__bf16)v.x; p[1] = (__bf16)v.y; p[2] = (__bf16)v.z; p[3] = (__bf16)v.w;
+}
+
+template <typename TA, typename TD>
+__global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* __restrict__ g, const float* __restrict__ HO,
+                                                        const TA* __restrict__ C0,
+                                                        const TA* __restrict__ CIN,
                                                         const float* __restrict__ Wc0,  // [128][64]
-                                                        const float* __restrict__ bc0,  // [128]
                                                         const float* __restrict__ Wc1,  // [32][128]
-                                                        float* __restrict__ dO16, float* __restrict__ partial,
+                                                        TD* __restrict__ dO16, float* __restrict__ partial,
                                                         int64_t slab, int64_t off_w0, int64_t off_b0,
                                                         int64_t off_w1, int64_t off_b1, int64_t rps, int64_t M,
                                                         int64_t Mp, float* __restrict__ partial2, int64_t cslab,
                                                         int64_t p2base, int ldd) {
-  // dC0 overwrites C0 in place (each element by the thread that read it, so without a barrier between): 53 KB of LDS,
-  // two workgroups per CU, four barriers per tile.  Workgroup TAIL_NQ s + q walks part q of split s; part 0 writes the
+  // dC0 overwrites C0 in place (each element by the thread that read it, so without a barrier between): 52 KB of LDS,
+  // two workgroups per CU, three barriers per tile.  Workgroup TAIL_NQ s + q walks part q of split s; part 0 writes the
   // colour sums into slab s, part q > 0 into row (q - 1) S + s of partial2 (cslab floats: packed offsets p2base ..
   // total of one slab; p2base <= off_w0).  dO16 rows have pitch ldd: 32 (columns 16..31 written as zeros) or 16.
   __shared__ __attribute__((aligned(16))) float s_c0[CB_ROWS * CB_C0];
@@ -81,46 +87,26 @@ static __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* _
   int64_t r0, r1;
   tail_part_rows(sp, q, rps, Mp, CB_ROWS, r0, r1);
 
-  // CIN rebuild: thread (row cr, quarter cq) writes head-aligned cols 16 cq .. 16 cq + 15 of its row; it prefetches
-  // the row's O16 part of HO (quarter 0 uses it) and its direction.  Wave 0 also prefetches the tile's d_rgb_sigma
-  // (M rows: the index is clamped, the value zeroed below for m >= M) and the HO lead (colour pre-activations,
-  // sigma_raw).  r0, r1, rps and the part length are multiples of CB_ROWS (the host rounds rps to 64; Mp is a multiple
-  // of 256), so every row of a tile is < r1 <= Mp and the loads carry no row guard.
-  const int cr = tid >> 2, cq = tid & 3;
-  float4 ph[4], pdir = make_float4(0.f, 0.f, 0.f, 0.f), pg = pdir, po = pdir;
+  // register prefetch of one tile: C0 = 2048 float4 (8 / thread), CIN = 1024 float4 (4 / thread); wave 0 also
+  // prefetches the tile's head outputs: d_rgb_sigma (M rows: the row index is clamped, the value zeroed below for
+  // m >= M) and the HO row (the three colour pre-activations, sigma_raw).
+  float4 pc[8], pi[4], pg = make_float4(0.f, 0.f, 0.f, 0.f), po = pg;
+  // r0, r1, rps and the part length are multiples of CB_ROWS (the host rounds rps to 64; Mp is a multiple of 256),
+  // so every row of a tile is < r1 and the loads carry no row guard (a guarded load became a branch with a
+  // vmcnt(0) drain after it); a uniform tile base + 32-bit lane offsets keeps no 64-bit address per load live
   auto fetch = [&](int64_t t0) {
-    const float* hr = HO + (t0 + cr) * FT_HO;
+    const TA* c0t = C0 + t0 * 128;
+    const TA* cit = CIN + t0 * 64;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) ph[u] = *reinterpret_cast<const float4*>(hr + 4 + 4 * u);
-    pdir = *reinterpret_cast<const float4*>(hr + 20);
+    for (int u = 0; u < 8; ++u) pc[u] = tail_ld4(c0t + (tid + 256 * u) * 4);  // row f >> 5, float4 f & 31
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pi[u] = tail_ld4(cit + (tid + 256 * u) * 4);  // row f >> 4, float4 f & 15
     if (tid < CB_ROWS) {  // wave 0 (uniform branch)
       const int64_t m = t0 + tid, mc = m < M ? m : M - 1;
       pg = reinterpret_cast<const float4*>(g)[mc];
-      po = *reinterpret_cast<const float4*>(HO + m * FT_HO);
+      po = reinterpret_cast<const float4*>(HO)[m];
     }
   };
-
-  // C0 recompute (the forward tail's colour layer 0): wave w computes column blocks 2w, 2w + 1 of all 64 rows; lane
-  // (lr, gk) holds the shifted weight image's rows 16 cb + lr, k = 16 ch + 4 gk .. + 3 (col j <- Wc0 col j - 1, col
-  // 0 = 0), the bias of its output columns, for the whole kernel
-  const int lr = lane & 15, gk = lane >> 4;
-  float4 wf[2][3];
-  float4 b0[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = 16 * (2 * wave + j) + lr;
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int col = 16 * ch + 4 * gk + e;
-        v[e] = col == 0 ? 0.f : Wc0[n * 64 + col - 1];
-      }
-      wf[j][ch] = make_float4(v[0], v[1], v[2], v[3]);
-    }
-    b0[j] = *reinterpret_cast<const float4*>(bc0 + 16 * (2 * wave + j) + 4 * gk);
-  }
 
   // colour_out / dC0 phase: thread (column jw, row half rh); its colour_out weight column lives in registers
   const int jw = tid & 127, rh = tid >> 7;
@@ -139,42 +125,15 @@ static __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* _
   if (r0 < r1) fetch(r0);
   for (int64_t t0 = r0; t0 < r1; t0 += CB_ROWS) {
     __syncthreads();  // previous tile's LDS readers are done
-    {  // ---- the CIN row in the head's alignment (rows >= M all zero, as the forward's colour input).  Thread (row cr,
-      // quarter cq): ONE sincosf per (dimension, band) pair p = 3 cq .. 3 cq + 2 of its row (the same libm call on the
-      // same argument as the forward tail's cin_dir_value, so the same bits; cos -> canonical col 18 + 8 k + l, sin ->
-      // 22 + 8 k + l), geo / d cols 5 cq .. 5 cq + 4 (< 18), and the zero cols 43 + 8 cq .. of the head-aligned
-      // tile; no lane runs another quarter's branch
-      const bool real = t0 + cr < M;
-      const float d[3] = {pdir.x, pdir.y, pdir.z};
-      float* sr = s_cin + cr * CB_CIN;      // head-aligned: canonical col c at c + 1
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int p = 3 * cq + i, k = p >> 2, l = p & 3;
-        float sn, cs;
-        sincosf(d[k] * (float)(1 << l), &sn, &cs);
-        sr[1 + 18 + 8 * k + l] = real ? cs : 0.f;
-        sr[1 + 22 + 8 * k + l] = real ? sn : 0.f;
-      }
-      const float o[16] = {ph[0].x, ph[0].y, ph[0].z, ph[0].w, ph[1].x, ph[1].y, ph[1].z, ph[1].w,
-                           ph[2].x, ph[2].y, ph[2].z, ph[2].w, ph[3].x, ph[3].y, ph[3].z, ph[3].w};
+    for (int u = 0; u < 8; ++u) {
+      const int f = tid + 256 * u;
+      *reinterpret_cast<float4*>(s_c0 + (f >> 5) * CB_C0 + 4 * (f & 31)) = pc[u];
+    }
 #pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        const int c = 5 * cq + i;           // canonical geo 0..14 (O16 col c + 1), d 15..17
-        if (c < 18) {
-          float v = 0.f;
-#pragma unroll
-          for (int e = 0; e < 15; ++e)
-            if (c == e) v = o[e + 1];
-          if (c >= 15) v = d[c - 15];
-          sr[1 + c] = real ? v : 0.f;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {         // head-aligned cols 0 and 43..71 (canonical 42..62 and the padding)
-        const int c = 43 + 8 * cq + i;
-        if (c < CB_CIN) sr[c] = 0.f;
-      }
-      if (cq == 0) sr[0] = 0.f;
+    for (int u = 0; u < 4; ++u) {
+      const int f = tid + 256 * u;
+      *reinterpret_cast<float4*>(s_cin + (f >> 4) * CB_CIN + 4 * (f & 15)) = pi[u];
     }
     if (tid < CB_ROWS) {
       const int64_t m = t0 + tid;
@@ -187,30 +146,6 @@ static __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* _
         ds = pg.w * expf(fminf(fmaxf(po.w, -EXP_MAX), EXP_MAX));
       }
       *reinterpret_cast<float4*>(s_do3 + tid * 4) = make_float4(a, b, c, ds);
-    }
-    __syncthreads();
-    // ---- C0 = relu(CIN Wc0^T + b): per output element the forward tail's k order (ch, then the four k-slots), so
-    // the same fp32 values; wave w -> column blocks 2w, 2w + 1, row blocks rb = 0..3
-#pragma unroll
-    for (int rb = 0; rb < 4; ++rb) {
-      const float* cr_row = s_cin + (16 * rb + lr) * CB_CIN + 4 * gk;
-      float4 cin[3];
-#pragma unroll
-      for (int ch = 0; ch < 3; ++ch) cin[ch] = *reinterpret_cast<const float4*>(cr_row + 16 * ch);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        nerf_f32x4 ac = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) {
-          ac = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[j][ch].x, cin[ch].x, ac, 0, 0, 0);
-          ac = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[j][ch].y, cin[ch].y, ac, 0, 0, 0);
-          ac = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[j][ch].z, cin[ch].z, ac, 0, 0, 0);
-          ac = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[j][ch].w, cin[ch].w, ac, 0, 0, 0);
-        }
-        *reinterpret_cast<float4*>(s_c0 + (16 * rb + lr) * CB_C0 + 16 * (2 * wave + j) + 4 * gk) =
-            make_float4(fmaxf(ac[0] + b0[j].x, 0.f), fmaxf(ac[1] + b0[j].y, 0.f), fmaxf(ac[2] + b0[j].z, 0.f),
-                        fmaxf(ac[3] + b0[j].w, 0.f));
-      }
     }
     __syncthreads();
     if (t0 + CB_ROWS < r1) fetch(t0 + CB_ROWS);  // in flight during this tile's compute
@@ -228,15 +163,15 @@ static __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* _
       s_dc0[r * CB_C0 + jw] = c0 > 0.f ? v : 0.f;
     }
     __syncthreads();
-    // ---- MFMA: dWc0 (wave w -> rows 32w..), bias sums.  k-step st pairs rows r and r + 8 (lane halves); canonical CIN
-    // col c sits at c + 1 of the head-aligned tile
+    // ---- MFMA: dWc0 (wave w -> rows 32w..), bias sums.  k-step st pairs rows r and r + 8 (lane halves): 8 rows apart
+    // the two halves' LDS reads sit 32 banks apart (pitches 132 / 68), conflict-free
 #pragma unroll 16
     for (int st = 0; st < CB_ROWS / 2; ++st) {
       const int row = (st & 7) + 16 * (st >> 3) + 8 * lh;
       const float av = s_dc0[row * CB_C0 + 32 * wave + li];
       bsum0 += av;
-      acc0[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, s_cin[row * CB_CIN + 1 + li], acc0[0], 0, 0, 0);
-      acc0[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, s_cin[row * CB_CIN + 33 + li], acc0[1], 0, 0, 0);
+      acc0[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, s_cin[row * CB_CIN + li], acc0[0], 0, 0, 0);
+      acc0[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, s_cin[row * CB_CIN + 32 + li], acc0[1], 0, 0, 0);
     }
     // ---- dgeo = dC0 Wc0[:, :15] (16x16x4: A lane (row gc, k 32 kg + kk), B lane (k, column gc)), then the dO16 rows
     //      [ds, dgeo, 0...] straight from the accumulator (lane (kg, gc) holds rows 4 kg + v, column gc)
@@ -254,10 +189,10 @@ static __global__ __launch_bounds__(256, 2) void color_bwd_kernel(const float* _
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int r = 16 * wave + 4 * kg + v;
-        float* drow = dO16 + (t0 + r) * ldd;
-        if (gc < 15) drow[gc + 1] = accg[v];
-        else drow[0] = s_do3[r * 4 + 3];
-        if (ldd == 32) drow[16 + gc] = 0.f;
+        TD* drow = dO16 + (t0 + r) * ldd;
+        if (gc < 15) drow[gc + 1] = (TD)accg[v];
+        else drow[0] = (TD)s_do3[r * 4 + 3];
+        if (ldd == 32) drow[16 + gc] = (TD)0.f;
       }
     }
   }
