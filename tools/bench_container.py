@@ -61,9 +61,10 @@ def parse():
                          "device-sized sync-free one (container.py, DESIGN.md §3.8)")
     ap.add_argument("--graph", dest="graph", action="store_true", default=None,
                     help="replay the train step as ONE captured hipGraph (nerf_amd/graph_step.py; world size 1, "
-                         "device-sized render); the default at world size 1")
+                         "device-sized render).  Off by default: measured no faster than eager on this ROCm "
+                         "(DESIGN.md §3.8, profiles/r06/a5, a6)")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
-                    help="launch every kernel of the step from Python (eager)")
+                    help="launch every kernel of the step from Python (eager; the default)")
     ap.add_argument("--no-bucket", action="store_true",
                     help="one all-reduce of the flat gradient in step() instead of per-table buckets started by the "
                          "hash-table backward")
