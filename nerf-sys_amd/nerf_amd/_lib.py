@@ -144,8 +144,14 @@ def lib():
             "nerf_moe_blend_finish": [P, P, I64, P, P],
             "nerf_moe_blend_bwd": [P, I64, P, P, I, I, P, P, P, P, P],
         }
+        ab = "NERF_AMD_LIB" in os.environ  # an A/B build of an older revision may lack the newer entry points
         for name, args in sig.items():
-            fn = getattr(L, name)
+            try:
+                fn = getattr(L, name)
+            except AttributeError:
+                if ab:
+                    continue
+                raise
             fn.argtypes = args
             fn.restype = c_int
         L.nerf_mlp_layout.restype = c_int64
