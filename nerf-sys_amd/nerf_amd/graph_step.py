@@ -4,7 +4,9 @@ The production container step (march -> union -> routin
 -> blend -> packed compositing -> MSE -> backward -> FlatAdam) is ~150 short launches per 4096-ray step; launched one
 by one from Python the GPU idles between them.  With every size kept on the device (the
 "device-sized" render of container.py) the step has no host read, so it can be captured: a replay submits the whole
-step at once.
+step at once.  Measured on this ROCm (profiles/r06/a5, a6): a replay costs the host about what the
+eager launches do and the early steps are GPU-bound, so the container bench keeps eager launches by default
+(``--graph`` opts in).
 
 What a replay cannot take from the host, the step reads from device memory:
   * the ray batch seed and the marching jitter seed: ``seed = base + step * mul`` with ``step`` an int64 counter in HBM
@@ -44,7 +46,6 @@ class GraphedStep:
         self.graph = None
         self.out = None
         self.calls = 0
-        self.pool = None
 
     def __call__(self, step: int) -> torch.Tensor:
         st = torch.cuda.current_stream()
