@@ -15,9 +15,8 @@ Prints ONE JSON line on rank 0 (contract in the task statement), with
   roofline      — the dominant kernel class of the fine net's trunk GEMMs: the class (fwd / dgrad / wgrad)
                   with the largest mean launch time.  Durations are HIP events the library records on the
                   launch stream in --timing-steps (default 3) extra steps AFTER the timed region, run with
-                  every launch alone on the device (the production step overlaps the coarse backward with
-                  the fine forward and the fine weight gradients with its input gradients on three streams,
-                  where a launch's wall time is shared); achieved = algorithmic FLOP per launch / mean.
+                  every launch alone on the device (the production step runs the coarse backward on a second
+                  stream beside the fine backward, --overlap-with; a launch's wall time is shared there); achieved = algorithmic FLOP per launch / mean.
                   With --precision bf16 the MLP is one fused forward launch plus one fused backward launch
                   per trunk layer (HBM-bound): the kernel with the largest total time per step is reported
                   against the HBM peak, with algorithmic bytes per launch (roofline_bf16).
@@ -110,6 +109,8 @@ def parse():
     ap.add_argument("--no-psnr", action="store_true",
                     help="skip the full-image PSNR record (training to --psnr-steps + held-out renders, N = 1 only)")
     ap.add_argument("--no-overlap", action="store_true", help="run the coarse-net backward on the main stream")
+    ap.add_argument("--overlap-with", default="bwd", choices=["fwd", "bwd"],
+                    help="what the side-stream coarse backward runs beside: the fine backward (default) or forward")
     ap.add_argument("--split-wgrad", action="store_true",
                     help="fp32: the fine net's weight-gradient GEMMs on a second stream (nerf_mlp_bwd_2s)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -460,7 +461,7 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_
     torch.manual_seed(0)   # the same initial weights for every precision (the PSNR comparison starts from them)
     coarse, fine = VanillaNeRF().to(dev), VanillaNeRF().to(dev)
     tr = NeRFTrainer(coarse, fine, n_samples=a.samples, n_importance=a.importance, world_size=world, device=dev,
-                     overlap=not a.no_overlap, precision=precision,
+                     overlap=not a.no_overlap, overlap_with=getattr(a, "overlap_with", "bwd"), precision=precision,
                      bf16_flags=a.bf16_flags if precision == "bf16" else 0, split_wgrad=a.split_wgrad,
                      fp32_gemm=fp32_gemm or a.fp32_gemm)
 
@@ -534,7 +535,8 @@ def engine_run(a, dev, rb, world, rank, n_local, precision, barrier, nccl, fp32_
                                             else False)), event_steps=n_ev,
                             event_pass="the timing_steps steps after the timed region, every launch alone (no "
                                        "side-stream coarse backward, fine weight gradients in line)"),
-           "streams": {"coarse_bwd_beside_fine_fwd": tr.overlap, "fine_wgrad_stream": tr.split_wgrad}}
+           "streams": {"coarse_bwd_beside_fine_fwd": tr.overlap and tr.overlap_with == "fwd",
+                       "coarse_bwd_beside_fine_bwd": tr.overlap and tr.overlap_with == "bwd", "fine_wgrad_stream": tr.split_wgrad}}
     if precision == "fp32":
         rec["fp32_gemm"] = tr.fp32_gemm
     peak = BF16_MFMA_PEAK_TFLOPS if precision == "bf16" else FP32_MFMA_PEAK_TFLOPS

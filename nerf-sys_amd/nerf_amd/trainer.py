@@ -63,7 +63,7 @@ class NeRFTrainer:
                  eps: float = 1e-8, weight_decay: float = 0.0, grad_clip: Optional[float] = 1.0,
                  color_space: str = "linear", bg: str = "white", sigma_scale: float = 1.0,
                  world_size: int = 1, device="cuda", overlap: bool = True, precision: str = "fp32",
-                 overlap_with: str = "fwd", bf16_flags: int = 0, split_wgrad: bool = False,
+                 overlap_with: str = "bwd", bf16_flags: int = 0, split_wgrad: bool = False,
                  fp32_gemm: str = "split"):
         L = PackedLayout.get()
         self.L = L
@@ -127,10 +127,14 @@ class NeRFTrainer:
         # 28.1-28.5 ms vs 29.6 ms on one stream; joining the streams before the fine backward instead of at
         # the end of the step serialises it (34.2 ms); stream priorities change nothing.
         self.overlap = bool(overlap) and self.n_nets == 2 and self.device.type == "cuda"
-        # what the coarse backward runs beside: the fine forward (default) or the fine backward (overlap_with="bwd",
-        # A/B runs).  Measured on MI355X: fp32 27.4 (fwd) vs 28.4 ms (bwd); bf16 7.30 vs 7.36 ms (the fused bf16
-        # forward is one persistent launch holding every CU's LDS, so the coarse backward mostly queues behind it
-        # either way).
+        # what the coarse backward runs beside: the fine backward (default) or the fine forward (overlap_with="fwd").
+        # Measured on MI355X with the round-6 kernels, three alternated rounds on one box (profiles/r06/overlap_ab.txt):
+        # bf16 (C3) 4.51-4.53 ms beside the backward vs 4.66-4.67 beside the forward and 4.66-4.68 on one stream; fp32
+        # (C2) 17.10-17.13 vs 17.15 vs 17.32-17.34 ms.  The fused bf16 forward is one persistent launch holding every
+        # CU's LDS: the coarse layer backward beside it got the CUs only between its tiles (1.08 ms for a 0.10 ms
+        # launch) and slowed it by 0.16 ms; beside the fine layer backward (byte-bound, one workgroup pair per split)
+        # the coarse launches fill the CUs' idle issue slots.  (Rounds 2-3, on the earlier kernels, measured the
+        # opposite: fp32 27.4 (fwd) vs 28.4 ms (bwd), bf16 7.30 vs 7.36 ms.)
         if overlap_with not in ("fwd", "bwd"):
             raise ValueError("overlap_with must be 'fwd' or 'bwd'")
         self.overlap_with = overlap_with
@@ -252,7 +256,7 @@ class NeRFTrainer:
                           bf16_flags=self.bf16_flags,
                           fp32_flags=self.fp32_flags)
                 # bucket 1 of the data-parallel exchange: the coarse net's gradient is final here, so its all-reduce
-                # starts now and runs beside the fine net's forward / backward (bucket 2 trails the backward)
+                # starts now and runs beside the rest of the fine net's pass (bucket 2 trails the backward)
                 self._exchange(self.gbuf[:P], ev_box[0], 0)
                 done = torch.cuda.Event()
                 done.record(self._side)

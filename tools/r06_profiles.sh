@@ -11,11 +11,13 @@ for P in fp32 bf16; do
     python3 bench.py --precision $P --steps 20 --warmup 5 --no-cpu-baseline --no-psnr --no-dropin --no-other-precision --no-native-ref --no-ngp --no-container --no-llff --no-sweep \
     > $O/prof_$P.log 2>&1 || { tail -20 $O/prof_$P.log; exit 1; }
   python3 tools/prof_summary.py $O/prof_$P/run_kernel_stats.csv 28 3 > $O/prof_${P}_summary.txt 2>&1
-  python3 tools/step_timeline.py $O/prof_$P/run_kernel_trace.csv > $O/step_${P}.txt 2>&1 || true
+  python3 tools/step_timeline.py $O/prof_$P/run_kernel_trace.csv mid > $O/step_${P}.txt 2>&1 || true
+  python3 tools/step_timeline.py $O/prof_$P/run_kernel_trace.csv last > $O/step_${P}_events.txt 2>&1 || true
   rm -f $O/prof_$P/run_kernel_trace.csv
   echo "prof $P: $(tail -1 $O/prof_$P.log | cut -c1-160)"
 done
 fi
+[ -n "$STOP_AFTER_PROF" ] && exit 0
 export LEG_ARGS="--no-llff --no-sweep"
 PMC_OUT=$O/pmc_fp32 PMC_BENCH_ARGS="--no-dropin --no-other-precision --no-native-ref" bash tools/pmc_traffic.sh > $O/pmc_fp32.txt 2>&1 || { tail -20 $O/pmc_fp32.txt; exit 1; }
 PMC_OUT=$O/pmc_bf16 PMC_PRECISION=bf16fused PMC_BENCH_ARGS="--precision bf16 --no-dropin --no-other-precision" bash tools/pmc_traffic.sh > $O/pmc_bf16.txt 2>&1 || { tail -20 $O/pmc_bf16.txt; exit 1; }
