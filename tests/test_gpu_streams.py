@@ -74,3 +74,38 @@ def test_trainer_split_wgrad_equals_inline(K):
         assert abs(a[0] - b[0]) <= 1e-5 * abs(a[0]), (s, a[0], b[0])
         assert torch.equal(a[1], b[1]), f"step {s}: gradient buffers differ"
         assert torch.equal(a[2], b[2]), f"step {s}: parameters differ"
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_trainer_stream_schedules_equal(K, precision):
+    """Where the coarse backward runs — beside the fine backward (the default since round 6), beside the fine forward,
+    or in line on the main stream (overlap=False) — is scheduling only: the two nets' gradients land in disjoint
+    segments of the flat buffer, so the gradients and post-Adam parameters are bitwise equal over three steps."""
+    from nerf_amd.trainer import NeRFTrainer
+    from nerf_amd.vanilla import VanillaNeRF
+    g = torch.Generator().manual_seed(37)
+    n = 1024
+    o = torch.tensor([0.0, -4.0311, 0.5]).expand(n, 3)
+    d = torch.nn.functional.normalize(torch.randn(n, 3, generator=g) * 0.2 + torch.tensor([0.0, 1.0, -0.12]), dim=-1)
+    rays = torch.cat([o, d, torch.full((n, 1), 2.0), torch.full((n, 1), 6.0)], -1).to(DEV)
+    gt = torch.rand(n, 3, generator=g).to(DEV)
+    us = [torch.rand(n, 64, generator=g).to(DEV) for _ in range(3)]
+    up = [torch.rand(n, 128, generator=g).to(DEV) for _ in range(3)]
+    res = {}
+    for name, kw in (("bwd", {}), ("fwd", {"overlap_with": "fwd"}), ("inline", {"overlap": False})):
+        tr = NeRFTrainer(VanillaNeRF().load_reference_state(O.init_vanilla_params(1)).to(DEV),
+                         VanillaNeRF().load_reference_state(O.init_vanilla_params(2)).to(DEV),
+                         n_samples=64, n_importance=128, precision=precision, **kw)
+        assert tr.overlap == (name != "inline") and (name == "inline" or tr.overlap_with == name)
+        out = []
+        for s in range(3):
+            loss = tr.step(rays, gt, seed=s, u_strat=us[s], u_pdf=up[s])
+            torch.cuda.synchronize()
+            out.append((float(loss.item()), tr.grads.clone(), tr.params.clone()))
+        res[name] = out
+    for name in ("fwd", "inline"):
+        for s in range(3):
+            a, b = res["bwd"][s], res[name][s]
+            assert abs(a[0] - b[0]) <= 1e-5 * abs(a[0]), (name, s, a[0], b[0])  # per-ray atomics in the loss sum
+            assert torch.equal(a[1], b[1]), f"{name} step {s}: gradient buffers differ"
+            assert torch.equal(a[2], b[2]), f"{name} step {s}: parameters differ"

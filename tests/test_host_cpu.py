@@ -95,3 +95,14 @@ def test_engine_refuses_fp16():
     from nerf_amd.vanilla import VanillaNeRF
     with pytest.raises(ValueError, match="fp16"):
         NeRFTrainer(VanillaNeRF(), VanillaNeRF(), device="cpu", precision="fp16")
+
+
+def test_engine_overlap_with_values():
+    """The coarse backward's stream placement: "bwd" (default, beside the fine backward) or "fwd"; anything else is
+    refused.  (On a CPU device there is no side stream: overlap is off.)"""
+    from nerf_amd.trainer import NeRFTrainer
+    from nerf_amd.vanilla import VanillaNeRF
+    tr = NeRFTrainer(VanillaNeRF(), VanillaNeRF(), device="cpu")
+    assert tr.overlap_with == "bwd" and not tr.overlap
+    with pytest.raises(ValueError, match="overlap_with"):
+        NeRFTrainer(VanillaNeRF(), VanillaNeRF(), device="cpu", overlap_with="tail")
