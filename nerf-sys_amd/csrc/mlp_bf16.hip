@@ -354,6 +354,20 @@ int wgradb(const nerf_bf16* G, int ldg, const nerf_bf16* X, int ldx, int tensor_
 // defaults are the fused kernels (mlp_bf16_fused.hpp, mlp_bf16_bwd.hpp); the layered launches are their bitwise
 // references in the tests.
 
+// The fused backward's W_i^T images of trunk layers 1..7 (bf16 [k][n], first 256 input columns; W.WTf) through 32 x 32
+// LDS tiles, coalesced on both sides.  Made by the training FORWARD, with the colour layer-0 fragments the fused tail
+// reads (W.Wf), so that the backward launches no weight preparation of its own: on the two-stream schedule (coarse
+// backward beside the fine backward) each such small launch queued behind the other net's persistent workgroups for
+// ~90 us of the fine chain (profiles/r06/a17/step_bf16.txt).  The backward's weights are the forward's (the
+// workspace holds that forward's activations), so the images are this call's.
+void bwd_weight_images(const float* w, const WSB& W, hipStream_t st) {
+  const Layout& L = layout();
+  TJobsB jobs{};
+  for (int i = 1; i < 8; ++i)
+    jobs.j[i - 1] = TJobB{w + L.off[2 * i], W.WTf + (int64_t)(i - 1) * nerf_bwd::WT_LAYER, 256, 256, KPAD[i]};
+  transpose_bf16_kernel<<<dim3(8, 8, 7), 256, 0, st>>>(jobs);
+}
+
 int fused_forward(const float* w, const float* x_d, int64_t M, float* rgb_sigma, const WSB& W, int training,
                   bool layered_bwd, hipEvent_t* ev, hipStream_t st) {
   using namespace nerf_fused;
@@ -375,6 +389,7 @@ int fused_forward(const float* w, const float* x_d, int64_t M, float* rgb_sigma,
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
   }
   frag_pack_kernel<<<(unsigned)nerf_cdiv(T.off[FT] / 8, 256), 256, 0, st>>>(w, W.Wf, T);
+  if (training) bwd_weight_images(w, W, st);  // (also beside a layered backward's masks: either backward may follow)
   FusedArgs A{};  // (the io waves encode x_d themselves: io_encode, no pe_prefill_bf16_kernel launch)
   A.xd = x_d;
   A.wf = W.Wf;
@@ -487,10 +502,9 @@ int fused_backward(const float* w, int64_t M, const float* d_rgb_sigma, float* d
   const int64_t Mp = W.Mp;
   if (W.rps % nerf_bwd::TR) return NERF_E_ARG;
   const int S8 = (W.S + 7) / 8 * 8;
-  // the fused tail recomputes C0 with the forward's colour layer-0 fragments: packed here too (a few us), so they are
-  // this call's weights whichever forward (fused or layered) filled the workspace
+  // the fused tail recomputes C0 with the forward's colour layer-0 fragments (W.Wf) and the layers read the W_i^T
+  // images (W.WTf): both made by the training forward, fused or layered (bwd_weight_images)
   const nerf_fused::FragTab FT_ = nerf_fused::frag_tab();
-  nerf_fused::frag_pack_kernel<<<(unsigned)nerf_cdiv(FT_.off[nerf_fused::FT] / 8, 256), 256, 0, st>>>(w, W.Wf, FT_);
   nerf_tail::TailArgs T{};
   T.w = w; T.g = d_rgb_sigma; T.HO = W.HO; T.Y7 = W.Y[7]; T.CIN = W.CIN;
   T.wfc0 = W.Wf + FT_.off[9];
@@ -503,11 +517,6 @@ int fused_backward(const float* w, int64_t M, const float* d_rgb_sigma, float* d
   if (ev) (void)hipEventRecord(ev[3], st);
   nerf_bf16* dcur = W.dA;
   nerf_bf16* dnext = W.dB;
-  {  // W_i^T images (bf16 [k][n], first 256 input columns) through 32 x 32 LDS tiles: coalesced on both sides
-    TJobsB jobs{};
-    for (int i = 1; i < 8; ++i) jobs.j[i - 1] = TJobB{w + L.off[2 * i], W.WTf + (int64_t)(i - 1) * nerf_bwd::WT_LAYER, 256, 256, KPAD[i]};
-    transpose_bf16_kernel<<<dim3(8, 8, 7), 256, 0, st>>>(jobs);
-  }
   for (int i = 7; i >= 1; --i) {
     nerf_bwd::LayerArgs A{};
     A.G = dcur;
@@ -589,6 +598,11 @@ extern "C" int NERF_H16_FN(nerf_mlp_fwd)(const float* w, const float* x_d, int64
                              128, 64, st)));
   TRY((ntb<EPI_BIAS, 0>(W.C0, 128, Wb(20), 128, Bias(21), W.O3, 32, nullptr, nullptr, Mp, 32, 128, st)));
   head_out_b_kernel<<<(unsigned)nerf_cdiv(M, 256), 256, 0, st>>>(W.O3, W.O16, M, rgb_sigma, training ? W.HO : nullptr);
+  if (training) {  // the fused backward's weight images (bwd_weight_images): either backward may follow
+    const nerf_fused::FragTab T = nerf_fused::frag_tab();
+    nerf_fused::frag_pack_kernel<<<(unsigned)nerf_cdiv(T.off[nerf_fused::FT] / 8, 256), 256, 0, st>>>(w, W.Wf, T);
+    bwd_weight_images(w, W, st);
+  }
   return nerf_launch_status();
 }
 
