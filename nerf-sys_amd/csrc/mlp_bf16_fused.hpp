@@ -578,7 +578,12 @@ __device__ __forceinline__ void io_role(const FusedArgs& A, nerf_bf16* Hs, nerf_
         cin.store(Es, EP, j, lane);
         if (next) io_encode<true>(enc, A.xd, A.M, m0 + (int64_t)G * BMF, j, lane, A.X3E);
       }
+#ifdef NERF_EXP_ODD_NOSTORE
+      // probe of the odd-layer recompute: X1, X3, X5, X7 (epilogues k = 0, 2, 4, 6) not saved
+      if (TRAIN && (k & 1)) {
+#else
       if (TRAIN) {
+#endif
         nerf_bf16* Y = (k == 3) ? A.X3E : A.Y + (int64_t)(k < 3 ? k : k - 1) * Mp * 256;
         io_copy<256, MASKS>(Hs + (k & 1) * BMF * HP, HP, Y, k == 3 ? 320 : 256, m0, MASKS ? A.MB + (int64_t)k * Mp * 8 : nullptr, j,
                             lane);

@@ -1,6 +1,6 @@
 #!/bin/bash
-# A/B of the engine step between ab/$A.so and the in-tree library (alternated), plus named tests first.
-#   A=pre_pe PREC=bf16 TESTS="tests/x.py ..." tools/r06_ab.sh OUTDIR
+# A/B of the engine step between ab/$A.so (A may list several names) and the in-tree library (alternated), plus named
+# tests first.   A=pre_pe PREC=bf16 TESTS="tests/x.py ..." tools/r06_ab.sh OUTDIR
 set -o pipefail
 cd "$(dirname "$0")/.."
 O=gpurun_out/r06/$1; mkdir -p $O; export TMPDIR=/tmp
@@ -9,7 +9,7 @@ if [ -n "$TESTS" ]; then
   tail -1 $O/pytest_ab.log
 fi
 ARGS="--precision ${PREC:-bf16} --steps 30 --warmup 5 --no-cpu-baseline --no-psnr --no-dropin --no-other-precision --no-native-ref --no-ngp --no-container --no-llff --no-sweep"
-for r in 1 2 3; do
+for r in $(seq 1 ${ROUNDS:-3}); do
   for v in $A new; do
     if [ $v = new ]; then L=""; else L="NERF_AMD_LIB=ab/$v.so"; fi
     env $L timeout -k 10 200 python bench.py $ARGS > $O/ab_${v}_$r.json 2> $O/ab_${v}_$r.err || { tail -20 $O/ab_${v}_$r.err; exit 1; }
