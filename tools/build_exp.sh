@@ -19,5 +19,7 @@ for f in $SRC/*.hip; do
 done
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mllvm -disable-promote-alloca-to-lds -DNERF_F16=1 $2 -c $SRC/mlp_bf16.hip -o /tmp/exp_$1/mlp_f16.o &
 for j in $(jobs -p); do wait $j; done
+echo "extern \"C\" const char* nerf_version(void) { return \"nerf_amd 0.2 gfx950 src=exp-$1\"; }" > /tmp/exp_$1/version.cpp
+g++ -O2 -fPIC -c /tmp/exp_$1/version.cpp -o /tmp/exp_$1/version.o
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 /tmp/exp_$1/*.o -o ../exp/$1.so
 echo built exp/$1.so
